@@ -1,0 +1,458 @@
+// Training/eval BatchNorm2d with fused activation and residual on NHWC bf16 activations.
+//
+// Replaces cuDNN BN + F.relu + the in-place residual add of the reference blocks
+// (models/resnet.py:47-51 `relu(bn2(conv2(out)) + shortcut(x))`,
+// efficientnet.py:96-103 swish(bn(...)), mobilenetv2.py:33-36).
+//
+// Forward:  stats partials (from the conv epilogue, or bn_stats_kernel for a bare tensor)
+//           -> colsum (stage-1 fold) -> bn_finalize (mean/invstd/scale/shift + running stats)
+//           -> bn_apply: out = act(y*scale + shift [+ res | + y2*scale2 + shift2]).
+// Backward: bn_bwd_reduce (sum dz, sum dz*xhat [, sum dz*xhat2]) -> colsum -> bn_bwd_finalize
+//           (dgamma, dbeta, per-channel affine coefficients) -> bn_bwd_apply
+//           dy = a*dz + b*y + d  (dz = dout * act'(z), the residual gradient is dz itself).
+// Every reduction is a deterministic slab fold (no float atomics).
+#include "common.h"
+
+namespace pca {
+
+// Row-parallel geometry for an [M][C] NHWC matrix: TPR threads cover a row's granules
+// (VEC channels each), RPP rows are processed per pass by one 256-thread block.
+struct RowPar {
+  int C, G, TPR, RPP;
+};
+
+static inline RowPar make_rowpar(int C, int vec) {
+  RowPar r;
+  r.C = C;
+  r.G = (C + vec - 1) / vec;
+  r.TPR = r.G < 256 ? r.G : 256;
+  r.RPP = 256 / r.TPR;
+  return r;
+}
+
+template <int VEC>
+__device__ __forceinline__ void load_vec(const bf16* p, float* f) {
+  if constexpr (VEC == 8) {
+    unpack8(*reinterpret_cast<const uint4*>(p), f);
+  } else {
+    f[0] = bf2f(*p);
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(bf16* p, const float* f) {
+  if constexpr (VEC == 8) {
+    *reinterpret_cast<uint4*>(p) = pack8(f);
+  } else {
+    *p = f2bf(f[0]);
+  }
+}
+
+// ---- per-channel sum / sumsq partials of a bare tensor: partial[P][2][C] ----
+template <int VEC>
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ x, int M,
+                                                       RowPar rp, int rows_per_block,
+                                                       float* __restrict__ partial) {
+  __shared__ float red[256 * VEC * 2];
+  const int t = threadIdx.x;
+  const int gx = t % rp.TPR, ry = t / rp.TPR;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  for (int gbase = 0; gbase < rp.G; gbase += rp.TPR) {
+    const int gi = gbase + gx;
+    float s[VEC], q[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) s[v] = q[v] = 0.f;
+    if (ry < rp.RPP && gi < rp.G) {
+      for (int r = r0 + ry; r < r1; r += rp.RPP) {
+        float f[VEC];
+        load_vec<VEC>(x + (size_t)r * rp.C + gi * VEC, f);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          s[v] += f[v];
+          q[v] += f[v] * f[v];
+        }
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      red[(t * VEC + v) * 2] = s[v];
+      red[(t * VEC + v) * 2 + 1] = q[v];
+    }
+    __syncthreads();
+    if (ry == 0 && gi < rp.G) {
+      for (int k = 1; k < rp.RPP; ++k) {
+        const int tt = k * rp.TPR + gx;
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          s[v] += red[(tt * VEC + v) * 2];
+          q[v] += red[(tt * VEC + v) * 2 + 1];
+        }
+      }
+      float* prow = partial + (size_t)blockIdx.x * 2 * rp.C;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        const int c = gi * VEC + v;
+        if (c < rp.C) {
+          prow[c] = s[v];
+          prow[rp.C + c] = q[v];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- stage-1 fold: in[R][L] -> out[R2][L], out row j sums rows [j*chunk, (j+1)*chunk) ----
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ in, int R, int L,
+                                                     int chunk, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= L) return;
+  const int r0 = blockIdx.y * chunk, r1 = min(R, r0 + chunk);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += in[(size_t)r * L + c];
+  out[(size_t)blockIdx.y * L + c] = s;
+}
+
+// ---- forward finalize: stat[R][2][C] -> aux[4][C] = {mean, invstd, scale, shift} ----
+__global__ void bn_finalize_kernel(const float* __restrict__ stat, int R, int C, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ rmean, float* __restrict__ rvar,
+                                   int64_t* __restrict__ nbt, float momentum, float eps,
+                                   int training, int update_running, float* __restrict__ aux) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) nbt[0] += 1;
+  if (c >= C) return;
+  float mean, var;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < R; ++r) {
+      s += stat[(size_t)r * 2 * C + c];
+      q += stat[(size_t)r * 2 * C + C + c];
+    }
+    const double m = s / count;
+    double v = q / count - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+    if (update_running) {
+      const double unb = count > 1.0 ? v * count / (count - 1.0) : v;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  const float invstd = rsqrtf(var + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  aux[c] = mean;
+  aux[C + c] = invstd;
+  aux[2 * C + c] = g * invstd;
+  aux[3 * C + c] = b - mean * g * invstd;
+}
+
+// ---- apply: out = act(y*scale + shift [+ res] [+ y2*scale2 + shift2]) ----
+template <int VEC>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ y,
+                                                       const float* __restrict__ aux, int C,
+                                                       size_t total, const bf16* __restrict__ res,
+                                                       const bf16* __restrict__ y2,
+                                                       const float* __restrict__ aux2, int act,
+                                                       bf16* __restrict__ out) {
+  const size_t nvec = total / VEC;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 256) {
+    const size_t e = i * VEC;
+    const int c0 = (int)(e % C);
+    float f[VEC];
+    load_vec<VEC>(y + e, f);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) f[v] = f[v] * aux[2 * C + c0 + v] + aux[3 * C + c0 + v];
+    if (res) {
+      float r[VEC];
+      load_vec<VEC>(res + e, r);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) f[v] += r[v];
+    }
+    if (y2) {
+      float r[VEC];
+      load_vec<VEC>(y2 + e, r);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) f[v] += r[v] * aux2[2 * C + c0 + v] + aux2[3 * C + c0 + v];
+    }
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) f[v] = apply_act(f[v], act);
+    store_vec<VEC>(out + e, f);
+  }
+}
+
+// dz from the incoming gradient: relu uses the saved output as mask; swish/sigmoid recompute z.
+template <int VEC>
+__device__ __forceinline__ void compute_dz(const bf16* dout, const bf16* out, const bf16* y,
+                                           const float* aux, int C, int c0, size_t e, int act,
+                                           float* dz) {
+  load_vec<VEC>(dout + e, dz);
+  if (act == ACT_RELU) {
+    float o[VEC];
+    load_vec<VEC>(out + e, o);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) dz[v] = o[v] > 0.f ? dz[v] : 0.f;
+  } else if (act != ACT_NONE) {
+    float yy[VEC];
+    load_vec<VEC>(y + e, yy);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const float z = yy[v] * aux[2 * C + c0 + v] + aux[3 * C + c0 + v];
+      dz[v] *= act_grad(z, act);
+    }
+  }
+}
+
+// ---- backward reduce: partial[P][NS][C] with sums of dz, dz*xhat, (dz*xhat2) ----
+template <int VEC, int NS>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const bf16* __restrict__ dout, const bf16* __restrict__ out, const bf16* __restrict__ y,
+    const float* __restrict__ aux, const bf16* __restrict__ y2, const float* __restrict__ aux2,
+    int act, int M, RowPar rp, int rows_per_block, float* __restrict__ partial) {
+  __shared__ float red[256 * VEC * NS];
+  const int t = threadIdx.x;
+  const int gx = t % rp.TPR, ry = t / rp.TPR;
+  const int C = rp.C;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  for (int gbase = 0; gbase < rp.G; gbase += rp.TPR) {
+    const int gi = gbase + gx;
+    const int c0 = gi * VEC;
+    float acc[NS][VEC];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[k][v] = 0.f;
+    if (ry < rp.RPP && gi < rp.G) {
+      float mean[VEC], istd[VEC], mean2[VEC], istd2[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        mean[v] = aux[c0 + v];
+        istd[v] = aux[C + c0 + v];
+        if (NS == 3) {
+          mean2[v] = aux2[c0 + v];
+          istd2[v] = aux2[C + c0 + v];
+        }
+      }
+      for (int r = r0 + ry; r < r1; r += rp.RPP) {
+        const size_t e = (size_t)r * C + c0;
+        float dz[VEC], yy[VEC];
+        compute_dz<VEC>(dout, out, y, aux, C, c0, e, act, dz);
+        load_vec<VEC>(y + e, yy);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          acc[0][v] += dz[v];
+          acc[1][v] += dz[v] * (yy[v] - mean[v]) * istd[v];
+        }
+        if constexpr (NS == 3) {
+          float y2v[VEC];
+          load_vec<VEC>(y2 + e, y2v);
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[2][v] += dz[v] * (y2v[v] - mean2[v]) * istd2[v];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) red[(t * VEC + v) * NS + k] = acc[k][v];
+    __syncthreads();
+    if (ry == 0 && gi < rp.G) {
+      for (int j = 1; j < rp.RPP; ++j) {
+        const int tt = j * rp.TPR + gx;
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[k][v] += red[(tt * VEC + v) * NS + k];
+      }
+      float* prow = partial + (size_t)blockIdx.x * NS * C;
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          const int c = c0 + v;
+          if (c < C) prow[k * C + c] = acc[k][v];
+        }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- backward finalize: stat[R][NS][C] -> dgamma/dbeta (+ second BN) and coef[NS>2?6:3][C] ----
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ stat, int R, int NS, int C,
+                                       float count, const float* __restrict__ aux,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ aux2,
+                                       const float* __restrict__ gamma2, int training,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ dgamma2, float* __restrict__ dbeta2,
+                                       float* __restrict__ coef, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s[3] = {0.f, 0.f, 0.f};
+  for (int r = 0; r < R; ++r)
+    for (int k = 0; k < NS; ++k) s[k] += stat[((size_t)r * NS + k) * C + c];
+  const float db = s[0];
+  for (int b = 0; b < (NS == 3 ? 2 : 1); ++b) {
+    const float* ax = b == 0 ? aux : aux2;
+    const float* gm = b == 0 ? gamma : gamma2;
+    const float dg = s[1 + b];
+    const float mean = ax[c], istd = ax[C + c];
+    const float g = gm ? gm[c] : 1.f;
+    float A, Bc, D;
+    if (training) {
+      A = g * istd;
+      Bc = -g * istd * istd * dg / count;
+      D = -g * istd * db / count + g * istd * istd * mean * dg / count;
+    } else {
+      A = g * istd;
+      Bc = 0.f;
+      D = 0.f;
+    }
+    float* cf = coef + (size_t)b * 3 * C;
+    cf[c] = A;
+    cf[C + c] = Bc;
+    cf[2 * C + c] = D;
+    float* dgo = b == 0 ? dgamma : dgamma2;
+    float* dbo = b == 0 ? dbeta : dbeta2;
+    if (dgo) dgo[c] = accumulate ? dgo[c] + dg : dg;
+    if (dbo) dbo[c] = accumulate ? dbo[c] + db : db;
+  }
+}
+
+// ---- backward apply: dy = a*dz + b*y + d ; dres = dz ; dy2 = a2*dz + b2*y2 + d2 ----
+template <int VEC>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const bf16* __restrict__ dout, const bf16* __restrict__ out, const bf16* __restrict__ y,
+    const float* __restrict__ aux, const float* __restrict__ coef, int act, int C, size_t total,
+    bf16* __restrict__ dy, bf16* __restrict__ dres, const bf16* __restrict__ y2,
+    bf16* __restrict__ dy2) {
+  const size_t nvec = total / VEC;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 256) {
+    const size_t e = i * VEC;
+    const int c0 = (int)(e % C);
+    float dz[VEC], yy[VEC], o[VEC];
+    compute_dz<VEC>(dout, out, y, aux, C, c0, e, act, dz);
+    load_vec<VEC>(y + e, yy);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) o[v] = coef[c0 + v] * dz[v] + coef[C + c0 + v] * yy[v] + coef[2 * C + c0 + v];
+    store_vec<VEC>(dy + e, o);
+    if (dres) store_vec<VEC>(dres + e, dz);
+    if (dy2) {
+      load_vec<VEC>(y2 + e, yy);
+      const float* cf = coef + 3 * C;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) o[v] = cf[c0 + v] * dz[v] + cf[C + c0 + v] * yy[v] + cf[2 * C + c0 + v];
+      store_vec<VEC>(dy2 + e, o);
+    }
+  }
+}
+
+// =========================================== host ========================================
+
+static int grid_for(size_t nvec) {
+  size_t b = (nvec + 255) / 256;
+  return (int)(b < 4096 ? (b ? b : 1) : 4096);
+}
+
+int bn_row_blocks(int M, int C) {
+  const int vec = (C % 8 == 0) ? 8 : 1;
+  RowPar rp = make_rowpar(C, vec);
+  int P = cdiv(M, rp.RPP * 8);
+  if (P > 1024) P = 1024;
+  if (P < 1) P = 1;
+  return P;
+}
+
+void bn_stats_launch(const bf16* x, int M, int C, float* partial, int P, hipStream_t st) {
+  const int rows = cdiv(M, P);
+  if (C % 8 == 0) {
+    RowPar rp = make_rowpar(C, 8);
+    hipLaunchKernelGGL(bn_stats_kernel<8>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial);
+  } else {
+    RowPar rp = make_rowpar(C, 1);
+    hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial);
+  }
+}
+
+// Fold R rows of width L down to <= 64 rows (stage 1); returns rows in the output buffer.
+int colsum_launch(const float* in, int R, int L, float* out, hipStream_t st) {
+  if (R <= 64) return 0;
+  const int R2 = 64;
+  const int chunk = cdiv(R, R2);
+  const int r2 = cdiv(R, chunk);
+  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(L, 256), r2), dim3(256), 0, st, in, R, L, chunk, out);
+  return r2;
+}
+
+void bn_finalize_launch(const float* stat, int R, int C, double count, const float* gamma,
+                        const float* beta, float* rmean, float* rvar, int64_t* nbt,
+                        float momentum, float eps, int training, int update_running, float* aux,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, stat, R, C, count,
+                     gamma, beta, rmean, rvar, nbt, momentum, eps, training, update_running, aux);
+}
+
+void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const bf16* res,
+                     const bf16* y2, const float* aux2, int act, bf16* out, hipStream_t st) {
+  if (C % 8 == 0) {
+    hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, y, aux, C,
+                       total, res, y2, aux2, act, out);
+  } else {
+    hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(total)), dim3(256), 0, st, y, aux, C,
+                       total, res, y2, aux2, act, out);
+  }
+}
+
+void bn_bwd_reduce_launch(const bf16* dout, const bf16* out, const bf16* y, const float* aux,
+                          const bf16* y2, const float* aux2, int act, int M, int C,
+                          float* partial, int P, hipStream_t st) {
+  const int rows = cdiv(M, P);
+  if (C % 8 == 0) {
+    RowPar rp = make_rowpar(C, 8);
+    if (y2)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<8, 3>), dim3(P), dim3(256), 0, st, dout, out, y, aux,
+                         y2, aux2, act, M, rp, rows, partial);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<8, 2>), dim3(P), dim3(256), 0, st, dout, out, y, aux,
+                         y2, aux2, act, M, rp, rows, partial);
+  } else {
+    RowPar rp = make_rowpar(C, 1);
+    if (y2)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, 3>), dim3(P), dim3(256), 0, st, dout, out, y, aux,
+                         y2, aux2, act, M, rp, rows, partial);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, 2>), dim3(P), dim3(256), 0, st, dout, out, y, aux,
+                         y2, aux2, act, M, rp, rows, partial);
+  }
+}
+
+void bn_bwd_finalize_launch(const float* stat, int R, int NS, int C, float count,
+                            const float* aux, const float* gamma, const float* aux2,
+                            const float* gamma2, int training, float* dgamma, float* dbeta,
+                            float* dgamma2, float* dbeta2, float* coef, int accumulate,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, stat, R, NS, C,
+                     count, aux, gamma, aux2, gamma2, training, dgamma, dbeta, dgamma2, dbeta2,
+                     coef, accumulate);
+}
+
+void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const bf16* y, const float* aux,
+                         const float* coef, int act, int C, size_t total, bf16* dy, bf16* dres,
+                         const bf16* y2, bf16* dy2, hipStream_t st) {
+  if (C % 8 == 0) {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, dout,
+                       out, y, aux, coef, act, C, total, dy, dres, y2, dy2);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(grid_for(total)), dim3(256), 0, st, dout, out,
+                       y, aux, coef, act, C, total, dy, dres, y2, dy2);
+  }
+}
+
+}  // namespace pca

@@ -1,0 +1,622 @@
+// Python bindings of the gfx950 kernel library (module pytorch_cifar_amd._C).
+//
+// Every entry point validates dtype/layout/shape on the host before launching (a mis-shaped
+// launch of a hand-written kernel can fault the whole GPU), allocates outputs through the
+// PyTorch caching allocator and enqueues on the current HIP stream, so all ops are
+// hipGraph-capturable (no host syncs, no hipMalloc inside).
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <torch/extension.h>
+
+#include <vector>
+
+typedef __bf16 bf16;
+
+namespace pca {
+// conv_mfma.hip
+void conv_fwd_launch(const bf16*, const bf16*, const float*, bf16*, float*, int, int, int, int, int, int, int,
+                     int, int, int, int, int, hipStream_t);
+int conv_fwd_bm();
+void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int, int, int, int,
+                       int, int, int, int, hipStream_t);
+void conv_wgrad_launch(const bf16*, const bf16*, float*, int, int, int, int, int, int, int, int,
+                       int, int, int, int, hipStream_t);
+// batchnorm.hip
+int bn_row_blocks(int M, int C);
+void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t);
+int colsum_launch(const float*, int, int, float*, hipStream_t);
+void bn_finalize_launch(const float*, int, int, double, const float*, const float*, float*, float*,
+                        int64_t*, float, float, int, int, float*, hipStream_t);
+void bn_apply_launch(const bf16*, const float*, int, size_t, const bf16*, const bf16*,
+                     const float*, int, bf16*, hipStream_t);
+void bn_bwd_reduce_launch(const bf16*, const bf16*, const bf16*, const float*, const bf16*,
+                          const float*, int, int, int, float*, int, hipStream_t);
+void bn_bwd_finalize_launch(const float*, int, int, int, float, const float*, const float*,
+                            const float*, const float*, int, float*, float*, float*, float*,
+                            float*, int, hipStream_t);
+void bn_bwd_apply_launch(const bf16*, const bf16*, const bf16*, const float*, const float*, int,
+                         int, size_t, bf16*, bf16*, const bf16*, bf16*, hipStream_t);
+// misc.hip
+void nchw_to_nhwc_launch(const float*, int, int, int, int, bf16*, hipStream_t);
+void nhwc_to_nchw_launch(const bf16*, int, int, int, int, float*, hipStream_t);
+void augment_launch(const uint8_t*, const int64_t*, const int32_t*, int, int, int, int,
+                    const float*, const float*, bf16*, hipStream_t);
+void gap_fwd_launch(const bf16*, int, int, int, float*, hipStream_t);
+void gap_bwd_launch(const float*, int, int, int, bf16*, hipStream_t);
+void avgpool_fwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, hipStream_t);
+void avgpool_bwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, hipStream_t);
+void maxpool_fwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, uint8_t*,
+                        hipStream_t);
+void maxpool_bwd_launch(const bf16*, const uint8_t*, int, int, int, int, int, int, int, int, int,
+                        bf16*, hipStream_t);
+void ce_fused_launch(const float*, const int64_t*, int, int, float*, float*, double*, hipStream_t);
+void scale_by_scalar_launch(const float*, const float*, size_t, float*, hipStream_t);
+void sgd_launch(const int64_t*, int, float* const*, const float* const*, float* const*,
+                bf16* const*, const float*, float, float, float, float, int, int, hipStream_t);
+void se_scale_fwd_launch(const bf16*, const float*, int, int, int, bf16*, hipStream_t);
+void se_scale_bwd_launch(const bf16*, const bf16*, const float*, int, int, int, bf16*, float*,
+                         hipStream_t);
+void act_fwd_launch(const bf16*, size_t, int, bf16*, hipStream_t);
+void act_bwd_launch(const bf16*, const bf16*, size_t, int, bf16*, hipStream_t);
+void add_act_launch(const bf16*, const bf16*, size_t, int, bf16*, hipStream_t);
+void weight_prep_launch(const float*, int, int, int, int, bf16*, bf16*, hipStream_t);
+// dwconv.hip
+void dw_fwd_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int, int, int,
+                   bf16*, hipStream_t);
+void dw_dgrad_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int, int,
+                     int, bf16*, hipStream_t);
+int dw_wgrad_partials(int, int, int);
+void dw_wgrad_launch(const bf16*, const bf16*, int, int, int, int, int, int, int, int, int, int,
+                     int, float*, int, float*, float*, hipStream_t);
+// conv_direct.hip
+void direct_fwd_launch(const bf16*, const float*, const float*, int, int, int, int, int, int, int,
+                       int, int, int, int, int, bf16*, hipStream_t);
+void direct_dgrad_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int,
+                         int, int, int, bf16*, hipStream_t);
+int direct_wgrad_splits(int, int, int, int);
+void direct_wgrad_launch(const bf16*, const bf16*, int, int, int, int, int, int, int, int, int,
+                         int, int, int, int, float*, int, float*, hipStream_t);
+// comm.cpp
+void register_comm(py::module& m);
+}  // namespace pca
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+template <typename T>
+T* ptr(const Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+template <typename T>
+T* optr(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void check_bf16(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous (NHWC)");
+}
+void check_f32(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be fp32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
+
+// ------------------------------------------------------------------------------ conv
+std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<Tensor>& bias,
+                             int stride, int pad, int groups, bool want_stats) {
+  check_bf16(x, "x");
+  check_bf16(wb, "weight");
+  TORCH_CHECK(x.dim() == 4 && wb.dim() == 4, "conv_fwd expects x[N,H,W,C], w[Cout,KH,KW,Cin/G]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  const int Cout = wb.size(0), KH = wb.size(1), KW = wb.size(2), Cg = wb.size(3);
+  TORCH_CHECK(groups >= 1 && Cin % groups == 0 && Cout % groups == 0, "bad groups");
+  TORCH_CHECK(Cg == Cin / groups, "weight Cin/G mismatch");
+  TORCH_CHECK(Cg % 8 == 0 && (Cout / groups) % 8 == 0,
+              "MFMA conv path needs Cin/G and Cout/G multiples of 8");
+  const int Ho = out_dim(H, KH, stride, pad), Wo = out_dim(W, KW, stride, pad);
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
+  auto y = at::empty({N, Ho, Wo, Cout}, x.options());
+  Tensor stats;
+  if (want_stats) {
+    const int gm = (N * Ho * Wo + pca::conv_fwd_bm() - 1) / pca::conv_fwd_bm();
+    stats = at::empty({gm, 2, Cout}, x.options().dtype(at::kFloat));
+  }
+  if (bias.has_value() && bias->defined()) {
+    check_f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() == Cout, "bias size");
+  }
+  pca::conv_fwd_launch(ptr<bf16>(x), ptr<bf16>(wb), optr<float>(bias), ptr<bf16>(y),
+                       want_stats ? ptr<float>(stats) : nullptr, N, H, W, Cin, Cout, KH, KW,
+                       stride, pad, groups, Ho, Wo, cur_stream());
+  return {y, stats};
+}
+
+Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, int pad,
+                  int groups) {
+  check_bf16(dy, "dy");
+  check_bf16(wt, "wt");
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
+  const int Cin = wt.size(0), KH = wt.size(1), KW = wt.size(2), Cog = wt.size(3);
+  TORCH_CHECK(Cog * groups == Cout, "wt Cout/G mismatch");
+  TORCH_CHECK(Cog % 8 == 0 && (Cin / groups) % 8 == 0, "MFMA dgrad needs multiples of 8");
+  TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo,
+              "dgrad geometry mismatch");
+  auto dx = at::empty({N, H, W, Cin}, dy.options());
+  pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dx), N, H, W, Cin, Cout, KH, KW,
+                         stride, pad, groups, Ho, Wo, cur_stream());
+  return dx;
+}
+
+// dw: fp32 [Cout, KH, KW, Cin/G] (zeroed here)
+Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride, int pad,
+                  int groups, const optional<Tensor>& out) {
+  check_bf16(x, "x");
+  check_bf16(dy, "dy");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
+  TORCH_CHECK(dy.size(0) == N, "batch mismatch");
+  TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo,
+              "wgrad geometry mismatch");
+  TORCH_CHECK((Cin / groups) % 8 == 0 && (Cout / groups) % 8 == 0, "MFMA wgrad needs multiples of 8");
+  // fp32 atomics accumulate into `out` (a .grad buffer in physical order) when given.
+  Tensor dw;
+  if (out.has_value() && out->defined()) {
+    check_f32(*out, "dw out");
+    TORCH_CHECK(out->dim() == 4 && out->size(0) == Cout && out->size(1) == KH &&
+                    out->size(2) == KW && out->size(3) == Cin / groups,
+                "dw out shape");
+    dw = *out;
+  } else {
+    dw = at::zeros({Cout, KH, KW, Cin / groups}, x.options().dtype(at::kFloat));
+  }
+  pca::conv_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), ptr<float>(dw), N, H, W, Cin, Cout, KH, KW,
+                         stride, pad, groups, Ho, Wo, cur_stream());
+  return dw;
+}
+
+// w fp32 [Cout, KH, KW, Cin/G] contiguous -> (bf16 same layout, bf16 [Cin, KH, KW, Cout/G])
+std::vector<Tensor> weight_prep(const Tensor& w, int groups, bool want_t) {
+  check_f32(w, "w");
+  const int Cout = w.size(0), KH = w.size(1), KW = w.size(2), Cg = w.size(3);
+  auto wb = at::empty(w.sizes(), w.options().dtype(at::kBFloat16));
+  Tensor wt;
+  if (want_t) wt = at::empty({Cg * groups, KH, KW, Cout / groups}, wb.options());
+  pca::weight_prep_launch(ptr<float>(w), groups, Cout / groups, KH * KW, Cg, ptr<bf16>(wb),
+                          want_t ? ptr<bf16>(wt) : nullptr, cur_stream());
+  return {wb, wt};
+}
+
+// ------------------------------------------------------------------------------- BN
+Tensor bn_stats(const Tensor& x) {
+  check_bf16(x, "x");
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  const int P = pca::bn_row_blocks(M, C);
+  auto partial = at::empty({P, 2, C}, x.options().dtype(at::kFloat));
+  pca::bn_stats_launch(ptr<bf16>(x), M, C, ptr<float>(partial), P, cur_stream());
+  return partial;
+}
+
+// partial [R, 2, C] (or undefined in eval) -> aux [4, C] = {mean, invstd, scale, shift}
+Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional<Tensor>& gamma,
+                   const optional<Tensor>& beta, const Tensor& rmean, const Tensor& rvar,
+                   const optional<Tensor>& nbt, double momentum, double eps, bool training,
+                   bool update_running) {
+  const int C = rmean.numel();
+  auto aux = at::empty({4, C}, rmean.options());
+  const float* stat = nullptr;
+  int R = 0;
+  Tensor folded;
+  if (training) {
+    TORCH_CHECK(partial.has_value(), "training BN needs statistics");
+    const Tensor& p = *partial;
+    check_f32(p, "partial");
+    TORCH_CHECK(p.size(-1) == C, "stat channel mismatch");
+    R = p.size(0);
+    stat = ptr<float>(p);
+    if (R > 64) {
+      folded = at::empty({64, 2, C}, p.options());
+      R = pca::colsum_launch(stat, R, 2 * C, ptr<float>(folded), cur_stream());
+      stat = ptr<float>(folded);
+    }
+  }
+  pca::bn_finalize_launch(stat, R, C, count, optr<float>(gamma), optr<float>(beta),
+                          ptr<float>(rmean), ptr<float>(rvar), optr<int64_t>(nbt), (float)momentum,
+                          (float)eps, training ? 1 : 0, update_running ? 1 : 0, ptr<float>(aux),
+                          cur_stream());
+  return aux;
+}
+
+Tensor bn_apply(const Tensor& y, const Tensor& aux, const optional<Tensor>& res,
+                const optional<Tensor>& y2, const optional<Tensor>& aux2, int act) {
+  check_bf16(y, "y");
+  const int C = y.size(-1);
+  TORCH_CHECK(aux.size(1) == C, "aux channel mismatch");
+  if (res.has_value() && res->defined()) {
+    check_bf16(*res, "res");
+    TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
+  }
+  if (y2.has_value() && y2->defined()) {
+    check_bf16(*y2, "y2");
+    TORCH_CHECK(y2->sizes() == y.sizes(), "second BN input shape mismatch");
+  }
+  auto out = at::empty_like(y);
+  pca::bn_apply_launch(ptr<bf16>(y), ptr<float>(aux), C, y.numel(), optr<bf16>(res), optr<bf16>(y2),
+                       optr<float>(aux2), act, ptr<bf16>(out), cur_stream());
+  return out;
+}
+
+// Full BN backward: returns {dy, dres, dy2, dgamma, dbeta, dgamma2, dbeta2}
+std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out, const Tensor& y,
+                                const Tensor& aux, const optional<Tensor>& gamma,
+                                const optional<Tensor>& y2, const optional<Tensor>& aux2,
+                                const optional<Tensor>& gamma2, int act, bool training,
+                                bool need_dres, const optional<Tensor>& dgamma_acc,
+                                const optional<Tensor>& dbeta_acc,
+                                const optional<Tensor>& dgamma2_acc,
+                                const optional<Tensor>& dbeta2_acc) {
+  check_bf16(dout, "dout");
+  check_bf16(y, "y");
+  const int C = y.size(-1);
+  const int M = y.numel() / C;
+  const bool dual = y2.has_value() && y2->defined();
+  const int NS = dual ? 3 : 2;
+  if (act == 1) TORCH_CHECK(out.has_value() && out->defined(), "relu backward needs the output");
+  auto st = cur_stream();
+  const int P = pca::bn_row_blocks(M, C);
+  auto fopt = y.options().dtype(at::kFloat);
+  auto partial = at::empty({P, NS, C}, fopt);
+  pca::bn_bwd_reduce_launch(ptr<bf16>(dout), optr<bf16>(out), ptr<bf16>(y), ptr<float>(aux),
+                            optr<bf16>(y2), optr<float>(aux2), act, M, C, ptr<float>(partial), P,
+                            st);
+  const float* stat = ptr<float>(partial);
+  int R = P;
+  Tensor folded;
+  if (R > 64) {
+    folded = at::empty({64, NS, C}, fopt);
+    R = pca::colsum_launch(stat, R, NS * C, ptr<float>(folded), st);
+    stat = ptr<float>(folded);
+  }
+  // Parameter gradients are accumulated straight into the caller's .grad buffers when given
+  // (the flat gradient arena); otherwise fresh tensors are returned.
+  auto pick = [&](const optional<Tensor>& acc) {
+    if (acc.has_value() && acc->defined()) {
+      check_f32(*acc, "grad accumulator");
+      TORCH_CHECK(acc->numel() == C, "grad accumulator size");
+      return *acc;
+    }
+    return at::zeros({C}, fopt);
+  };
+  auto dgamma = pick(dgamma_acc), dbeta = pick(dbeta_acc);
+  Tensor dgamma2, dbeta2;
+  if (dual) {
+    dgamma2 = pick(dgamma2_acc);
+    dbeta2 = pick(dbeta2_acc);
+  }
+  auto coef = at::empty({dual ? 6 : 3, C}, fopt);
+  pca::bn_bwd_finalize_launch(stat, R, NS, C, (float)M, ptr<float>(aux), optr<float>(gamma),
+                              optr<float>(aux2), optr<float>(gamma2), training ? 1 : 0,
+                              ptr<float>(dgamma), ptr<float>(dbeta),
+                              dual ? ptr<float>(dgamma2) : nullptr,
+                              dual ? ptr<float>(dbeta2) : nullptr, ptr<float>(coef), 1, st);
+  auto dy = at::empty_like(y);
+  Tensor dres, dy2;
+  if (need_dres) dres = at::empty_like(y);
+  if (dual) dy2 = at::empty_like(y);
+  pca::bn_bwd_apply_launch(ptr<bf16>(dout), optr<bf16>(out), ptr<bf16>(y), ptr<float>(aux),
+                           ptr<float>(coef), act, C, y.numel(), ptr<bf16>(dy),
+                           need_dres ? ptr<bf16>(dres) : nullptr, optr<bf16>(y2),
+                           dual ? ptr<bf16>(dy2) : nullptr, st);
+  return {dy, dres, dy2, dgamma, dbeta, dgamma2, dbeta2};
+}
+
+// ------------------------------------------------------------------------------ misc
+Tensor nchw_to_nhwc(const Tensor& x, int Cp) {
+  check_f32(x, "x");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(Cp >= C, "pad channels");
+  auto y = at::empty({N, H, W, Cp}, x.options().dtype(at::kBFloat16));
+  pca::nchw_to_nhwc_launch(ptr<float>(x), N, C, H * W, Cp, ptr<bf16>(y), cur_stream());
+  return y;
+}
+
+Tensor nhwc_to_nchw(const Tensor& y, int C) {
+  check_bf16(y, "y");
+  const int N = y.size(0), H = y.size(1), W = y.size(2), Cp = y.size(3);
+  auto x = at::empty({N, C, H, W}, y.options().dtype(at::kFloat));
+  pca::nhwc_to_nchw_launch(ptr<bf16>(y), N, C, H * W, Cp, ptr<float>(x), cur_stream());
+  return x;
+}
+
+Tensor augment(const Tensor& data, const Tensor& idx, const Tensor& rnd, int pad,
+               std::vector<double> mean, std::vector<double> std) {
+  TORCH_CHECK(data.is_cuda() && data.scalar_type() == at::kByte && data.dim() == 4 &&
+                  data.size(3) == 3 && data.is_contiguous(),
+              "data must be uint8 [N,H,W,3] on GPU");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && rnd.scalar_type() == at::kInt, "idx/rnd dtypes");
+  TORCH_CHECK(idx.numel() == rnd.numel(), "idx/rnd size");
+  TORCH_CHECK(mean.size() == 3 && std.size() == 3, "mean/std");
+  const int B = idx.numel(), H = data.size(1), W = data.size(2);
+  auto out = at::empty({B, H, W, 8}, data.options().dtype(at::kBFloat16));
+  float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  float s[3] = {(float)std[0], (float)std[1], (float)std[2]};
+  pca::augment_launch(ptr<uint8_t>(data), ptr<int64_t>(idx), ptr<int32_t>(rnd), B, H, W, pad, m, s,
+                      ptr<bf16>(out), cur_stream());
+  return out;
+}
+
+Tensor gap_fwd(const Tensor& x) {
+  check_bf16(x, "x");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto y = at::empty({N, C}, x.options().dtype(at::kFloat));
+  pca::gap_fwd_launch(ptr<bf16>(x), N, HW, C, ptr<float>(y), cur_stream());
+  return y;
+}
+
+Tensor gap_bwd(const Tensor& dy, int H, int W) {
+  check_f32(dy, "dy");
+  const int N = dy.size(0), C = dy.size(1);
+  auto dx = at::empty({N, H, W, C}, dy.options().dtype(at::kBFloat16));
+  pca::gap_bwd_launch(ptr<float>(dy), N, H * W, C, ptr<bf16>(dx), cur_stream());
+  return dx;
+}
+
+Tensor avgpool_fwd(const Tensor& x, int k, int s, int p) {
+  check_bf16(x, "x");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = out_dim(H, k, s, p), Wo = out_dim(W, k, s, p);
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  pca::avgpool_fwd_launch(ptr<bf16>(x), N, H, W, C, Ho, Wo, k, s, p, ptr<bf16>(y), cur_stream());
+  return y;
+}
+
+Tensor avgpool_bwd(const Tensor& dy, int H, int W, int k, int s, int p) {
+  check_bf16(dy, "dy");
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), C = dy.size(3);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  pca::avgpool_bwd_launch(ptr<bf16>(dy), N, H, W, C, Ho, Wo, k, s, p, ptr<bf16>(dx), cur_stream());
+  return dx;
+}
+
+std::vector<Tensor> maxpool_fwd(const Tensor& x, int k, int s, int p) {
+  check_bf16(x, "x");
+  TORCH_CHECK(k * k <= 255, "maxpool window too large");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = out_dim(H, k, s, p), Wo = out_dim(W, k, s, p);
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  auto arg = at::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  pca::maxpool_fwd_launch(ptr<bf16>(x), N, H, W, C, Ho, Wo, k, s, p, ptr<bf16>(y), ptr<uint8_t>(arg),
+                          cur_stream());
+  return {y, arg};
+}
+
+Tensor maxpool_bwd(const Tensor& dy, const Tensor& arg, int H, int W, int k, int s, int p) {
+  check_bf16(dy, "dy");
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), C = dy.size(3);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  pca::maxpool_bwd_launch(ptr<bf16>(dy), ptr<uint8_t>(arg), N, H, W, C, Ho, Wo, k, s, p,
+                          ptr<bf16>(dx), cur_stream());
+  return dx;
+}
+
+std::vector<Tensor> ce_fused(const Tensor& logits, const Tensor& tgt,
+                             const optional<Tensor>& metrics, bool want_grad) {
+  check_f32(logits, "logits");
+  TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.is_cuda(), "targets int64 on GPU");
+  const int N = logits.size(0), K = logits.size(1);
+  TORCH_CHECK(tgt.numel() == N, "target count");
+  if (metrics.has_value() && metrics->defined())
+    TORCH_CHECK(metrics->scalar_type() == at::kDouble && metrics->numel() >= 3, "metrics buffer");
+  auto loss = at::empty({}, logits.options());
+  Tensor dl;
+  if (want_grad) dl = at::empty_like(logits);
+  pca::ce_fused_launch(ptr<float>(logits), ptr<int64_t>(tgt), N, K, ptr<float>(loss),
+                       want_grad ? ptr<float>(dl) : nullptr, optr<double>(metrics), cur_stream());
+  return {loss, dl};
+}
+
+Tensor scale_by_scalar(const Tensor& g, const Tensor& s) {
+  check_f32(g, "g");
+  auto out = at::empty_like(g);
+  pca::scale_by_scalar_launch(ptr<float>(g), ptr<float>(s), g.numel(), ptr<float>(out),
+                              cur_stream());
+  return out;
+}
+
+// ptr tables are int64 GPU tensors holding device addresses; chunks [n,3] int64 on GPU
+void sgd_step(const Tensor& chunks, const Tensor& pptr, const Tensor& gptr, const Tensor& bptr,
+              const optional<Tensor>& sptr, const Tensor& lr, double momentum, double dampening,
+              double wd, double grad_scale, bool nesterov, bool first) {
+  TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == at::kLong, "chunks");
+  TORCH_CHECK(lr.is_cuda() && lr.scalar_type() == at::kFloat, "lr must be a GPU fp32 scalar");
+  pca::sgd_launch(ptr<int64_t>(chunks), chunks.size(0), ptr<float* const>(pptr),
+                  ptr<const float* const>(gptr), ptr<float* const>(bptr),
+                  sptr.has_value() && sptr->defined() ? ptr<bf16* const>(*sptr) : nullptr,
+                  ptr<float>(lr), (float)momentum, (float)dampening, (float)wd, (float)grad_scale,
+                  nesterov ? 1 : 0, first ? 1 : 0, cur_stream());
+}
+
+Tensor se_scale_fwd(const Tensor& x, const Tensor& s) {
+  check_bf16(x, "x");
+  check_f32(s, "s");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  TORCH_CHECK(s.numel() == (int64_t)N * C, "excitation shape");
+  auto out = at::empty_like(x);
+  pca::se_scale_fwd_launch(ptr<bf16>(x), ptr<float>(s), N, HW, C, ptr<bf16>(out), cur_stream());
+  return out;
+}
+
+std::vector<Tensor> se_scale_bwd(const Tensor& dout, const Tensor& x, const Tensor& s) {
+  check_bf16(dout, "dout");
+  check_bf16(x, "x");
+  check_f32(s, "s");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto dx = at::empty_like(x);
+  auto ds = at::empty({N, C}, s.options());
+  pca::se_scale_bwd_launch(ptr<bf16>(dout), ptr<bf16>(x), ptr<float>(s), N, HW, C, ptr<bf16>(dx),
+                           ptr<float>(ds), cur_stream());
+  return {dx, ds};
+}
+
+Tensor act_fwd(const Tensor& x, int act) {
+  check_bf16(x, "x");
+  auto y = at::empty_like(x);
+  pca::act_fwd_launch(ptr<bf16>(x), x.numel(), act, ptr<bf16>(y), cur_stream());
+  return y;
+}
+
+Tensor act_bwd(const Tensor& dy, const Tensor& x, int act) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  auto dx = at::empty_like(x);
+  pca::act_bwd_launch(ptr<bf16>(dy), ptr<bf16>(x), x.numel(), act, ptr<bf16>(dx), cur_stream());
+  return dx;
+}
+
+Tensor add_act(const Tensor& a, const Tensor& b, int act) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  TORCH_CHECK(a.sizes() == b.sizes(), "add shape mismatch");
+  auto y = at::empty_like(a);
+  pca::add_act_launch(ptr<bf16>(a), ptr<bf16>(b), a.numel(), act, ptr<bf16>(y), cur_stream());
+  return y;
+}
+
+// ---------------------------------------------------------------------------- dwconv
+// wT fp32 [KH*KW, Cout]
+Tensor dw_fwd(const Tensor& x, const Tensor& wT, int KH, int KW, int stride, int pad) {
+  check_bf16(x, "x");
+  check_f32(wT, "wT");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Co = wT.size(1);
+  TORCH_CHECK(wT.size(0) == KH * KW && Co % C == 0, "depthwise weight shape");
+  const int Ho = out_dim(H, KH, stride, pad), Wo = out_dim(W, KW, stride, pad);
+  auto y = at::empty({N, Ho, Wo, Co}, x.options());
+  pca::dw_fwd_launch(ptr<bf16>(x), ptr<float>(wT), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad,
+                     ptr<bf16>(y), cur_stream());
+  return y;
+}
+
+Tensor dw_dgrad(const Tensor& dy, const Tensor& wT, int H, int W, int C, int KH, int KW, int stride,
+                int pad) {
+  check_bf16(dy, "dy");
+  check_f32(wT, "wT");
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo, "geometry");
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  pca::dw_dgrad_launch(ptr<bf16>(dy), ptr<float>(wT), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad,
+                       ptr<bf16>(dx), cur_stream());
+  return dx;
+}
+
+// returns dw fp32 [Cout, KH*KW]
+Tensor dw_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride, int pad) {
+  check_bf16(x, "x");
+  check_bf16(dy, "dy");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo, "geometry");
+  const int chunks = pca::dw_wgrad_partials(N, Ho, Wo);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto partial = at::empty({chunks, KH * KW, Co}, fopt);
+  auto dw = at::empty({Co, KH * KW}, fopt);
+  pca::dw_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad,
+                       ptr<float>(partial), chunks, nullptr, ptr<float>(dw), cur_stream());
+  return dw;
+}
+
+// ------------------------------------------------------------------------- direct conv
+// w fp32 [Cout, KH, KW, Cin/G] contiguous (physical layout of the channels_last parameter)
+Tensor direct_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, int stride,
+                  int pad, int groups) {
+  check_bf16(x, "x");
+  check_f32(w, "w");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  const int Cout = w.size(0), KH = w.size(1), KW = w.size(2);
+  TORCH_CHECK(w.size(3) * groups == Cin && Cout % groups == 0, "direct conv weight shape");
+  const int Ho = out_dim(H, KH, stride, pad), Wo = out_dim(W, KW, stride, pad);
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
+  auto y = at::empty({N, Ho, Wo, Cout}, x.options());
+  pca::direct_fwd_launch(ptr<bf16>(x), ptr<float>(w), optr<float>(bias), N, H, W, Cin, Ho, Wo, Cout,
+                         KH, KW, stride, pad, groups, ptr<bf16>(y), cur_stream());
+  return y;
+}
+
+Tensor direct_dgrad(const Tensor& dy, const Tensor& w, int H, int W, int stride, int pad,
+                    int groups) {
+  check_bf16(dy, "dy");
+  check_f32(w, "w");
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
+  const int KH = w.size(1), KW = w.size(2), Cin = w.size(3) * groups;
+  TORCH_CHECK(w.size(0) == Cout, "direct dgrad weight shape");
+  TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo, "geometry");
+  auto dx = at::empty({N, H, W, Cin}, dy.options());
+  pca::direct_dgrad_launch(ptr<bf16>(dy), ptr<float>(w), N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                           pad, groups, ptr<bf16>(dx), cur_stream());
+  return dx;
+}
+
+// returns fp32 [Cout*KH*KW*Cin/G + (bias ? Cout : 0)]
+Tensor direct_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride, int pad,
+                    int groups, bool with_bias) {
+  check_bf16(x, "x");
+  check_bf16(dy, "dy");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
+  TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo, "geometry");
+  const int tot = Cout * KH * KW * (Cin / groups) + (with_bias ? Cout : 0);
+  const int splits = pca::direct_wgrad_splits(N, Ho, Wo, tot);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto partial = at::empty({splits, tot}, fopt);
+  auto out = at::empty({tot}, fopt);
+  pca::direct_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                           pad, groups, with_bias ? 1 : 0, ptr<float>(partial), splits,
+                           ptr<float>(out), cur_stream());
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "pytorch_cifar_amd gfx950 kernels";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("weight_prep", &weight_prep);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_backward", &bn_backward);
+  m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("nhwc_to_nchw", &nhwc_to_nchw);
+  m.def("augment", &augment);
+  m.def("gap_fwd", &gap_fwd);
+  m.def("gap_bwd", &gap_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("ce_fused", &ce_fused);
+  m.def("scale_by_scalar", &scale_by_scalar);
+  m.def("sgd_step", &sgd_step);
+  m.def("se_scale_fwd", &se_scale_fwd);
+  m.def("se_scale_bwd", &se_scale_bwd);
+  m.def("act_fwd", &act_fwd);
+  m.def("act_bwd", &act_bwd);
+  m.def("add_act", &add_act);
+  m.def("dw_fwd", &dw_fwd);
+  m.def("dw_dgrad", &dw_dgrad);
+  m.def("dw_wgrad", &dw_wgrad);
+  m.def("direct_fwd", &direct_fwd);
+  m.def("direct_dgrad", &direct_dgrad);
+  m.def("direct_wgrad", &direct_wgrad);
+  pca::register_comm(m);
+}

@@ -1,0 +1,132 @@
+// Native RCCL communicator (one per process/GPU) for the data-parallel engine.
+//
+// Replaces the NCCL communicator that the reference obtains implicitly through
+// torch.nn.parallel.DistributedDataParallel (main_dist.py:73-74 init_process_group('nccl'),
+// main_dist.py:141 DDP: constructor broadcast C3, per-forward buffer broadcast C4,
+// per-backward bucketed all-reduce C5 — SURVEY §2.9).
+//
+// The unique id is exchanged through the torch.distributed TCPStore by the Python side; every
+// collective is enqueued on the caller-supplied HIP stream so the data-parallel engine can put
+// gradient buckets on a dedicated communication stream and overlap them with backward (and so
+// the calls are capturable into a hipGraph together with the step that produces the buckets).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <torch/extension.h>
+
+#include <stdexcept>
+#include <string>
+
+namespace pca {
+
+#define RCCL_CHECK(cmd)                                                              \
+  do {                                                                               \
+    ncclResult_t r_ = (cmd);                                                         \
+    if (r_ != ncclSuccess)                                                           \
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r_) + \
+                               " at " #cmd);                                         \
+  } while (0)
+
+static ncclDataType_t to_nccl(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kLong: return ncclInt64;
+    case at::kInt: return ncclInt32;
+    case at::kByte: return ncclUint8;
+    default: throw std::runtime_error("unsupported dtype for RCCL");
+  }
+}
+
+static ncclRedOp_t to_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "avg") return ncclAvg;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  throw std::runtime_error("unsupported reduction op " + op);
+}
+
+py::bytes rccl_unique_id() {
+  ncclUniqueId id;
+  RCCL_CHECK(ncclGetUniqueId(&id));
+  return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+class RcclComm {
+ public:
+  RcclComm(const std::string& id_bytes, int world, int rank, int device)
+      : world_(world), rank_(rank), device_(device) {
+    if (id_bytes.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad RCCL unique id");
+    ncclUniqueId id;
+    memcpy(&id, id_bytes.data(), sizeof(id));
+    hipSetDevice(device);
+    RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+  }
+  ~RcclComm() { destroy(); }
+
+  void destroy() {
+    if (comm_) {
+      ncclCommDestroy(comm_);
+      comm_ = nullptr;
+    }
+  }
+
+  void all_reduce(at::Tensor t, const std::string& op, int64_t stream) {
+    check(t);
+    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
+                             to_op(op), comm_, reinterpret_cast<hipStream_t>(stream)));
+  }
+  void broadcast(at::Tensor t, int root, int64_t stream) {
+    check(t);
+    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root,
+                             comm_, reinterpret_cast<hipStream_t>(stream)));
+  }
+  void reduce_scatter(at::Tensor in, at::Tensor out, const std::string& op, int64_t stream) {
+    check(in);
+    check(out);
+    RCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(),
+                                 to_nccl(in.scalar_type()), to_op(op), comm_,
+                                 reinterpret_cast<hipStream_t>(stream)));
+  }
+  void all_gather(at::Tensor in, at::Tensor out, int64_t stream) {
+    check(in);
+    check(out);
+    RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()),
+                             comm_, reinterpret_cast<hipStream_t>(stream)));
+  }
+  void group_start() { RCCL_CHECK(ncclGroupStart()); }
+  void group_end() { RCCL_CHECK(ncclGroupEnd()); }
+  int world() const { return world_; }
+  int rank() const { return rank_; }
+
+ private:
+  void check(const at::Tensor& t) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL tensors must be contiguous GPU tensors");
+    TORCH_CHECK(comm_ != nullptr, "communicator destroyed");
+  }
+  ncclComm_t comm_ = nullptr;
+  int world_, rank_, device_;
+};
+
+void register_comm(py::module& m) {
+  m.def("rccl_unique_id", &rccl_unique_id);
+  m.def("rccl_version", []() {
+    int v = 0;
+    ncclGetVersion(&v);
+    return v;
+  });
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init<const std::string&, int, int, int>())
+      .def("all_reduce", &RcclComm::all_reduce)
+      .def("broadcast", &RcclComm::broadcast)
+      .def("reduce_scatter", &RcclComm::reduce_scatter)
+      .def("all_gather", &RcclComm::all_gather)
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end)
+      .def("destroy", &RcclComm::destroy)
+      .def_property_readonly("world", &RcclComm::world)
+      .def_property_readonly("rank", &RcclComm::rank);
+}
+
+}  // namespace pca

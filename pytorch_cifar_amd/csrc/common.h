@@ -1,0 +1,107 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels of pytorch_cifar_amd.
+//
+// Conventions used by every kernel in csrc/:
+//   * activations are NHWC bf16 ("channels-last"), one contiguous [N*H*W][C] matrix;
+//   * parameters are fp32 masters whose *physical* layout is [Cout][KH][KW][Cin/G]
+//     (torch.channels_last strides on the reference [Cout,Cin,KH,KW] shape), so a conv
+//     weight is already the K-contiguous GEMM operand the MFMA B-fragment wants;
+//   * all reductions accumulate in fp32; per-block partials are written to slabs and
+//     folded by a finalize kernel (deterministic, no cross-XCD atomics on hot counters).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pca {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+__device__ __forceinline__ float bf2f(bf16 v) { return static_cast<float>(v); }
+__device__ __forceinline__ bf16 f2bf(float v) { return static_cast<bf16>(v); }
+
+// 16-byte vector of 8 bf16 as raw bits (for loads/stores/LDS traffic).
+struct alignas(16) U128 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  bf16 ha = f2bf(a), hb = f2bf(b);
+  uint16_t ua = __builtin_bit_cast(uint16_t, ha);
+  uint16_t ub = __builtin_bit_cast(uint16_t, hb);
+  return (uint32_t)ua | ((uint32_t)ub << 16);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 u;
+  u.x = pack2(f[0], f[1]);
+  u.y = pack2(f[2], f[3]);
+  u.z = pack2(f[4], f[5]);
+  u.w = pack2(f[6], f[7]);
+  return u;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, "XCD swizzle must be
+// bijective"): blocks b and b+8 share an XCD, so give each XCD a contiguous chunk of tiles.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = orig % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
+}
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_SIGMOID = 3 };
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  if (act == ACT_SWISH) return v * sigmoidf_(v);
+  if (act == ACT_SIGMOID) return sigmoidf_(v);
+  return v;
+}
+
+// d act(z)/dz evaluated from the pre-activation z.
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_SWISH) {
+    const float s = sigmoidf_(z);
+    return s * (1.f + z * (1.f - s));
+  }
+  if (act == ACT_SIGMOID) {
+    const float s = sigmoidf_(z);
+    return s * (1.f - s);
+  }
+  return 1.f;
+}
+
+}  // namespace pca

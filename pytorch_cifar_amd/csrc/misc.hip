@@ -1,0 +1,512 @@
+// Memory-bound kernels around the conv/BN core, NHWC bf16 activations, fp32 parameters.
+//
+//   layout      : NCHW fp32 model input -> NHWC bf16 (channel-padded) and back      (K26)
+//   augment     : GPU-resident uint8 CIFAR images -> random crop(pad 4) + flip +
+//                 normalize -> NHWC bf16 (main.py:30-35 / main_dist.py:93-97)       (K25)
+//   pooling     : global average (head + SE squeeze), kxk avg, kxk max (+ saved argmax)
+//                 (resnet.py:127, googlenet.py:42/68/79, lenet.py:16)               (K15/K16)
+//   cross-entropy: log-softmax + NLL + dlogits + argmax/correct in one kernel
+//                 (main.py:103,108-110)                                              (K18/K19)
+//   sgd         : one multi-tensor launch, momentum 0.9 / wd 5e-4 semantics of
+//                 torch.optim.SGD (main.py:87-88)                                    (K20)
+//   se / swish  : squeeze-excite channel scaling and standalone activations          (K13/K14)
+//   eltwise     : residual add(+act) for the non-fused paths, act backward
+#include "common.h"
+
+namespace pca {
+
+static int grid_cap(size_t work, int per_block = 256, int cap = 8192) {
+  size_t b = (work + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  return (int)(b < (size_t)cap ? b : cap);
+}
+
+// ------------------------------------------------------------------------------ layout
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int HW, int Cp,
+                                    bf16* __restrict__ y) {
+  const size_t total = (size_t)N * HW * Cp;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    const size_t p = i / Cp;
+    const int hw = (int)(p % HW);
+    const int n = (int)(p / HW);
+    y[i] = c < C ? f2bf(x[((size_t)n * C + c) * HW + hw]) : f2bf(0.f);
+  }
+}
+
+__global__ void nhwc_to_nchw_kernel(const bf16* __restrict__ y, int N, int C, int HW, int Cp,
+                                    float* __restrict__ x) {
+  const size_t total = (size_t)N * C * HW;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int hw = (int)(i % HW);
+    const size_t q = i / HW;
+    const int c = (int)(q % C);
+    const int n = (int)(q / C);
+    x[i] = bf2f(y[((size_t)n * HW + hw) * Cp + c]);
+  }
+}
+
+// ----------------------------------------------------------------------------- augment
+// One thread per output pixel: gathers 3 uint8 channels, writes 8 bf16 (16 B, C padded to 8).
+__global__ void augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx,
+                               const int32_t* __restrict__ rnd, int B, int H, int W, int pad,
+                               float m0, float m1, float m2, float is0, float is1, float is2,
+                               bf16* __restrict__ out) {
+  const int total = B * H * W;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int b = i / (H * W);
+    const int hw = i % (H * W);
+    const int h = hw / W, w = hw % W;
+    const int r = rnd[b];
+    const int dy = (r & 0xff) % (2 * pad + 1);
+    const int dx = ((r >> 8) & 0xff) % (2 * pad + 1);
+    const bool flip = (r >> 16) & 1;
+    const int sh = h + dy - pad;
+    const int sw0 = flip ? (W - 1 - w) : w;
+    const int sw = sw0 + dx - pad;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // torchvision RandomCrop(padding) zero-pads the uint8 image, so a padded pixel is 0 before
+    // ToTensor/Normalize: (0 - mean) / std.
+    float px[3] = {0.f, 0.f, 0.f};
+    if (sh >= 0 && sh < H && sw >= 0 && sw < W) {
+      const uint8_t* src = data + (((size_t)idx[b] * H + sh) * W + sw) * 3;
+      px[0] = src[0] * (1.f / 255.f);
+      px[1] = src[1] * (1.f / 255.f);
+      px[2] = src[2] * (1.f / 255.f);
+    }
+    v[0] = (px[0] - m0) * is0;
+    v[1] = (px[1] - m1) * is1;
+    v[2] = (px[2] - m2) * is2;
+    *reinterpret_cast<uint4*>(out + (size_t)i * 8) = pack8(v);
+  }
+}
+
+// ------------------------------------------------------------------------------ pooling
+// Global average over HW: x[N][HW][C] bf16 -> y[N][C] fp32. One block per (n, 256-channel tile).
+__global__ void gap_fwd_kernel(const bf16* __restrict__ x, int HW, int C, float* __restrict__ y) {
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const bf16* p = x + (size_t)n * HW * C + c;
+  float s = 0.f;
+  for (int i = 0; i < HW; ++i) s += bf2f(p[(size_t)i * C]);
+  y[(size_t)n * C + c] = s / HW;
+}
+
+__global__ void gap_bwd_kernel(const float* __restrict__ dy, int N, int HW, int C,
+                               bf16* __restrict__ dx) {
+  const size_t total = (size_t)N * HW * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const int n = (int)(i / ((size_t)HW * C));
+    dx[i] = f2bf(dy[(size_t)n * C + c] / HW);
+  }
+}
+
+// k x k pooling (avg: count_include_pad semantics of F.avg_pool2d; max: -inf padding)
+struct PoolGeom {
+  int N, H, W, C, Ho, Wo, k, s, p;
+};
+
+__global__ void avgpool_fwd_kernel(const bf16* __restrict__ x, PoolGeom g, bf16* __restrict__ y) {
+  const size_t total = (size_t)g.N * g.Ho * g.Wo * g.C;
+  const float inv = 1.f / (g.k * g.k);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    size_t q = i / g.C;
+    const int ow = (int)(q % g.Wo);
+    q /= g.Wo;
+    const int oh = (int)(q % g.Ho);
+    const int n = (int)(q / g.Ho);
+    float s = 0.f;
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int ih = oh * g.s - g.p + kh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int iw = ow * g.s - g.p + kw;
+        if (iw < 0 || iw >= g.W) continue;
+        s += bf2f(x[(((size_t)n * g.H + ih) * g.W + iw) * g.C + c]);
+      }
+    }
+    y[i] = f2bf(s * inv);
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const bf16* __restrict__ dy, PoolGeom g, bf16* __restrict__ dx) {
+  const size_t total = (size_t)g.N * g.H * g.W * g.C;
+  const float inv = 1.f / (g.k * g.k);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    size_t q = i / g.C;
+    const int iw = (int)(q % g.W);
+    q /= g.W;
+    const int ih = (int)(q % g.H);
+    const int n = (int)(q / g.H);
+    float s = 0.f;
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int t = ih + g.p - kh;
+      if (t < 0 || t % g.s) continue;
+      const int oh = t / g.s;
+      if (oh >= g.Ho) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int u = iw + g.p - kw;
+        if (u < 0 || u % g.s) continue;
+        const int ow = u / g.s;
+        if (ow >= g.Wo) continue;
+        s += bf2f(dy[(((size_t)n * g.Ho + oh) * g.Wo + ow) * g.C + c]);
+      }
+    }
+    dx[i] = f2bf(s * inv);
+  }
+}
+
+__global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, PoolGeom g, bf16* __restrict__ y,
+                                   uint8_t* __restrict__ arg) {
+  const size_t total = (size_t)g.N * g.Ho * g.Wo * g.C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    size_t q = i / g.C;
+    const int ow = (int)(q % g.Wo);
+    q /= g.Wo;
+    const int oh = (int)(q % g.Ho);
+    const int n = (int)(q / g.Ho);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int ih = oh * g.s - g.p + kh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int iw = ow * g.s - g.p + kw;
+        if (iw < 0 || iw >= g.W) continue;
+        const float v = bf2f(x[(((size_t)n * g.H + ih) * g.W + iw) * g.C + c]);
+        if (v > best || (v != v)) {
+          best = v;
+          bi = kh * g.k + kw;
+        }
+      }
+    }
+    y[i] = f2bf(best);
+    arg[i] = (uint8_t)bi;
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                   PoolGeom g, bf16* __restrict__ dx) {
+  const size_t total = (size_t)g.N * g.H * g.W * g.C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    size_t q = i / g.C;
+    const int iw = (int)(q % g.W);
+    q /= g.W;
+    const int ih = (int)(q % g.H);
+    const int n = (int)(q / g.H);
+    float s = 0.f;
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int t = ih + g.p - kh;
+      if (t < 0 || t % g.s) continue;
+      const int oh = t / g.s;
+      if (oh >= g.Ho) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int u = iw + g.p - kw;
+        if (u < 0 || u % g.s) continue;
+        const int ow = u / g.s;
+        if (ow >= g.Wo) continue;
+        const size_t o = (((size_t)n * g.Ho + oh) * g.Wo + ow) * g.C + c;
+        if (arg[o] == kh * g.k + kw) s += bf2f(dy[o]);
+      }
+    }
+    dx[i] = f2bf(s);
+  }
+}
+
+// ----------------------------------------------------------------------- cross-entropy
+// logits[N][K] fp32, targets int64. One 256-thread block, deterministic reductions.
+// Writes loss (mean), dlogits = (softmax - onehot) / N, and accumulates
+// metrics[0] += sum loss, metrics[1] += correct, metrics[2] += N (fp64 accumulator).
+__global__ __launch_bounds__(256) void ce_fused_kernel(const float* __restrict__ logits,
+                                                       const int64_t* __restrict__ tgt, int N,
+                                                       int K, float* __restrict__ loss,
+                                                       float* __restrict__ dlogits,
+                                                       double* __restrict__ metrics) {
+  __shared__ float sl[256];
+  __shared__ int sc[256];
+  float lsum = 0.f;
+  int corr = 0;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const float* row = logits + (size_t)n * K;
+    float mx = -INFINITY;
+    int am = 0;
+    for (int k = 0; k < K; ++k) {
+      const float v = row[k];
+      if (v > mx) {
+        mx = v;
+        am = k;
+      }
+    }
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += __expf(row[k] - mx);
+    const float lse = mx + __logf(se);
+    const int t = (int)tgt[n];
+    lsum += lse - row[t];
+    corr += (am == t);
+    if (dlogits) {
+      const float invN = 1.f / N;
+      for (int k = 0; k < K; ++k) {
+        const float p = __expf(row[k] - lse);
+        dlogits[(size_t)n * K + k] = (p - (k == t ? 1.f : 0.f)) * invN;
+      }
+    }
+  }
+  sl[threadIdx.x] = lsum;
+  sc[threadIdx.x] = corr;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sl[threadIdx.x] += sl[threadIdx.x + o];
+      sc[threadIdx.x] += sc[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    loss[0] = sl[0] / N;
+    if (metrics) {
+      metrics[0] += (double)sl[0] / N;
+      metrics[1] += (double)sc[0];
+      metrics[2] += (double)N;
+    }
+  }
+}
+
+__global__ void scale_by_scalar_kernel(const float* __restrict__ g, const float* __restrict__ s,
+                                       size_t n, float* __restrict__ out) {
+  const float v = s[0];
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    out[i] = g[i] * v;
+}
+
+// ---------------------------------------------------------------------------------- SGD
+// Multi-tensor SGD with momentum/weight decay/nesterov/dampening (torch.optim.SGD semantics).
+// `meta` holds per-chunk {tensor index, start, end}; ptrs holds param/grad/buf pointers.
+struct SgdArgs {
+  const int64_t* chunks;   // [nchunks][3]
+  float* const* params;
+  const float* const* grads;
+  float* const* bufs;
+  bf16* const* shadows;    // optional bf16 copies (nullptr entries allowed)
+  const float* lr;         // device scalar (graph-capture friendly)
+  float momentum, dampening, wd, grad_scale;
+  int nesterov, first;
+};
+
+__global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) {
+  const int64_t* ch = a.chunks + (size_t)blockIdx.x * 3;
+  const int t = (int)ch[0];
+  const int64_t s = ch[1], e = ch[2];
+  float* p = a.params[t];
+  const float* g = a.grads[t];
+  float* b = a.bufs[t];
+  bf16* sh = a.shadows ? a.shadows[t] : nullptr;
+  const float lr = a.lr[0];
+  for (int64_t i = s + threadIdx.x; i < e; i += 256) {
+    float d = g ? g[i] * a.grad_scale : 0.f;
+    const float pv = p[i];
+    if (a.wd != 0.f) d += a.wd * pv;
+    if (a.momentum != 0.f) {
+      float bv = a.first ? d : a.momentum * b[i] + (1.f - a.dampening) * d;
+      b[i] = bv;
+      d = a.nesterov ? d + a.momentum * bv : bv;
+    }
+    const float np = pv - lr * d;
+    p[i] = np;
+    if (sh) sh[i] = f2bf(np);
+  }
+}
+
+// -------------------------------------------------------------------------- SE / acts
+// out[n,hw,c] = x[n,hw,c] * sigmoid(s[n,c])   (s = pre-sigmoid excitation logits, fp32)
+__global__ void se_scale_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ s,
+                                    int N, int HW, int C, bf16* __restrict__ out) {
+  const size_t total = (size_t)N * HW * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const int n = (int)(i / ((size_t)HW * C));
+    out[i] = f2bf(bf2f(x[i]) * sigmoidf_(s[(size_t)n * C + c]));
+  }
+}
+
+// dx = dout * sig(s);  ds[n,c] = sum_hw dout*x * sig'(s). One block per (n, 64-channel tile).
+__global__ __launch_bounds__(256) void se_scale_bwd_kernel(const bf16* __restrict__ dout,
+                                                           const bf16* __restrict__ x,
+                                                           const float* __restrict__ s, int N,
+                                                           int HW, int C, bf16* __restrict__ dx,
+                                                           float* __restrict__ ds) {
+  __shared__ float red[4][64];
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < C) {
+    const float sg = sigmoidf_(s[(size_t)n * C + c]);
+    for (int hw = r; hw < HW; hw += 4) {
+      const size_t i = ((size_t)n * HW + hw) * C + c;
+      const float d = bf2f(dout[i]);
+      dx[i] = f2bf(d * sg);
+      acc += d * bf2f(x[i]);
+    }
+    acc *= sg * (1.f - sg);
+  }
+  red[r][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (r == 0 && c < C)
+    ds[(size_t)n * C + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                            red[3][threadIdx.x];
+}
+
+__global__ void act_fwd_kernel(const bf16* __restrict__ x, size_t n, int act, bf16* __restrict__ y) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(apply_act(bf2f(x[i]), act));
+}
+
+__global__ void act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, size_t n,
+                               int act, bf16* __restrict__ dx) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    dx[i] = f2bf(bf2f(dy[i]) * act_grad(bf2f(x[i]), act));
+}
+
+// out = act(a + b), vectorized by 8 when possible
+__global__ void add_act_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b, size_t n,
+                               int act, bf16* __restrict__ y) {
+  const size_t nv = n / 8;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float fa[8], fb[8];
+    unpack8(reinterpret_cast<const uint4*>(a)[i], fa);
+    unpack8(reinterpret_cast<const uint4*>(b)[i], fb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) fa[k] = apply_act(fa[k] + fb[k], act);
+    reinterpret_cast<uint4*>(y)[i] = pack8(fa);
+  }
+  for (size_t i = nv * 8 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(apply_act(bf2f(a[i]) + bf2f(b[i]), act));
+}
+
+// fp32 -> bf16 cast (weights) and the dgrad weight transpose
+// w [G][Cn][T][Cr] -> wt [G][Cr][T][Cn]
+__global__ void weight_prep_kernel(const float* __restrict__ w, int G, int Cn, int T, int Cr,
+                                   bf16* __restrict__ wb, bf16* __restrict__ wt) {
+  const size_t total = (size_t)G * Cn * T * Cr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % Cr);
+    size_t q = i / Cr;
+    const int t = (int)(q % T);
+    q /= T;
+    const int co = (int)(q % Cn);
+    const int g = (int)(q / Cn);
+    const bf16 v = f2bf(w[i]);
+    if (wb) wb[i] = v;
+    if (wt) wt[(((size_t)g * Cr + ci) * T + t) * Cn + co] = v;
+  }
+}
+
+// ================================================================================ host
+void nchw_to_nhwc_launch(const float* x, int N, int C, int HW, int Cp, bf16* y, hipStream_t st) {
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_cap((size_t)N * HW * Cp)), dim3(256), 0, st, x,
+                     N, C, HW, Cp, y);
+}
+void nhwc_to_nchw_launch(const bf16* y, int N, int C, int HW, int Cp, float* x, hipStream_t st) {
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_cap((size_t)N * HW * C)), dim3(256), 0, st, y,
+                     N, C, HW, Cp, x);
+}
+void augment_launch(const uint8_t* data, const int64_t* idx, const int32_t* rnd, int B, int H,
+                    int W, int pad, const float* mean, const float* std, bf16* out,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(augment_kernel, dim3(grid_cap((size_t)B * H * W)), dim3(256), 0, st, data, idx,
+                     rnd, B, H, W, pad, mean[0], mean[1], mean[2], 1.f / std[0], 1.f / std[1],
+                     1.f / std[2], out);
+}
+void gap_fwd_launch(const bf16* x, int N, int HW, int C, float* y, hipStream_t st) {
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(cdiv(C, 64), N), dim3(64), 0, st, x, HW, C, y);
+}
+void gap_bwd_launch(const float* dy, int N, int HW, int C, bf16* dx, hipStream_t st) {
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_cap((size_t)N * HW * C)), dim3(256), 0, st, dy, N, HW,
+                     C, dx);
+}
+static PoolGeom pg(int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+  PoolGeom g{N, H, W, C, Ho, Wo, k, s, p};
+  return g;
+}
+void avgpool_fwd_launch(const bf16* x, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
+                        int p, bf16* y, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_cap((size_t)N * Ho * Wo * C)), dim3(256), 0, st,
+                     x, pg(N, H, W, C, Ho, Wo, k, s, p), y);
+}
+void avgpool_bwd_launch(const bf16* dy, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
+                        int p, bf16* dx, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_cap((size_t)N * H * W * C)), dim3(256), 0, st, dy,
+                     pg(N, H, W, C, Ho, Wo, k, s, p), dx);
+}
+void maxpool_fwd_launch(const bf16* x, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
+                        int p, bf16* y, uint8_t* arg, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_cap((size_t)N * Ho * Wo * C)), dim3(256), 0, st,
+                     x, pg(N, H, W, C, Ho, Wo, k, s, p), y, arg);
+}
+void maxpool_bwd_launch(const bf16* dy, const uint8_t* arg, int N, int H, int W, int C, int Ho,
+                        int Wo, int k, int s, int p, bf16* dx, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_cap((size_t)N * H * W * C)), dim3(256), 0, st, dy,
+                     arg, pg(N, H, W, C, Ho, Wo, k, s, p), dx);
+}
+void ce_fused_launch(const float* logits, const int64_t* tgt, int N, int K, float* loss,
+                     float* dlogits, double* metrics, hipStream_t st) {
+  hipLaunchKernelGGL(ce_fused_kernel, dim3(1), dim3(256), 0, st, logits, tgt, N, K, loss, dlogits,
+                     metrics);
+}
+void scale_by_scalar_launch(const float* g, const float* s, size_t n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(scale_by_scalar_kernel, dim3(grid_cap(n)), dim3(256), 0, st, g, s, n, out);
+}
+void sgd_launch(const int64_t* chunks, int nchunks, float* const* params, const float* const* grads,
+                float* const* bufs, bf16* const* shadows, const float* lr, float momentum,
+                float dampening, float wd, float grad_scale, int nesterov, int first,
+                hipStream_t st) {
+  SgdArgs a{chunks, params, grads, bufs, shadows, lr, momentum, dampening, wd, grad_scale,
+            nesterov, first};
+  hipLaunchKernelGGL(sgd_kernel, dim3(nchunks), dim3(256), 0, st, a);
+}
+void se_scale_fwd_launch(const bf16* x, const float* s, int N, int HW, int C, bf16* out,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(se_scale_fwd_kernel, dim3(grid_cap((size_t)N * HW * C)), dim3(256), 0, st, x, s,
+                     N, HW, C, out);
+}
+void se_scale_bwd_launch(const bf16* dout, const bf16* x, const float* s, int N, int HW, int C,
+                         bf16* dx, float* ds, hipStream_t st) {
+  hipLaunchKernelGGL(se_scale_bwd_kernel, dim3(cdiv(C, 64), N), dim3(256), 0, st, dout, x, s, N, HW,
+                     C, dx, ds);
+}
+void act_fwd_launch(const bf16* x, size_t n, int act, bf16* y, hipStream_t st) {
+  hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_cap(n)), dim3(256), 0, st, x, n, act, y);
+}
+void act_bwd_launch(const bf16* dy, const bf16* x, size_t n, int act, bf16* dx, hipStream_t st) {
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_cap(n)), dim3(256), 0, st, dy, x, n, act, dx);
+}
+void add_act_launch(const bf16* a, const bf16* b, size_t n, int act, bf16* y, hipStream_t st) {
+  hipLaunchKernelGGL(add_act_kernel, dim3(grid_cap(n / 8 + 1)), dim3(256), 0, st, a, b, n, act, y);
+}
+void weight_prep_launch(const float* w, int G, int Cn, int T, int Cr, bf16* wb, bf16* wt,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(grid_cap((size_t)G * Cn * T * Cr)), dim3(256), 0, st, w,
+                     G, Cn, T, Cr, wb, wt);
+}
+
+}  // namespace pca

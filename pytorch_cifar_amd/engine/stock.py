@@ -1,0 +1,74 @@
+"""Like-for-like comparator: the reference training step on stock PyTorch-ROCm.
+
+What main_dist.py runs per step (SGD 0.9/5e-4, CE, autocast) with the library kernels PyTorch
+ships for ROCm (MIOpen convolutions/BN, hipBLASLt linear, RCCL DDP), in the best stock
+configuration: channels_last + bf16 autocast, synthetic batches already on the GPU. Used by
+``bench.py --baseline`` to put our number next to the stock one measured on the same box.
+The network is built from torch.nn layers with the CIFAR ResNet topology of models/resnet.py.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _cbr(cin, cout, k, s):
+    return nn.Sequential(nn.Conv2d(cin, cout, k, s, k // 2, bias=False), nn.BatchNorm2d(cout))
+
+
+class _Res(nn.Module):
+    def __init__(self, cin, cout, s):
+        super().__init__()
+        self.a = _cbr(cin, cout, 3, s)
+        self.b = _cbr(cout, cout, 3, 1)
+        self.proj = _cbr(cin, cout, 1, s) if (s != 1 or cin != cout) else None
+
+    def forward(self, x):
+        y = self.b(F.relu(self.a(x)))
+        return F.relu(y + (self.proj(x) if self.proj is not None else x))
+
+
+def stock_resnet18(num_classes=10):
+    widths, blocks = (64, 128, 256, 512), (2, 2, 2, 2)
+    layers, cin = [_cbr(3, 64, 3, 1), nn.ReLU()], 64
+    for i, (w, n) in enumerate(zip(widths, blocks)):
+        for j in range(n):
+            layers.append(_Res(cin, w, 2 if (j == 0 and i > 0) else 1))
+            cin = w
+    layers += [nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(512, num_classes)]
+    return nn.Sequential(*layers)
+
+
+def build_stock_step(model_name, per_rank_batch, device, ctx, images, labels):
+    if model_name != "ResNet18":
+        raise ValueError("stock comparator implements ResNet18 only")
+    torch.manual_seed(0)
+    net = stock_resnet18().to(device).to(memory_format=torch.channels_last)
+    model = net
+    if ctx.world > 1:
+        model = nn.parallel.DistributedDataParallel(net, device_ids=[device.index])
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4)
+    torch.backends.cudnn.benchmark = True
+    mean = torch.tensor((0.4914, 0.4822, 0.4465), device=device).view(1, 3, 1, 1)
+    std = torch.tensor((0.2023, 0.1994, 0.2010), device=device).view(1, 3, 1, 1)
+    imgs = torch.from_numpy(images).to(device)
+    labs = torch.from_numpy(labels).to(device)
+    n = imgs.shape[0]
+    state = {"i": 0}
+
+    def run():
+        i = state["i"]
+        idx = torch.arange(i, i + per_rank_batch, device=device) % n
+        state["i"] = (i + per_rank_batch) % n
+        x = imgs.index_select(0, idx).permute(0, 3, 1, 2).float().div_(255)
+        x = ((x - mean) / std).contiguous(memory_format=torch.channels_last)
+        y = labs.index_select(0, idx)
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+            loss = F.cross_entropy(out, y)
+        loss.backward()
+        opt.step()
+
+    return run, {"comparator": "torch.nn + MIOpen + autocast bf16 + channels_last"}

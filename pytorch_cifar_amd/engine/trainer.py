@@ -1,0 +1,161 @@
+"""Training engine: the step, hipGraph capture, epoch loops and on-device metrics.
+
+Reference loop (main.py:93-113, main_dist.py:166-202): per batch ``zero_grad -> net(x) -> CE ->
+backward -> step`` and two ``.item()`` host syncs per step for the running loss/accuracy.
+
+Here a step is: on-device batch gather+augment, forward, fused CE (which also accumulates loss
+sum / correct / count in an fp64 device buffer), backward (native kernels write gradients into
+the flat arena, RCCL buckets overlap), one SGD launch.  No host sync per step; the metrics buffer
+is read once per log interval. With ``graph=True`` the whole step is captured once into a
+hipGraph (``torch.cuda.CUDAGraph`` on ROCm = hipGraph) and replayed: the batch indices are
+copied into a static buffer before each replay and the learning rate lives in a device scalar,
+so one capture serves the whole run.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..ops.functional import cross_entropy
+
+
+class TrainStep:
+    def __init__(self, net, optimizer, loader, batch_size, ddp=None, graph=False, metrics=None):
+        self.net = net
+        self.opt = optimizer
+        self.loader = loader
+        self.B = batch_size
+        self.ddp = ddp
+        self.device = loader.device
+        self.metrics = metrics if metrics is not None else torch.zeros(3, dtype=torch.float64, device=self.device)
+        self.graph_requested = graph and self.device.type == "cuda"
+        self.graph = None
+        self.static_idx = torch.zeros(batch_size, dtype=torch.int64, device=self.device)
+        self.last_loss = None
+        self.graph_error = None
+
+    # one eager step on a given index batch
+    def _body(self, idx):
+        x, y = self.loader.make_batch(idx)
+        self.opt.zero_grad()
+        out = self.net(x)
+        loss = cross_entropy(out, y, self.metrics)
+        loss.backward()
+        if self.ddp is not None:
+            self.ddp.finish()
+        self.opt.step()
+        return loss
+
+    def _capture(self):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                self._body(self.static_idx)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        self.opt.capturing = True
+        self.loader.graph_safe_rng = True
+        try:
+            with torch.cuda.graph(g):
+                self.static_loss = self._body(self.static_idx)
+        finally:
+            self.opt.capturing = False
+        self.graph = g
+
+    def __call__(self, idx: torch.Tensor):
+        """Run one training step on the sample indices ``idx`` (device int64)."""
+        full = idx.numel() == self.B
+        if self.graph_requested and full:
+            if self.graph is None and self.graph_error is None:
+                try:
+                    self.static_idx.copy_(idx)
+                    self._capture()
+                except Exception as e:  # capture unsupported -> stay eager
+                    self.graph_error = e
+                    self.graph = None
+                    torch.cuda.synchronize()
+            if self.graph is not None:
+                self.static_idx.copy_(idx)
+                self.opt.sync_lr()
+                self.graph.replay()
+                self.last_loss = self.static_loss
+                return self.last_loss
+        self.last_loss = self._body(idx)
+        return self.last_loss
+
+
+def read_metrics(metrics: torch.Tensor, reset: bool = True):
+    """(mean loss per step, correct, total) from the device accumulator (one host sync)."""
+    m = metrics.tolist()
+    if reset:
+        metrics.zero_()
+    return m
+
+
+def build_bench_step(model_name, per_rank_batch, device, ctx, graph=True, baseline=False,
+                     bucket_mb=25.0, n_images=50000):
+    """Closure running one timed training step of the headline benchmark + metadata."""
+    from ..data.loader import DeviceLoader
+    from ..data.synthetic import synthetic_cifar10
+
+    images, labels = synthetic_cifar10(n_images, seed=1234)
+    if baseline:
+        from .stock import build_stock_step
+
+        return build_stock_step(model_name, per_rank_batch, device, ctx, images, labels)
+
+    from .. import models
+    from .arena import ParamArena
+    from .optim import SGD
+
+    torch.manual_seed(0)
+    model = getattr(models, model_name)().to(device)
+    arena = ParamArena(model.parameters())
+    opt = SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4).attach_arena(arena)
+    ddp = None
+    net = model
+    if ctx.world > 1:
+        from ..parallel.ddp import DistributedDataParallel
+
+        ddp = DistributedDataParallel(model, ctx, bucket_cap_mb=bucket_mb, arena=arena)
+        net = ddp
+    loader = DeviceLoader(images, labels, per_rank_batch, device, train=True, crop_pad=4, flip=True,
+                          world=ctx.world, rank=ctx.rank, seed=0, drop_last=True)
+    step = TrainStep(net, opt, loader, per_rank_batch, ddp=ddp, graph=graph)
+    state = {"it": None, "epoch": 0}
+
+    def next_idx():
+        while True:
+            if state["it"] is None:
+                loader.set_epoch(state["epoch"])
+                state["it"] = iter(loader.batch_indices())
+            try:
+                idx = next(state["it"])
+                if idx.numel() == per_rank_batch:
+                    return idx
+            except StopIteration:
+                state["it"] = None
+                state["epoch"] += 1
+
+    def run():
+        step(next_idx())
+
+    meta = {"buckets_mib": ddp.bucket_sizes_mib() if ddp else None}
+
+    def info():
+        return {"graph_captured": step.graph is not None,
+                "graph_error": repr(step.graph_error) if step.graph_error else None}
+
+    run.info = info
+    return run, meta
+
+
+class EpochTimer:
+    def __init__(self):
+        self.t0 = time.perf_counter()
+
+    def elapsed(self):
+        return time.perf_counter() - self.t0

@@ -1,0 +1,99 @@
+"""Layer modules of the model zoo.
+
+Subclasses of the torch.nn layers so parameter/buffer names, shapes, default initialisation and
+``state_dict`` keys are exactly those of the reference models (``conv1.weight``,
+``bn1.running_mean``, ``shortcut.0.weight`` ...), while ``forward`` routes through the fused
+gfx950 ops of :mod:`pytorch_cifar_amd.ops.functional`:
+
+* ``Conv2d`` keeps its weight channels_last (physically [Cout][KH][KW][Cin/G], the MFMA B
+  operand) and, in training mode, asks the kernel for per-channel BatchNorm partial sums in its
+  epilogue; they ride on the output tensor to the ``BatchNorm2d`` that consumes it.
+* ``BatchNorm2d.forward(x, act=..., residual=..., residual_bn=...)`` is one fused
+  normalize + residual + activation pass (plain ``bn(x)`` still works).
+* ``Sequential`` fuses ``BatchNorm2d`` → ``ReLU`` pairs (the VGG/GoogLeNet/DLA stems).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops import functional as OF
+
+_STATS_ATTR = "_pca_stats"
+
+
+class Conv2d(nn.Conv2d):
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        if self.dilation not in ((1, 1), 1):
+            raise NotImplementedError("dilated convolutions are not used by the CIFAR zoo")
+        if self.padding_mode != "zeros":
+            raise NotImplementedError("only zero padding")
+        with torch.no_grad():
+            self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
+
+    def forward(self, x, want_stats=None):
+        if want_stats is None:
+            want_stats = self.training
+        y, stats = OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.groups,
+                             bool(want_stats and x.is_cuda))
+        if stats is not None:
+            setattr(y, _STATS_ATTR, stats)
+        return y
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+        # load_state_dict copies values into the existing (channels_last) storage; nothing else
+        # to do, but keep the layout invariant explicit for parameters replaced wholesale.
+        if not self.weight.is_contiguous(memory_format=torch.channels_last):
+            with torch.no_grad():
+                self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    def forward(self, x, act=None, residual=None, residual_bn=None):
+        stats = getattr(x, _STATS_ATTR, None) if self.training else None
+        rb = None
+        if residual_bn is not None:
+            bn_b, xb = residual_bn
+            rb = (bn_b, xb, getattr(xb, _STATS_ATTR, None) if bn_b.training else None)
+        return OF.batch_norm_act(self, x, act, residual, rb, stats)
+
+
+class Linear(nn.Linear):
+    def forward(self, x):
+        if x.dtype != self.weight.dtype:
+            x = x.to(self.weight.dtype)
+        return nn.functional.linear(x, self.weight, self.bias)
+
+
+class ReLU(nn.ReLU):
+    def forward(self, x):
+        return OF.relu(x)
+
+
+class MaxPool2d(nn.MaxPool2d):
+    def forward(self, x):
+        return OF.max_pool2d(x, self.kernel_size, self.stride, self.padding)
+
+
+class AvgPool2d(nn.AvgPool2d):
+    def forward(self, x):
+        return OF.avg_pool2d(x, self.kernel_size, self.stride, self.padding)
+
+
+class Sequential(nn.Sequential):
+    """nn.Sequential that fuses BatchNorm2d -> ReLU into one kernel pass."""
+
+    def forward(self, x):
+        mods = list(self._modules.values())
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if isinstance(m, BatchNorm2d) and i + 1 < len(mods) and isinstance(mods[i + 1], (ReLU, nn.ReLU)):
+                x = m(x, act="relu")
+                i += 2
+                continue
+            x = m(x)
+            i += 1
+        return x

@@ -1,0 +1,577 @@
+"""Autograd wiring of the native gfx950 kernels.
+
+Tensor convention: activations are NCHW-shaped tensors whose memory is NHWC (torch
+``channels_last``) bf16 on the GPU, so ``x.permute(0, 2, 3, 1)`` is the contiguous [N,H,W,C]
+matrix the kernels consume and the model code keeps the reference's NCHW indexing
+(``torch.cat(dim=1)``, ``x[:, :c]``, ``out.view(N, -1)``).  CPU tensors take the pure PyTorch
+reference path with identical semantics (used by the CPU tests and the LeNet CPU config).
+
+Every GPU op here calls the extension; nothing silently falls back to stock PyTorch kernels
+except pure data movement (cat/slice/shuffle views) which has no arithmetic.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native
+from ..engine import grads as G
+
+ACT = {None: 0, "none": 0, "relu": 1, "swish": 2, "silu": 2, "sigmoid": 3}
+COMPUTE_DTYPE = torch.bfloat16
+
+
+def _C():
+    return _native.lib()
+
+
+# ------------------------------------------------------------------------------- layout
+def to_nhwc(x: torch.Tensor, pad_to: int | None = None) -> torch.Tensor:
+    """Contiguous NHWC bf16 [N,H,W,C'] view/copy of an NCHW-shaped tensor (C' >= C if padded)."""
+    N, C, H, W = x.shape
+    if pad_to is not None and pad_to != C:
+        # channel-padded storage produced by the loader / a previous pad: reuse it
+        base = getattr(x, "_pca_padded", None)
+        if base is not None and base.shape[-1] == pad_to:
+            return base
+        if x.dtype == torch.float32 and x.is_contiguous():
+            return _C().nchw_to_nhwc(x, pad_to)
+        v = to_nhwc(x)
+        return F.pad(v, (0, pad_to - C))
+    v = x.permute(0, 2, 3, 1)
+    if v.dtype == COMPUTE_DTYPE and v.is_contiguous():
+        return v
+    if x.dtype == torch.float32 and x.is_contiguous():
+        return _C().nchw_to_nhwc(x, C)
+    out = torch.empty((N, H, W, C), dtype=COMPUTE_DTYPE, device=x.device)
+    out.copy_(v)
+    return out
+
+
+def to_nchw(y: torch.Tensor) -> torch.Tensor:
+    """NCHW-shaped channels_last view of an NHWC tensor (no copy)."""
+    return y.permute(0, 3, 1, 2)
+
+
+def padded_input(x_nhwc_padded: torch.Tensor, C: int) -> torch.Tensor:
+    """Wrap a channel-padded NHWC buffer as an NCHW-shaped tensor with ``C`` visible channels.
+
+    The returned tensor remembers its padded storage so the first conv can consume it without a
+    copy (the GPU augmentation kernel writes 3 RGB channels into 8-channel pixels).
+    """
+    v = to_nchw(x_nhwc_padded)[:, :C]
+    v._pca_padded = x_nhwc_padded
+    return v
+
+
+# ------------------------------------------------------------------------------- conv
+def _round8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+class _ConvMFMA(torch.autograd.Function):
+    """Implicit-GEMM MFMA conv (fwd + BN-stat epilogue, dgrad, split-K wgrad)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, groups, want_stats, cin_pad):
+        C = _C()
+        w_phys = G.physical(weight)
+        if not w_phys.is_contiguous():
+            w_phys = w_phys.contiguous()
+        if cin_pad:
+            w_phys = F.pad(w_phys, (0, cin_pad - w_phys.shape[-1]))
+        need_dx = ctx.needs_input_grad[0]
+        wb, wt = C.weight_prep(w_phys, groups, need_dx)
+        y, stats = C.conv_fwd(x, wb, bias, stride, padding, groups, want_stats)
+        ctx.geom = (stride, padding, groups, cin_pad, x.shape[1], x.shape[2])
+        ctx.save_for_backward(x, wt if need_dx else None)
+        ctx.weight = weight
+        ctx.bias = bias
+        if stats is None or not want_stats:
+            stats = torch.empty(0, device=x.device)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        C = _C()
+        x, wt = ctx.saved_tensors
+        stride, padding, groups, cin_pad, H, W = ctx.geom
+        dy = dy.contiguous()
+        weight, bias = ctx.weight, ctx.bias
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
+        KH, KW = weight.shape[2], weight.shape[3]
+        if weight.requires_grad:
+            buf = None if cin_pad else G.grad_buffer(weight)
+            if buf is not None:
+                C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, buf)
+                G.fire(weight)
+            else:
+                dw = C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, None)
+                if cin_pad:
+                    dw = dw[..., : weight.shape[1]]
+                G.accumulate(weight, dw)
+        if bias is not None and bias.requires_grad:
+            G.accumulate(bias, C.bn_stats(dy)[:, 0].sum(0))
+        return dx, None, None, None, None, None, None, None
+
+
+class _ConvDirect(torch.autograd.Function):
+    """Generic direct conv for odd channel counts / tiny groups (LeNet, DPN, PNASNet-A...)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, groups):
+        C = _C()
+        w_phys = G.physical(weight).contiguous()
+        y = C.direct_fwd(x, w_phys, bias, stride, padding, groups)
+        ctx.save_for_backward(x, w_phys)
+        ctx.geom = (stride, padding, groups)
+        ctx.weight, ctx.bias = weight, bias
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        x, w_phys = ctx.saved_tensors
+        stride, padding, groups = ctx.geom
+        dy = dy.contiguous()
+        weight, bias = ctx.weight, ctx.bias
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = C.direct_dgrad(dy, w_phys, x.shape[1], x.shape[2], stride, padding, groups)
+        with_bias = bias is not None and bias.requires_grad
+        if weight.requires_grad or with_bias:
+            flat = C.direct_wgrad(x, dy, weight.shape[2], weight.shape[3], stride, padding, groups, with_bias)
+            nw = w_phys.numel()
+            if weight.requires_grad:
+                G.accumulate(weight, flat[:nw].view_as(w_phys))
+            if with_bias:
+                G.accumulate(bias, flat[nw:])
+        return dx, None, None, None, None, None
+
+
+class _ConvDepthwise(torch.autograd.Function):
+    """Depthwise conv (groups == Cin, multiplier Cout/Cin), bandwidth-bound direct kernels."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding):
+        C = _C()
+        Co, _, KH, KW = weight.shape
+        wT = weight.detach().reshape(Co, KH * KW).t().contiguous()
+        y = C.dw_fwd(x, wT, KH, KW, stride, padding)
+        ctx.save_for_backward(x, wT)
+        ctx.geom = (stride, padding, KH, KW)
+        ctx.weight = weight
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        x, wT = ctx.saved_tensors
+        stride, padding, KH, KW = ctx.geom
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = C.dw_dgrad(dy, wT, x.shape[1], x.shape[2], x.shape[3], KH, KW, stride, padding)
+        w = ctx.weight
+        if w.requires_grad:
+            dw = C.dw_wgrad(x, dy, KH, KW, stride, padding)  # [Co, KH*KW]
+            G.accumulate(w, dw.view(w.shape[0], KH, KW, 1))
+        return dx, None, None, None
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False):
+    """NCHW-shaped conv. On GPU returns (y, stats) where stats are BN partials (or None)."""
+    if isinstance(stride, (tuple, list)):
+        assert stride[0] == stride[1]
+        stride = stride[0]
+    if isinstance(padding, (tuple, list)):
+        assert padding[0] == padding[1]
+        padding = padding[0]
+    if not x.is_cuda:
+        return F.conv2d(x, weight, bias, stride, padding, 1, groups), None
+    Cout, Cg, KH, KW = weight.shape
+    Cin = x.shape[1]
+    cout_g = Cout // groups
+    if groups > 1 and groups == Cin and Cg == 1:
+        y = _ConvDepthwise.apply(to_nhwc(x), weight, stride, padding)
+        if bias is not None:
+            y = add_bias(y, bias)
+        return to_nchw(y), None
+    if Cg % 8 == 0 and cout_g % 8 == 0:
+        y, stats = _ConvMFMA.apply(to_nhwc(x), weight, bias, stride, padding, groups, want_stats, 0)
+        return to_nchw(y), (stats if want_stats else None)
+    if groups == 1 and cout_g % 8 == 0 and Cin < 8 * 2 and Cout >= 16:
+        # stem conv on 3-channel images: pad channels to 8 and run on MFMA
+        cp = _round8(Cin)
+        y, stats = _ConvMFMA.apply(to_nhwc(x, pad_to=cp), weight, bias, stride, padding, groups, want_stats, cp)
+        return to_nchw(y), (stats if want_stats else None)
+    y = _ConvDirect.apply(to_nhwc(x), weight, bias, stride, padding, groups)
+    return to_nchw(y), None
+
+
+class _AddBias(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, bias):
+        ctx.bias = bias
+        return (y.float() + bias).to(y.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        b = ctx.bias
+        if b.requires_grad:
+            G.accumulate(b, _C().bn_stats(dy.contiguous())[:, 0].sum(0))
+        return dy, None
+
+
+def add_bias(y_nhwc, bias):
+    return _AddBias.apply(y_nhwc, bias)
+
+
+# -------------------------------------------------------------------------- batch norm
+class _BNCfg:
+    __slots__ = ("bn", "bn2", "act", "training", "count")
+
+    def __init__(self, bn, bn2, act, training, count):
+        self.bn, self.bn2, self.act, self.training, self.count = bn, bn2, act, training, count
+
+
+def _bn_aux(C, bn, y, stats, training, count):
+    use_batch = training or bn.running_mean is None
+    rm = bn.running_mean
+    rv = bn.running_var
+    if rm is None:
+        rm = torch.zeros(y.shape[-1], device=y.device)
+        rv = torch.ones(y.shape[-1], device=y.device)
+    update = training and bn.running_mean is not None
+    if use_batch and stats is None:
+        stats = C.bn_stats(y)
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    w = bn.weight.detach() if bn.weight is not None else None
+    b = bn.bias.detach() if bn.bias is not None else None
+    return C.bn_finalize(stats if use_batch else None, float(count), w, b, rm, rv,
+                         bn.num_batches_tracked if update else None, momentum, bn.eps, use_batch, update)
+
+
+class _BatchNormAct(torch.autograd.Function):
+    """out = act(BN(y) [+ residual | + BN2(y2)]) with stats from the conv epilogue when given."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, res, y2, gamma2, beta2, stats, stats2, cfg):
+        C = _C()
+        aux = _bn_aux(C, cfg.bn, y, stats if stats is not None and stats.numel() else None, cfg.training, cfg.count)
+        aux2 = None
+        if y2 is not None:
+            aux2 = _bn_aux(C, cfg.bn2, y2, stats2 if stats2 is not None and stats2.numel() else None, cfg.training, cfg.count)
+        out = C.bn_apply(y, aux, res, y2, aux2, ACT[cfg.act])
+        ctx.cfg = cfg
+        ctx.has_res = res is not None
+        ctx.save_for_backward(y, out if ACT[cfg.act] == 1 else None, aux, y2, aux2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = _C()
+        y, out, aux, y2, aux2 = ctx.saved_tensors
+        cfg = ctx.cfg
+        bn, bn2 = cfg.bn, cfg.bn2
+        dout = dout.contiguous()
+
+        def acc(p):
+            if p is None or not p.requires_grad:
+                return None
+            return G.grad_buffer(p)
+
+        g1, b1 = acc(bn.weight), acc(bn.bias)
+        g2 = b2 = None
+        if bn2 is not None:
+            g2, b2 = acc(bn2.weight), acc(bn2.bias)
+        dy, dres, dy2, dg, db, dg2, db2 = C.bn_backward(
+            dout, out, y, aux,
+            bn.weight.detach() if bn.weight is not None else None,
+            y2, aux2,
+            bn2.weight.detach() if (bn2 is not None and bn2.weight is not None) else None,
+            ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2)
+        for p, buf, val in ((bn.weight, g1, dg), (bn.bias, b1, db)):
+            if p is not None and p.requires_grad:
+                G.fire(p) if buf is not None else G.accumulate(p, val)
+        if bn2 is not None:
+            for p, buf, val in ((bn2.weight, g2, dg2), (bn2.bias, b2, db2)):
+                if p is not None and p.requires_grad:
+                    G.fire(p) if buf is not None else G.accumulate(p, val)
+        return (dy, None, None, dres if ctx.has_res else None, dy2 if y2 is not None else None,
+                None, None, None, None, None)
+
+
+def _ref_bn(bn, x, training):
+    return F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                        training or bn.running_mean is None,
+                        bn.momentum if bn.momentum is not None else 0.1, bn.eps)
+
+
+def _ref_act(x, act):
+    if act in (None, "none"):
+        return x
+    if act == "relu":
+        return F.relu(x)
+    if act in ("swish", "silu"):
+        return x * torch.sigmoid(x)
+    if act == "sigmoid":
+        return torch.sigmoid(x)
+    raise ValueError(act)
+
+
+def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None):
+    """act(BN(x) [+ residual] [+ BN_b(x_b)]) — the fused block tail of the model zoo.
+
+    ``residual_bn=(bn_b, x_b, stats_b)`` fuses a projection-shortcut BatchNorm into the same pass
+    (resnet.py:47-51 with the 1x1 conv shortcut of resnet.py:31-36).
+    """
+    training = bn.training
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None and not x.is_cuda:
+        bn.num_batches_tracked.add_(1)
+        if residual_bn is not None and residual_bn[0].num_batches_tracked is not None:
+            residual_bn[0].num_batches_tracked.add_(1)
+    if not x.is_cuda:
+        out = _ref_bn(bn, x, training)
+        if residual is not None:
+            out = out + residual
+        if residual_bn is not None:
+            out = out + _ref_bn(residual_bn[0], residual_bn[1], residual_bn[0].training)
+        return _ref_act(out, act)
+    if ACT[act] >= 2 and (residual is not None or residual_bn is not None):
+        # swish/sigmoid backward recomputes z from y alone: keep the residual out of the fusion
+        out = batch_norm_act(bn, x, None, residual, residual_bn, stats)
+        return activation(out, act)
+    N, Cc, H, W = x.shape
+    y = to_nhwc(x)
+    res = to_nhwc(residual) if residual is not None else None
+    y2 = st2 = bn2 = None
+    if residual_bn is not None:
+        bn2, xb = residual_bn[0], residual_bn[1]
+        st2 = residual_bn[2] if len(residual_bn) > 2 else None
+        y2 = to_nhwc(xb)
+    cfg = _BNCfg(bn, bn2, act, training, N * H * W)
+    out = _BatchNormAct.apply(y, bn.weight, bn.bias, res, y2,
+                              bn2.weight if bn2 is not None else None,
+                              bn2.bias if bn2 is not None else None, stats, st2, cfg)
+    return to_nchw(out)
+
+
+# ------------------------------------------------------------------------ activations
+class _Act(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        ctx.act = act
+        ctx.save_for_backward(x)
+        return _C().act_fwd(x, act)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return _C().act_bwd(dy.contiguous(), x, ctx.act), None
+
+
+def activation(x, act):
+    if act in (None, "none"):
+        return x
+    if not x.is_cuda:
+        return _ref_act(x, act)
+    return to_nchw(_Act.apply(to_nhwc(x), ACT[act]))
+
+
+def relu(x):
+    return activation(x, "relu")
+
+
+class _AddAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, act):
+        y = _C().add_act(a, b, act)
+        ctx.act = act
+        ctx.save_for_backward(y if act == 1 else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        if ctx.act == 0:
+            return dy, dy, None
+        (y,) = ctx.saved_tensors
+        d = _C().act_bwd(dy, y, 1)
+        return d, d, None
+
+
+def add_act(a, b, act=None):
+    """act(a + b) — the un-fused residual join (PNASNet cells, DPN, ShuffleNet)."""
+    if not a.is_cuda:
+        return _ref_act(a + b, act)
+    if ACT[act] not in (0, 1):
+        return activation(add_act(a, b, None), act)
+    return to_nchw(_AddAct.apply(to_nhwc(a), to_nhwc(b), ACT[act]))
+
+
+# ---------------------------------------------------------------------------- pooling
+class _GAP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[1], x.shape[2])
+        return _C().gap_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _C().gap_bwd(dy.contiguous().float(), *ctx.hw)
+
+
+def global_avg_pool(x):
+    """[N,C,H,W] -> fp32 [N,C,1,1] (head / SE squeeze)."""
+    if not x.is_cuda:
+        return F.adaptive_avg_pool2d(x, 1)
+    return _GAP.apply(to_nhwc(x)).view(x.shape[0], x.shape[1], 1, 1)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        ctx.cfg = (x.shape[1], x.shape[2], k, s, p)
+        return _C().avgpool_fwd(x, k, s, p)
+
+    @staticmethod
+    def backward(ctx, dy):
+        H, W, k, s, p = ctx.cfg
+        return _C().avgpool_bwd(dy.contiguous(), H, W, k, s, p), None, None, None
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, arg = _C().maxpool_fwd(x, k, s, p)
+        ctx.cfg = (x.shape[1], x.shape[2], k, s, p)
+        ctx.save_for_backward(arg)
+        ctx.mark_non_differentiable(arg)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        H, W, k, s, p = ctx.cfg
+        return _C().maxpool_bwd(dy.contiguous(), arg, H, W, k, s, p), None, None, None
+
+
+def _pair1(v):
+    if isinstance(v, (tuple, list)):
+        assert v[0] == v[1], "only square pooling windows"
+        return v[0]
+    return v
+
+
+def avg_pool2d(x, kernel_size, stride=None, padding=0):
+    k = _pair1(kernel_size)
+    s = _pair1(stride) if stride is not None else k
+    p = _pair1(padding)
+    if not x.is_cuda:
+        return F.avg_pool2d(x, k, s, p)
+    H, W = x.shape[2], x.shape[3]
+    if p == 0 and k == H and k == W:
+        return global_avg_pool(x)
+    if k == 1 and s == 1 and p == 0:
+        return x
+    return to_nchw(_AvgPool.apply(to_nhwc(x), k, s, p))
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0):
+    k = _pair1(kernel_size)
+    s = _pair1(stride) if stride is not None else k
+    p = _pair1(padding)
+    if not x.is_cuda:
+        return F.max_pool2d(x, k, s, p)
+    return to_nchw(_MaxPool.apply(to_nhwc(x), k, s, p))
+
+
+def adaptive_avg_pool2d(x, output_size):
+    o = _pair1(output_size)
+    assert o == 1, "only global adaptive pooling is used by the zoo"
+    return global_avg_pool(x)
+
+
+# ------------------------------------------------------------------------ squeeze-excite
+class _SEScale(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.save_for_backward(x, s)
+        return _C().se_scale_fwd(x, s)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, s = ctx.saved_tensors
+        dx, ds = _C().se_scale_bwd(dy.contiguous(), x, s)
+        return dx, ds
+
+
+def se_excite(x, s_logits):
+    """x * sigmoid(s) with s = per-(n, c) excitation logits [N, C] (fp32)."""
+    if not x.is_cuda:
+        return x * torch.sigmoid(s_logits).view(x.shape[0], x.shape[1], 1, 1)
+    s = s_logits.reshape(x.shape[0], x.shape[1]).float().contiguous()
+    return to_nchw(_SEScale.apply(to_nhwc(x), s))
+
+
+# ------------------------------------------------------------------------ cross-entropy
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, metrics):
+        loss, dl = _C().ce_fused(logits, target, metrics, True)
+        ctx.save_for_backward(dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (dl,) = ctx.saved_tensors
+        return _C().scale_by_scalar(dl, dloss.float().reshape(1).contiguous()), None, None
+
+
+def cross_entropy(logits, target, metrics=None):
+    """Mean CE; ``metrics`` (fp64 [3] on device) accumulates (loss, correct, count) with no sync."""
+    if not logits.is_cuda:
+        loss = F.cross_entropy(logits.float(), target)
+        if metrics is not None:
+            with torch.no_grad():
+                metrics[0] += loss.double()
+                metrics[1] += (logits.argmax(1) == target).sum().double()
+                metrics[2] += target.numel()
+        return loss
+    logits = logits.float().contiguous()
+    if torch.is_grad_enabled() and logits.requires_grad:
+        return _CrossEntropy.apply(logits, target, metrics)
+    loss, _ = _C().ce_fused(logits, target, metrics, False)
+    return loss
+
+
+def dropout(x, p, training):
+    if not training or p == 0:
+        return x
+    return F.dropout(x, p=p, training=True)
+
+
+def channel_shuffle(x, groups):
+    """[N,C,H,W] -> [N,g,C/g,H,W] -> transpose -> [N,C,H,W] (shufflenet*.py ShuffleBlock)."""
+    N, C, H, W = x.shape
+    out = x.reshape(N, groups, C // groups, H, W).transpose(1, 2).reshape(N, C, H, W)
+    if out.is_cuda:
+        out = out.contiguous(memory_format=torch.channels_last)
+    return out
+
+
+def cat(xs, dim=1):
+    out = torch.cat(xs, dim)
+    if out.is_cuda and out.dim() == 4:
+        out = out.contiguous(memory_format=torch.channels_last)
+    return out
+
+
+def kaiming_fan_in_bound(fan_in: int) -> float:
+    return 1.0 / math.sqrt(fan_in) if fan_in > 0 else 0.0

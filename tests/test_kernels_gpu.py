@@ -1,0 +1,264 @@
+"""Numerics of every hand-written gfx950 kernel against a plain PyTorch fp32 reference.
+
+The kernels are called through the raw extension (``pytorch_cifar_amd._C``) so a failure
+points at the kernel, not at the autograd wiring (that is covered by test_ops_gpu.py).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def C():
+    from pytorch_cifar_amd import _native
+
+    return _native.lib()
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+CONV_CASES = [
+    # N, Cin, H, Cout, k, s, p, groups
+    (4, 64, 32, 64, 3, 1, 1, 1),
+    (2, 64, 32, 128, 3, 2, 1, 1),
+    (2, 64, 32, 128, 1, 2, 0, 1),
+    (3, 8, 32, 64, 3, 1, 1, 1),
+    (3, 32, 16, 96, 3, 1, 1, 1),
+    (2, 128, 8, 256, 3, 1, 1, 1),
+    (5, 256, 4, 512, 3, 1, 1, 1),
+    (2, 64, 16, 64, 3, 1, 1, 2),
+    (2, 32, 8, 32, 3, 2, 1, 4),
+    (2, 96, 8, 576, 1, 1, 0, 1),
+    (2, 24, 16, 16, 1, 1, 0, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(C, case):
+    N, Cin, H, Cout, k, s, p, G = case
+    torch.manual_seed(0)
+    x = bf(torch.randn(N, Cin, H, H, device="cuda"))
+    w = bf(torch.randn(Cout, Cin // G, k, k, device="cuda") * (2.0 / (Cin // G * k * k)) ** 0.5)
+    x.requires_grad_(True)
+    w.requires_grad_(True)
+    ref = F.conv2d(x, w, stride=s, padding=p, groups=G)
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+
+    x_n = nhwc(x.detach()).to(torch.bfloat16)
+    w_p = w.detach().permute(0, 2, 3, 1).contiguous()  # [Cout, KH, KW, Cin/G] fp32
+    wb, wt = C.weight_prep(w_p, G, True)
+    y, stats = C.conv_fwd(x_n, wb, None, s, p, G, True)
+    assert rel_err(nchw(y), ref) < 2e-2
+    ssum = stats[:, 0, :].sum(0)
+    ssq = stats[:, 1, :].sum(0)
+    assert rel_err(ssum, ref.detach().sum((0, 2, 3))) < 2e-3 + 1e-2
+    assert rel_err(ssq, (ref.detach() ** 2).sum((0, 2, 3))) < 1e-2
+
+    dy_n = nhwc(dy).to(torch.bfloat16)
+    dx = C.conv_dgrad(dy_n, wt, H, H, s, p, G)
+    assert rel_err(nchw(dx), x.grad) < 2e-2
+    dw = C.conv_wgrad(x_n, dy_n, k, k, s, p, G, None)
+    assert rel_err(dw.permute(0, 3, 1, 2), w.grad) < 2e-2
+
+
+@pytest.mark.parametrize("C_,act,res", [(64, 1, False), (64, 1, True), (24, 0, False), (116, 1, True), (96, 2, False)])
+def test_bn_fwd_bwd(C, C_, act, res):
+    torch.manual_seed(1)
+    N, H = 4, 8
+    y = bf(torch.randn(N, C_, H, H, device="cuda") * 2 + 0.5).requires_grad_(True)
+    r = bf(torch.randn(N, C_, H, H, device="cuda")).requires_grad_(True) if res else None
+    gamma = torch.rand(C_, device="cuda").add_(0.5).requires_grad_(True)
+    beta = torch.randn(C_, device="cuda").requires_grad_(True)
+    rm_ref = torch.zeros(C_, device="cuda")
+    rv_ref = torch.ones(C_, device="cuda")
+    z = F.batch_norm(y, rm_ref, rv_ref, gamma, beta, training=True, momentum=0.1, eps=1e-5)
+    if res:
+        z = z + r
+    out_ref = F.relu(z) if act == 1 else (F.silu(z) if act == 2 else z)
+    dout = bf(torch.randn_like(out_ref))
+    out_ref.backward(dout)
+
+    yn = nhwc(y.detach()).to(torch.bfloat16)
+    rn = nhwc(r.detach()).to(torch.bfloat16) if res else None
+    rm = torch.zeros(C_, device="cuda")
+    rv = torch.ones(C_, device="cuda")
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    partial = C.bn_stats(yn)
+    aux = C.bn_finalize(partial, float(N * H * H), gamma.detach(), beta.detach(), rm, rv, nbt, 0.1, 1e-5, True, True)
+    out = C.bn_apply(yn, aux, rn, None, None, act)
+    assert rel_err(nchw(out), out_ref) < 2e-2
+    assert rel_err(rm, rm_ref) < 1e-4 and rel_err(rv, rv_ref) < 1e-4
+    assert nbt.item() == 1
+    dn = nhwc(dout).to(torch.bfloat16)
+    dy, dres, _, dg, db, _, _ = C.bn_backward(dn, out, yn, aux, gamma.detach(), None, None, None, act, True, res, None, None, None, None)
+    assert rel_err(nchw(dy), y.grad) < 3e-2
+    assert rel_err(dg, gamma.grad) < 1e-2
+    assert rel_err(db, beta.grad) < 1e-2
+    if res:
+        assert rel_err(nchw(dres), r.grad) < 2e-2
+
+
+def test_bn_dual_shortcut(C):
+    torch.manual_seed(2)
+    N, Ch, H = 4, 64, 8
+    y1 = bf(torch.randn(N, Ch, H, H, device="cuda")).requires_grad_(True)
+    y2 = bf(torch.randn(N, Ch, H, H, device="cuda") * 3).requires_grad_(True)
+    g1 = torch.rand(Ch, device="cuda").add_(0.5).requires_grad_(True)
+    b1 = torch.randn(Ch, device="cuda").requires_grad_(True)
+    g2 = torch.rand(Ch, device="cuda").add_(0.5).requires_grad_(True)
+    b2 = torch.randn(Ch, device="cuda").requires_grad_(True)
+    z = F.batch_norm(y1, None, None, g1, b1, training=True) + F.batch_norm(y2, None, None, g2, b2, training=True)
+    out_ref = F.relu(z)
+    dout = bf(torch.randn_like(out_ref))
+    out_ref.backward(dout)
+    cnt = float(N * H * H)
+    y1n, y2n = nhwc(y1.detach()).bfloat16(), nhwc(y2.detach()).bfloat16()
+    z_ = torch.zeros(Ch, device="cuda")
+    o_ = torch.ones(Ch, device="cuda")
+    a1 = C.bn_finalize(C.bn_stats(y1n), cnt, g1.detach(), b1.detach(), z_.clone(), o_.clone(), None, 0.1, 1e-5, True, False)
+    a2 = C.bn_finalize(C.bn_stats(y2n), cnt, g2.detach(), b2.detach(), z_.clone(), o_.clone(), None, 0.1, 1e-5, True, False)
+    out = C.bn_apply(y1n, a1, None, y2n, a2, 1)
+    assert rel_err(nchw(out), out_ref) < 2e-2
+    dy1, _, dy2, dg1, db1, dg2, db2 = C.bn_backward(nhwc(dout).bfloat16(), out, y1n, a1, g1.detach(), y2n, a2, g2.detach(), 1, True, False, None, None, None, None)
+    assert rel_err(nchw(dy1), y1.grad) < 3e-2
+    assert rel_err(nchw(dy2), y2.grad) < 3e-2
+    assert rel_err(dg1, g1.grad) < 1e-2 and rel_err(dg2, g2.grad) < 1e-2
+    assert rel_err(db1, b1.grad) < 1e-2 and rel_err(db2, b2.grad) < 1e-2
+
+
+def test_cross_entropy(C):
+    torch.manual_seed(3)
+    logits = torch.randn(300, 10, device="cuda").requires_grad_(True)
+    tgt = torch.randint(0, 10, (300,), device="cuda")
+    ref = F.cross_entropy(logits, tgt)
+    ref.backward()
+    metrics = torch.zeros(3, dtype=torch.float64, device="cuda")
+    loss, dl = C.ce_fused(logits.detach(), tgt, metrics, True)
+    assert abs(loss.item() - ref.item()) < 1e-4
+    assert rel_err(dl, logits.grad) < 1e-4
+    correct = (logits.argmax(1) == tgt).sum().item()
+    assert metrics[1].item() == correct and metrics[2].item() == 300
+
+
+def test_pools_and_gap(C):
+    torch.manual_seed(4)
+    x = bf(torch.randn(2, 16, 8, 8, device="cuda")).requires_grad_(True)
+    xn = nhwc(x.detach()).bfloat16()
+    for k, s, p in [(2, 2, 0), (3, 1, 1), (3, 2, 1)]:
+        ref = F.max_pool2d(x, k, s, p)
+        dy = bf(torch.randn_like(ref))
+        (g,) = torch.autograd.grad(ref, x, dy)
+        y, arg = C.maxpool_fwd(xn, k, s, p)
+        assert rel_err(nchw(y), ref) < 1e-2
+        dx = C.maxpool_bwd(nhwc(dy).bfloat16(), arg, 8, 8, k, s, p)
+        assert rel_err(nchw(dx), g) < 1e-2
+    for k, s, p in [(2, 2, 0), (4, 4, 0), (3, 2, 1)]:
+        ref = F.avg_pool2d(x, k, s, p)
+        dy = bf(torch.randn_like(ref))
+        (g,) = torch.autograd.grad(ref, x, dy)
+        y = C.avgpool_fwd(xn, k, s, p)
+        assert rel_err(nchw(y), ref) < 1e-2
+        dx = C.avgpool_bwd(nhwc(dy).bfloat16(), 8, 8, k, s, p)
+        assert rel_err(nchw(dx), g) < 1e-2
+    pooled = C.gap_fwd(xn)
+    assert rel_err(pooled, x.detach().mean((2, 3))) < 1e-2
+
+
+@pytest.mark.parametrize("Cin,mult,k,s", [(32, 1, 3, 1), (144, 1, 3, 2), (240, 1, 5, 1), (44, 2, 7, 2), (58, 1, 3, 2)])
+def test_depthwise(C, Cin, mult, k, s):
+    torch.manual_seed(5)
+    N, H = 2, 16
+    p = (k - 1) // 2
+    Co = Cin * mult
+    x = bf(torch.randn(N, Cin, H, H, device="cuda")).requires_grad_(True)
+    w = (torch.randn(Co, 1, k, k, device="cuda") * 0.3).requires_grad_(True)
+    ref = F.conv2d(x, w, stride=s, padding=p, groups=Cin)
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    wT = w.detach().reshape(Co, k * k).t().contiguous()
+    xn = nhwc(x.detach()).bfloat16()
+    y = C.dw_fwd(xn, wT, k, k, s, p)
+    assert rel_err(nchw(y), ref) < 2e-2
+    dx = C.dw_dgrad(nhwc(dy).bfloat16(), wT, H, H, Cin, k, k, s, p)
+    assert rel_err(nchw(dx), x.grad) < 2e-2
+    dw = C.dw_wgrad(xn, nhwc(dy).bfloat16(), k, k, s, p)
+    assert rel_err(dw.reshape(Co, 1, k, k), w.grad) < 2e-2
+
+
+def test_se_scale(C):
+    torch.manual_seed(6)
+    x = bf(torch.randn(3, 48, 4, 4, device="cuda")).requires_grad_(True)
+    s = torch.randn(3, 48, device="cuda").requires_grad_(True)
+    ref = x * torch.sigmoid(s)[:, :, None, None]
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    xn = nhwc(x.detach()).bfloat16()
+    out = C.se_scale_fwd(xn, s.detach())
+    assert rel_err(nchw(out), ref) < 1e-2
+    dx, ds = C.se_scale_bwd(nhwc(dy).bfloat16(), xn, s.detach())
+    assert rel_err(nchw(dx), x.grad) < 1e-2
+    assert rel_err(ds, s.grad) < 1e-2
+
+
+def test_layout_and_augment(C):
+    torch.manual_seed(7)
+    x = torch.randn(2, 3, 32, 32, device="cuda")
+    y = C.nchw_to_nhwc(x, 8)
+    assert y.shape == (2, 32, 32, 8)
+    assert rel_err(y[..., :3].float(), nhwc(x)) < 1e-2 and y[..., 3:].abs().max().item() == 0
+    back = C.nhwc_to_nchw(y, 3)
+    assert rel_err(back, x) < 1e-2
+    data = torch.randint(0, 256, (5, 32, 32, 3), dtype=torch.uint8, device="cuda")
+    idx = torch.tensor([4, 0, 2], device="cuda")
+    # crop offsets (dy=4, dx=4 -> identity) and flip on sample 1
+    rnd = torch.tensor([4 | (4 << 8), 4 | (4 << 8) | (1 << 16), 0], dtype=torch.int32, device="cuda")
+    mean, std = [0.4914, 0.4822, 0.4465], [0.2023, 0.1994, 0.2010]
+    out = C.augment(data, idx, rnd, 4, mean, std)
+    m = torch.tensor(mean, device="cuda")
+    sd = torch.tensor(std, device="cuda")
+    ref0 = (data[4].float() / 255 - m) / sd
+    assert rel_err(out[0, ..., :3], ref0) < 1e-2
+    ref1 = (data[0].float().flip(1) / 255 - m) / sd
+    assert rel_err(out[1, ..., :3], ref1) < 1e-2
+    # dy=dx=0 shifts the image down/right by 4 with zero (-mean/std) padding
+    ref2 = torch.nn.functional.pad(data[2].float().permute(2, 0, 1), (4, 4, 4, 4))[:, :32, :32].permute(1, 2, 0)
+    ref2 = (ref2 / 255 - m) / sd
+    assert rel_err(out[2, ..., :3], ref2) < 1e-2
+
+
+def test_sgd_multi_tensor(C):
+    from pytorch_cifar_amd.engine.optim import SGD
+
+    torch.manual_seed(8)
+    ps = [torch.randn(n, device="cuda", requires_grad=True) for n in (10, 70000, 3)]
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    opt = SGD(ps, lr=0.1, momentum=0.9, weight_decay=5e-4)
+    ropt = torch.optim.SGD(ref, lr=0.1, momentum=0.9, weight_decay=5e-4)
+    for _ in range(3):
+        for p, r in zip(ps, ref):
+            g = torch.randn_like(p)
+            p.grad = g.clone()
+            r.grad = g.clone()
+        opt.step()
+        ropt.step()
+    for p, r in zip(ps, ref):
+        assert rel_err(p.detach(), r.detach()) < 1e-5
