@@ -115,23 +115,38 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ i
 }
 
 // ---- forward finalize: stat[R][2][C] -> aux[4][C] = {mean, invstd, scale, shift} ----
-__global__ void bn_finalize_kernel(const float* __restrict__ stat, int R, int C, double count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* __restrict__ rmean, float* __restrict__ rvar,
-                                   int64_t* __restrict__ nbt, float momentum, float eps,
-                                   int training, int update_running, float* __restrict__ aux) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// One 1024-thread block per 64 channels: 16 row-lanes fold the R (<= 1024) partial rows in
+// parallel (coalesced 256-byte row segments), then lane-row 0 combines them in fp64.
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(
+    const float* __restrict__ stat, int R, int C, double count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+    int64_t* __restrict__ nbt, float momentum, float eps, int training, int update_running,
+    float* __restrict__ aux) {
+  __shared__ float red[16][64][2];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) nbt[0] += 1;
-  if (c >= C) return;
-  float mean, var;
-  if (training) {
-    double s = 0.0, q = 0.0;
-    for (int r = 0; r < R; ++r) {
+  float s = 0.f, q = 0.f;
+  if (training && c < C) {
+#pragma unroll 4
+    for (int r = rl; r < R; r += 16) {
       s += stat[(size_t)r * 2 * C + c];
       q += stat[(size_t)r * 2 * C + C + c];
     }
-    const double m = s / count;
-    double v = q / count - m * m;
+  }
+  red[rl][cl][0] = s;
+  red[rl][cl][1] = q;
+  __syncthreads();
+  if (rl != 0 || c >= C) return;
+  float mean, var;
+  if (training) {
+    double ds = 0.0, dq = 0.0;
+    for (int k = 0; k < 16; ++k) {
+      ds += red[k][cl][0];
+      dq += red[k][cl][1];
+    }
+    const double m = ds / count;
+    double v = dq / count - m * m;
     if (v < 0.0) v = 0.0;
     mean = (float)m;
     var = (float)v;
@@ -284,25 +299,36 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   }
 }
 
-// ---- backward finalize: stat[R][NS][C] -> dgamma/dbeta (+ second BN) and coef[NS>2?6:3][C] ----
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ stat, int R, int NS, int C,
-                                       float count, const float* __restrict__ aux,
-                                       const float* __restrict__ gamma,
-                                       const float* __restrict__ aux2,
-                                       const float* __restrict__ gamma2, int training,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ dgamma2, float* __restrict__ dbeta2,
-                                       float* __restrict__ coef, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s[3] = {0.f, 0.f, 0.f};
-  for (int r = 0; r < R; ++r)
-    for (int k = 0; k < NS; ++k) s[k] += stat[((size_t)r * NS + k) * C + c];
-  const float db = s[0];
+// ---- backward finalize: stat[R][NS][C] -> dgamma/dbeta (+ second BN) and coef[3|6][C] ----
+template <int NS>
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
+    const float* __restrict__ stat, int R, int C, float count, const float* __restrict__ aux,
+    const float* __restrict__ gamma, const float* __restrict__ aux2,
+    const float* __restrict__ gamma2, int training, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ dgamma2, float* __restrict__ dbeta2,
+    float* __restrict__ coef, int accumulate) {
+  __shared__ float red[16][64][3];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float acc[3] = {0.f, 0.f, 0.f};
+  if (c < C) {
+#pragma unroll 4
+    for (int r = rl; r < R; r += 16)
+#pragma unroll
+      for (int k = 0; k < NS; ++k) acc[k] += stat[((size_t)r * NS + k) * C + c];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) red[rl][cl][k] = acc[k];
+  __syncthreads();
+  if (rl != 0 || c >= C) return;
+  double sd[3] = {0.0, 0.0, 0.0};
+  for (int j = 0; j < 16; ++j)
+    for (int k = 0; k < 3; ++k) sd[k] += red[j][cl][k];
+  const float db = (float)sd[0];
   for (int b = 0; b < (NS == 3 ? 2 : 1); ++b) {
     const float* ax = b == 0 ? aux : aux2;
     const float* gm = b == 0 ? gamma : gamma2;
-    const float dg = s[1 + b];
+    const float dg = (float)sd[1 + b];
     const float mean = ax[c], istd = ax[C + c];
     const float g = gm ? gm[c] : 1.f;
     float A, Bc, D;
@@ -395,7 +421,7 @@ void bn_finalize_launch(const float* stat, int R, int C, double count, const flo
                         const float* beta, float* rmean, float* rvar, int64_t* nbt,
                         float momentum, float eps, int training, int update_running, float* aux,
                         hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, stat, R, C, count,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C, count,
                      gamma, beta, rmean, rvar, nbt, momentum, eps, training, update_running, aux);
 }
 
@@ -438,9 +464,14 @@ void bn_bwd_finalize_launch(const float* stat, int R, int NS, int C, float count
                             const float* gamma2, int training, float* dgamma, float* dbeta,
                             float* dgamma2, float* dbeta2, float* coef, int accumulate,
                             hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, stat, R, NS, C,
-                     count, aux, gamma, aux2, gamma2, training, dgamma, dbeta, dgamma2, dbeta2,
-                     coef, accumulate);
+  if (NS == 3)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<3>, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C,
+                       count, aux, gamma, aux2, gamma2, training, dgamma, dbeta, dgamma2, dbeta2,
+                       coef, accumulate);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<2>, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C,
+                       count, aux, gamma, aux2, gamma2, training, dgamma, dbeta, dgamma2, dbeta2,
+                       coef, accumulate);
 }
 
 void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const bf16* y, const float* aux,

@@ -14,9 +14,10 @@ typedef __bf16 bf16;
 
 namespace pca {
 // conv_mfma.hip
-void conv_fwd_launch(const bf16*, const bf16*, const float*, bf16*, float*, int, int, int, int, int, int, int,
-                     int, int, int, int, int, hipStream_t);
-int conv_fwd_bm();
+void conv_fwd_launch(const bf16*, const bf16*, const float*, bf16*, float*, int, int, int, int, int,
+                     int, int, int, int, int, int, int, hipStream_t);
+int conv_fwd_stat_rows(int M, int Cout, int groups);
+void set_conv_tile(int kind, int idx);
 void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int, int, int, int,
                        int, int, int, int, hipStream_t);
 void conv_wgrad_launch(const bf16*, const bf16*, float*, int, int, int, int, int, int, int, int,
@@ -126,7 +127,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
   auto y = at::empty({N, Ho, Wo, Cout}, x.options());
   Tensor stats;
   if (want_stats) {
-    const int gm = (N * Ho * Wo + pca::conv_fwd_bm() - 1) / pca::conv_fwd_bm();
+    const int gm = pca::conv_fwd_stat_rows(N * Ho * Wo, Cout, groups);
     stats = at::empty({gm, 2, Cout}, x.options().dtype(at::kFloat));
   }
   if (bias.has_value() && bias->defined()) {
@@ -222,7 +223,7 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
     TORCH_CHECK(p.size(-1) == C, "stat channel mismatch");
     R = p.size(0);
     stat = ptr<float>(p);
-    if (R > 64) {
+    if (R > 1024) {  // finalize folds up to 1024 partial rows in one pass
       folded = at::empty({64, 2, C}, p.options());
       R = pca::colsum_launch(stat, R, 2 * C, ptr<float>(folded), cur_stream());
       stat = ptr<float>(folded);
@@ -280,7 +281,7 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
   const float* stat = ptr<float>(partial);
   int R = P;
   Tensor folded;
-  if (R > 64) {
+  if (R > 1024) {
     folded = at::empty({64, NS, C}, fopt);
     R = pca::colsum_launch(stat, R, NS * C, ptr<float>(folded), st);
     stat = ptr<float>(folded);
@@ -590,6 +591,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("set_conv_tile", &pca::set_conv_tile, "override tile config (kind 0: fwd/dgrad, 1: wgrad; -1 = heuristic)");
   m.def("weight_prep", &weight_prep);
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);

@@ -17,7 +17,7 @@ import torch
 
 from .. import _native
 
-_CHUNK = 65536
+_CHUNK = 8192
 
 
 class SGD(torch.optim.Optimizer):

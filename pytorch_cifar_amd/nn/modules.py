@@ -36,7 +36,7 @@ class Conv2d(nn.Conv2d):
         if want_stats is None:
             want_stats = self.training
         y, stats = OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.groups,
-                             bool(want_stats and x.is_cuda))
+                             bool(want_stats and not OF._ref(x)))
         if stats is not None:
             setattr(y, _STATS_ATTR, stats)
         return y

@@ -27,6 +27,29 @@ def _C():
     return _native.lib()
 
 
+_FORCE_REFERENCE = False
+
+
+def _ref(x: torch.Tensor) -> bool:
+    """True when ``x`` takes the pure-PyTorch reference path (CPU, or reference mode forced)."""
+    return _FORCE_REFERENCE or not x.is_cuda
+
+
+class reference_kernels:
+    """Context manager: run GPU tensors through stock PyTorch ops (the comparator / oracle)."""
+
+    def __enter__(self):
+        global _FORCE_REFERENCE
+        self._prev = _FORCE_REFERENCE
+        _FORCE_REFERENCE = True
+        return self
+
+    def __exit__(self, *a):
+        global _FORCE_REFERENCE
+        _FORCE_REFERENCE = self._prev
+        return False
+
+
 # ------------------------------------------------------------------------------- layout
 def to_nhwc(x: torch.Tensor, pad_to: int | None = None) -> torch.Tensor:
     """Contiguous NHWC bf16 [N,H,W,C'] view/copy of an NCHW-shaped tensor (C' >= C if padded)."""
@@ -192,7 +215,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
     if isinstance(padding, (tuple, list)):
         assert padding[0] == padding[1]
         padding = padding[0]
-    if not x.is_cuda:
+    if _ref(x):
         return F.conv2d(x, weight, bias, stride, padding, 1, groups), None
     Cout, Cg, KH, KW = weight.shape
     Cin = x.shape[1]
@@ -332,11 +355,11 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
     (resnet.py:47-51 with the 1x1 conv shortcut of resnet.py:31-36).
     """
     training = bn.training
-    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None and not x.is_cuda:
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None and _ref(x):
         bn.num_batches_tracked.add_(1)
         if residual_bn is not None and residual_bn[0].num_batches_tracked is not None:
             residual_bn[0].num_batches_tracked.add_(1)
-    if not x.is_cuda:
+    if _ref(x):
         out = _ref_bn(bn, x, training)
         if residual is not None:
             out = out + residual
@@ -379,7 +402,7 @@ class _Act(torch.autograd.Function):
 def activation(x, act):
     if act in (None, "none"):
         return x
-    if not x.is_cuda:
+    if _ref(x):
         return _ref_act(x, act)
     return to_nchw(_Act.apply(to_nhwc(x), ACT[act]))
 
@@ -408,7 +431,7 @@ class _AddAct(torch.autograd.Function):
 
 def add_act(a, b, act=None):
     """act(a + b) — the un-fused residual join (PNASNet cells, DPN, ShuffleNet)."""
-    if not a.is_cuda:
+    if _ref(a):
         return _ref_act(a + b, act)
     if ACT[act] not in (0, 1):
         return activation(add_act(a, b, None), act)
@@ -429,7 +452,7 @@ class _GAP(torch.autograd.Function):
 
 def global_avg_pool(x):
     """[N,C,H,W] -> fp32 [N,C,1,1] (head / SE squeeze)."""
-    if not x.is_cuda:
+    if _ref(x):
         return F.adaptive_avg_pool2d(x, 1)
     return _GAP.apply(to_nhwc(x)).view(x.shape[0], x.shape[1], 1, 1)
 
@@ -473,7 +496,7 @@ def avg_pool2d(x, kernel_size, stride=None, padding=0):
     k = _pair1(kernel_size)
     s = _pair1(stride) if stride is not None else k
     p = _pair1(padding)
-    if not x.is_cuda:
+    if _ref(x):
         return F.avg_pool2d(x, k, s, p)
     H, W = x.shape[2], x.shape[3]
     if p == 0 and k == H and k == W:
@@ -487,7 +510,7 @@ def max_pool2d(x, kernel_size, stride=None, padding=0):
     k = _pair1(kernel_size)
     s = _pair1(stride) if stride is not None else k
     p = _pair1(padding)
-    if not x.is_cuda:
+    if _ref(x):
         return F.max_pool2d(x, k, s, p)
     return to_nchw(_MaxPool.apply(to_nhwc(x), k, s, p))
 
@@ -514,7 +537,7 @@ class _SEScale(torch.autograd.Function):
 
 def se_excite(x, s_logits):
     """x * sigmoid(s) with s = per-(n, c) excitation logits [N, C] (fp32)."""
-    if not x.is_cuda:
+    if _ref(x):
         return x * torch.sigmoid(s_logits).view(x.shape[0], x.shape[1], 1, 1)
     s = s_logits.reshape(x.shape[0], x.shape[1]).float().contiguous()
     return to_nchw(_SEScale.apply(to_nhwc(x), s))
@@ -536,7 +559,7 @@ class _CrossEntropy(torch.autograd.Function):
 
 def cross_entropy(logits, target, metrics=None):
     """Mean CE; ``metrics`` (fp64 [3] on device) accumulates (loss, correct, count) with no sync."""
-    if not logits.is_cuda:
+    if _ref(logits):
         loss = F.cross_entropy(logits.float(), target)
         if metrics is not None:
             with torch.no_grad():
@@ -561,14 +584,14 @@ def channel_shuffle(x, groups):
     """[N,C,H,W] -> [N,g,C/g,H,W] -> transpose -> [N,C,H,W] (shufflenet*.py ShuffleBlock)."""
     N, C, H, W = x.shape
     out = x.reshape(N, groups, C // groups, H, W).transpose(1, 2).reshape(N, C, H, W)
-    if out.is_cuda:
+    if not _ref(out):
         out = out.contiguous(memory_format=torch.channels_last)
     return out
 
 
 def cat(xs, dim=1):
     out = torch.cat(xs, dim)
-    if out.is_cuda and out.dim() == 4:
+    if not _ref(out) and out.dim() == 4:
         out = out.contiguous(memory_format=torch.channels_last)
     return out
 

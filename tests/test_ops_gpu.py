@@ -1,4 +1,11 @@
-"""End-to-end numerics of the native GPU model path against the fp32 CPU reference path."""
+"""End-to-end numerics of the native GPU model path.
+
+Oracle: the same model (same weights) run in fp32 on the CPU reference path. Because the GPU
+path computes in bf16, its error against the oracle is compared with the error of the *stock*
+bf16 path — the identical model run on the GPU through stock PyTorch kernels under
+``torch.autocast(bfloat16)`` (``reference_kernels()`` mode). The native path must be as close
+to fp32 as stock bf16 PyTorch is (within a small factor), for logits and every gradient.
+"""
 import copy
 
 import pytest
@@ -12,41 +19,62 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-def _compare_model(name, batch=8, tol_out=0.05, tol_grad=0.08):
-    from pytorch_cifar_amd import models
+def _grads(model):
+    return {n: p.grad for n, p in model.named_parameters()}
 
+
+def _run(model, x, y, device, stock=False):
+    from pytorch_cifar_amd.ops.functional import cross_entropy, reference_kernels
+
+    x, y = x.to(device), y.to(device)
+    if stock:
+        with reference_kernels(), torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x.contiguous(memory_format=torch.channels_last))
+            loss = cross_entropy(out.float(), y)
+        loss.backward()
+    else:
+        out = model(x)
+        loss = cross_entropy(out, y)
+        loss.backward()
+    torch.cuda.synchronize() if device == "cuda" else None
+    return out.float()
+
+
+def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True):
     torch.manual_seed(0)
-    cpu = getattr(models, name)() if not isinstance(name, tuple) else getattr(models, name[0])(*name[1:])
-    gpu = copy.deepcopy(cpu).cuda()
+    ref = ctor()
+    native = copy.deepcopy(ref).cuda()
+    stock = copy.deepcopy(ref).cuda()
     x = torch.randn(batch, 3, 32, 32)
     y = torch.randint(0, 10, (batch,))
-    from pytorch_cifar_amd.ops.functional import cross_entropy
-
-    out_c = cpu(x)
-    loss_c = cross_entropy(out_c, y)
-    loss_c.backward()
-    out_g = gpu(x.cuda())
-    loss_g = cross_entropy(out_g, y.cuda())
-    loss_g.backward()
-    torch.cuda.synchronize()
-    assert rel(out_g, out_c) < tol_out, f"{name} logits rel err {rel(out_g, out_c)}"
-    errs = {}
-    for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
-        if pc.grad is None:
-            assert pg.grad is None or pg.grad.abs().max().item() == 0, n
+    out_r = _run(ref, x, y, "cpu")
+    out_n = _run(native, x, y, "cuda")
+    out_s = _run(stock, x, y, "cuda", stock=True)
+    e_n, e_s = rel(out_n, out_r), rel(out_s, out_r)
+    assert e_n <= factor * e_s + slack, f"logits: native {e_n:.4f} vs stock-bf16 {e_s:.4f}"
+    gr, gn, gs = _grads(ref), _grads(native), _grads(stock)
+    bad = []
+    for name, g in gr.items():
+        if g is None:
+            assert gn[name] is None or gn[name].abs().max().item() == 0, name
             continue
-        errs[n] = rel(pg.grad, pc.grad)
-    worst = max(errs.values())
-    assert worst < tol_grad, f"{name} worst grad {max(errs, key=errs.get)} {worst}"
-    for (n, bc), (_, bg) in zip(cpu.named_buffers(), gpu.named_buffers()):
-        if bc.dtype.is_floating_point:
-            assert rel(bg, bc) < 0.02, n
-        else:
-            assert int(bg.item()) == int(bc.item()), n
+        en, es = rel(gn[name], g), rel(gs[name], g)
+        if en > factor * es + slack:
+            bad.append((name, round(en, 4), round(es, 4)))
+    assert not bad, f"grads worse than stock bf16 (name, native, stock): {bad[:10]}"
+    if check_buffers:
+        for (n, br), (_, bn) in zip(ref.named_buffers(), native.named_buffers()):
+            if br.dtype.is_floating_point:
+                assert rel(bn, br) < 0.03, n
+            else:
+                assert int(bn.item()) == int(br.item()), n
+    return e_n, e_s
 
 
-def test_resnet18_matches_cpu_reference():
-    _compare_model("ResNet18")
+def test_resnet18_matches_reference():
+    from pytorch_cifar_amd import models
+
+    compare_model(models.ResNet18)
 
 
 def test_resnet18_trains():
