@@ -1,0 +1,89 @@
+"""DenseNet121/169/201/161 and densenet_cifar (parity: reference models/densenet.py:9-99).
+
+Pre-activation dense layers (BN-ReLU-1x1 -> BN-ReLU-3x3, concat [new, x]) with BN+ReLU fused;
+the BNs read concatenated tensors, so their statistics come from the standalone reduction
+kernel rather than a conv epilogue."""
+import math
+
+import torch.nn as tnn
+
+from ..nn import BatchNorm2d, Conv2d, Linear, Sequential
+from ..nn import functional as F
+
+
+class Bottleneck(tnn.Module):
+    def __init__(self, in_planes, growth_rate):
+        super().__init__()
+        self.bn1 = BatchNorm2d(in_planes)
+        self.conv1 = Conv2d(in_planes, 4 * growth_rate, kernel_size=1, bias=False)
+        self.bn2 = BatchNorm2d(4 * growth_rate)
+        self.conv2 = Conv2d(4 * growth_rate, growth_rate, kernel_size=3, padding=1, bias=False)
+
+    def forward(self, x):
+        out = self.conv1(self.bn1(x, act="relu"))
+        out = self.conv2(self.bn2(out, act="relu"), want_stats=False)
+        return F.cat([out, x], 1)
+
+
+class Transition(tnn.Module):
+    def __init__(self, in_planes, out_planes):
+        super().__init__()
+        self.bn = BatchNorm2d(in_planes)
+        self.conv = Conv2d(in_planes, out_planes, kernel_size=1, bias=False)
+
+    def forward(self, x):
+        out = self.conv(self.bn(x, act="relu"), want_stats=False)
+        return F.avg_pool2d(out, 2)
+
+
+class DenseNet(tnn.Module):
+    def __init__(self, block, nblocks, growth_rate=12, reduction=0.5, num_classes=10):
+        super().__init__()
+        self.growth_rate = growth_rate
+        planes = 2 * growth_rate
+        self.conv1 = Conv2d(3, planes, kernel_size=3, padding=1, bias=False)
+        for i in range(4):
+            setattr(self, f"dense{i + 1}", self._make_dense_layers(block, planes, nblocks[i]))
+            planes += nblocks[i] * growth_rate
+            if i < 3:
+                out_planes = int(math.floor(planes * reduction))
+                setattr(self, f"trans{i + 1}", Transition(planes, out_planes))
+                planes = out_planes
+        self.bn = BatchNorm2d(planes)
+        self.linear = Linear(planes, num_classes)
+
+    def _make_dense_layers(self, block, in_planes, nblock):
+        layers = []
+        for _ in range(nblock):
+            layers.append(block(in_planes, self.growth_rate))
+            in_planes += self.growth_rate
+        return Sequential(*layers)
+
+    def forward(self, x):
+        out = self.conv1(x, want_stats=False)
+        out = self.trans1(self.dense1(out))
+        out = self.trans2(self.dense2(out))
+        out = self.trans3(self.dense3(out))
+        out = self.dense4(out)
+        out = F.avg_pool2d(self.bn(out, act="relu"), 4)
+        return self.linear(out.reshape(out.size(0), -1))
+
+
+def DenseNet121():
+    return DenseNet(Bottleneck, [6, 12, 24, 16], growth_rate=32)
+
+
+def DenseNet169():
+    return DenseNet(Bottleneck, [6, 12, 32, 32], growth_rate=32)
+
+
+def DenseNet201():
+    return DenseNet(Bottleneck, [6, 12, 48, 32], growth_rate=32)
+
+
+def DenseNet161():
+    return DenseNet(Bottleneck, [6, 12, 36, 24], growth_rate=48)
+
+
+def densenet_cifar():
+    return DenseNet(Bottleneck, [6, 12, 24, 16], growth_rate=12)

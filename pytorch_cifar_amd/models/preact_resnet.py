@@ -1,0 +1,97 @@
+"""Pre-activation ResNet18/34/50/101/152 (parity: reference models/preact_resnet.py:12-110).
+
+BN+ReLU *precede* each conv; the shortcut (a plain 1x1 conv, no BN) reads the pre-activated
+tensor, and only exists as a submodule when the shape changes (``hasattr`` semantics kept)."""
+import torch.nn as tnn
+
+from ..nn import BatchNorm2d, Conv2d, Linear, Sequential
+from ..nn import functional as F
+
+
+class PreActBlock(tnn.Module):
+    expansion = 1
+
+    def __init__(self, in_planes, planes, stride=1):
+        super().__init__()
+        self.bn1 = BatchNorm2d(in_planes)
+        self.conv1 = Conv2d(in_planes, planes, kernel_size=3, stride=stride, padding=1, bias=False)
+        self.bn2 = BatchNorm2d(planes)
+        self.conv2 = Conv2d(planes, planes, kernel_size=3, stride=1, padding=1, bias=False)
+        if stride != 1 or in_planes != self.expansion * planes:
+            self.shortcut = Sequential(
+                Conv2d(in_planes, self.expansion * planes, kernel_size=1, stride=stride, bias=False))
+
+    def forward(self, x):
+        a = self.bn1(x, act="relu")
+        sc = self.shortcut(a) if hasattr(self, "shortcut") else x
+        out = self.conv2(self.bn2(self.conv1(a), act="relu"))
+        return F.add_act(out, sc)
+
+
+class PreActBottleneck(tnn.Module):
+    expansion = 4
+
+    def __init__(self, in_planes, planes, stride=1):
+        super().__init__()
+        self.bn1 = BatchNorm2d(in_planes)
+        self.conv1 = Conv2d(in_planes, planes, kernel_size=1, bias=False)
+        self.bn2 = BatchNorm2d(planes)
+        self.conv2 = Conv2d(planes, planes, kernel_size=3, stride=stride, padding=1, bias=False)
+        self.bn3 = BatchNorm2d(planes)
+        self.conv3 = Conv2d(planes, self.expansion * planes, kernel_size=1, bias=False)
+        if stride != 1 or in_planes != self.expansion * planes:
+            self.shortcut = Sequential(
+                Conv2d(in_planes, self.expansion * planes, kernel_size=1, stride=stride, bias=False))
+
+    def forward(self, x):
+        a = self.bn1(x, act="relu")
+        sc = self.shortcut(a) if hasattr(self, "shortcut") else x
+        out = self.conv1(a)
+        out = self.conv2(self.bn2(out, act="relu"))
+        out = self.conv3(self.bn3(out, act="relu"))
+        return F.add_act(out, sc)
+
+
+class PreActResNet(tnn.Module):
+    def __init__(self, block, num_blocks, num_classes=10):
+        super().__init__()
+        self.in_planes = 64
+        self.conv1 = Conv2d(3, 64, kernel_size=3, stride=1, padding=1, bias=False)
+        self.layer1 = self._make_layer(block, 64, num_blocks[0], stride=1)
+        self.layer2 = self._make_layer(block, 128, num_blocks[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, num_blocks[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, num_blocks[3], stride=2)
+        self.linear = Linear(512 * block.expansion, num_classes)
+
+    def _make_layer(self, block, planes, num_blocks, stride):
+        layers = []
+        for s in [stride] + [1] * (num_blocks - 1):
+            layers.append(block(self.in_planes, planes, s))
+            self.in_planes = planes * block.expansion
+        return Sequential(*layers)
+
+    def forward(self, x):
+        out = self.conv1(x)
+        out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
+        out = F.avg_pool2d(out, 4)
+        return self.linear(out.reshape(out.size(0), -1))
+
+
+def PreActResNet18():
+    return PreActResNet(PreActBlock, [2, 2, 2, 2])
+
+
+def PreActResNet34():
+    return PreActResNet(PreActBlock, [3, 4, 6, 3])
+
+
+def PreActResNet50():
+    return PreActResNet(PreActBottleneck, [3, 4, 6, 3])
+
+
+def PreActResNet101():
+    return PreActResNet(PreActBottleneck, [3, 4, 23, 3])
+
+
+def PreActResNet152():
+    return PreActResNet(PreActBottleneck, [3, 8, 36, 3])

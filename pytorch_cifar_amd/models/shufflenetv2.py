@@ -1,0 +1,111 @@
+"""ShuffleNetV2(net_size in {0.5, 1, 1.5, 2}) (parity: reference models/shufflenetv2.py:10-152).
+
+Channel split -> (1x1 + BN + ReLU -> depthwise 3x3 + BN -> 1x1 + BN + ReLU) -> concat -> shuffle;
+two-branch stride-2 DownBlock. Odd widths (58/116/232 for net_size 1) fall back to the generic
+direct-conv and scalar depthwise kernels where the MFMA tile needs multiples of 8."""
+import torch.nn as tnn
+
+from ..nn import BatchNorm2d, Conv2d, Linear, Sequential
+from ..nn import functional as F
+
+
+class ShuffleBlock(tnn.Module):
+    def __init__(self, groups=2):
+        super().__init__()
+        self.groups = groups
+
+    def forward(self, x):
+        return F.channel_shuffle(x, self.groups)
+
+
+class SplitBlock(tnn.Module):
+    def __init__(self, ratio):
+        super().__init__()
+        self.ratio = ratio
+
+    def forward(self, x):
+        c = int(x.size(1) * self.ratio)
+        return x[:, :c, :, :], x[:, c:, :, :]
+
+
+class BasicBlock(tnn.Module):
+    def __init__(self, in_channels, split_ratio=0.5):
+        super().__init__()
+        self.split = SplitBlock(split_ratio)
+        c = int(in_channels * split_ratio)
+        self.conv1 = Conv2d(c, c, kernel_size=1, bias=False)
+        self.bn1 = BatchNorm2d(c)
+        self.conv2 = Conv2d(c, c, kernel_size=3, stride=1, padding=1, groups=c, bias=False)
+        self.bn2 = BatchNorm2d(c)
+        self.conv3 = Conv2d(c, c, kernel_size=1, bias=False)
+        self.bn3 = BatchNorm2d(c)
+        self.shuffle = ShuffleBlock()
+
+    def forward(self, x):
+        x1, x2 = self.split(x)
+        out = self.bn1(self.conv1(x2), act="relu")
+        out = self.bn2(self.conv2(out))
+        out = self.bn3(self.conv3(out), act="relu")
+        return self.shuffle(F.cat([x1, out], 1))
+
+
+class DownBlock(tnn.Module):
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        mid = out_channels // 2
+        self.conv1 = Conv2d(in_channels, in_channels, kernel_size=3, stride=2, padding=1,
+                            groups=in_channels, bias=False)
+        self.bn1 = BatchNorm2d(in_channels)
+        self.conv2 = Conv2d(in_channels, mid, kernel_size=1, bias=False)
+        self.bn2 = BatchNorm2d(mid)
+        self.conv3 = Conv2d(in_channels, mid, kernel_size=1, bias=False)
+        self.bn3 = BatchNorm2d(mid)
+        self.conv4 = Conv2d(mid, mid, kernel_size=3, stride=2, padding=1, groups=mid, bias=False)
+        self.bn4 = BatchNorm2d(mid)
+        self.conv5 = Conv2d(mid, mid, kernel_size=1, bias=False)
+        self.bn5 = BatchNorm2d(mid)
+        self.shuffle = ShuffleBlock()
+
+    def forward(self, x):
+        left = self.bn2(self.conv2(self.bn1(self.conv1(x))), act="relu")
+        right = self.bn3(self.conv3(x), act="relu")
+        right = self.bn5(self.conv5(self.bn4(self.conv4(right))), act="relu")
+        return self.shuffle(F.cat([left, right], 1))
+
+
+class ShuffleNetV2(tnn.Module):
+    def __init__(self, net_size):
+        super().__init__()
+        out_channels = configs[net_size]["out_channels"]
+        num_blocks = configs[net_size]["num_blocks"]
+        self.conv1 = Conv2d(3, 24, kernel_size=3, stride=1, padding=1, bias=False)
+        self.bn1 = BatchNorm2d(24)
+        self.in_channels = 24
+        self.layer1 = self._make_layer(out_channels[0], num_blocks[0])
+        self.layer2 = self._make_layer(out_channels[1], num_blocks[1])
+        self.layer3 = self._make_layer(out_channels[2], num_blocks[2])
+        self.conv2 = Conv2d(out_channels[2], out_channels[3], kernel_size=1, stride=1, padding=0, bias=False)
+        self.bn2 = BatchNorm2d(out_channels[3])
+        self.linear = Linear(out_channels[3], 10)
+
+    def _make_layer(self, out_channels, num_blocks):
+        layers = [DownBlock(self.in_channels, out_channels)]
+        for _ in range(num_blocks):
+            layers.append(BasicBlock(out_channels))
+            self.in_channels = out_channels
+        return Sequential(*layers)
+
+    def forward(self, x):
+        out = self.bn1(self.conv1(x), act="relu")
+        out = self.layer3(self.layer2(self.layer1(out)))
+        out = self.bn2(self.conv2(out), act="relu")
+        out = F.avg_pool2d(out, 4)
+        return self.linear(out.reshape(out.size(0), -1))
+
+
+configs = {
+    0.5: {"out_channels": (48, 96, 192, 1024), "num_blocks": (3, 7, 3)},
+    1: {"out_channels": (116, 232, 464, 1024), "num_blocks": (3, 7, 3)},
+    1.5: {"out_channels": (176, 352, 704, 1024), "num_blocks": (3, 7, 3)},
+    2: {"out_channels": (224, 488, 976, 2048), "num_blocks": (3, 7, 3)},
+}
