@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+'''Train CIFAR10 on MI355X (single process) — CLI parity with the reference main.py.
+
+Reference flags: --lr (0.1), --resume/-r. Additive flags: --model (default SimpleDLA, the
+reference's main.py:71 choice), --epochs (200), --batch_size (128), --test_batch_size (100),
+--data_dir, --synthetic, --seed, --graph, --max_steps, --log_every, --checkpoint_dir, --cpu.
+
+Semantics kept: RandomCrop(32, pad 4) + HFlip + Normalize train transform, SGD(momentum 0.9,
+wd 5e-4), CosineAnnealingLR(T_max=200) stepped per epoch, CE loss, best-accuracy checkpoint
+``./checkpoint/ckpt.pth`` = {'net', 'acc', 'epoch'} with the wrapped net's ``module.`` keys.
+'''
+import argparse
+import os
+import sys
+
+import torch
+
+from pytorch_cifar_amd import models
+from pytorch_cifar_amd.data.factory import build_loaders
+from pytorch_cifar_amd.engine.arena import ParamArena
+from pytorch_cifar_amd.engine.checkpoint import load_checkpoint, save_checkpoint
+from pytorch_cifar_amd.engine.optim import SGD
+from pytorch_cifar_amd.engine.trainer import Trainer
+from pytorch_cifar_amd.parallel.data_parallel import DataParallel
+from pytorch_cifar_amd.parallel.launcher import DistContext
+from utils import progress_bar
+
+parser = argparse.ArgumentParser(description='PyTorch CIFAR10 Training (MI355X-native)')
+parser.add_argument('--lr', default=0.1, type=float, help='learning rate')
+parser.add_argument('--resume', '-r', action='store_true', help='resume from checkpoint')
+parser.add_argument('--model', default='SimpleDLA', help='model constructor name (see models.MODEL_REGISTRY)')
+parser.add_argument('--epochs', default=200, type=int, help='number of epochs')
+parser.add_argument('--batch_size', default=128, type=int)
+parser.add_argument('--test_batch_size', default=100, type=int)
+parser.add_argument('--data_dir', default='./data')
+parser.add_argument('--synthetic', action='store_true', help='synthetic CIFAR-shaped data (no dataset files)')
+parser.add_argument('--synthetic_size', default=None, type=int)
+parser.add_argument('--seed', default=0, type=int)
+parser.add_argument('--graph', default=1, type=int, help='capture the train step in a hipGraph (GPU)')
+parser.add_argument('--max_steps', default=None, type=int, help='cap steps per epoch (smoke runs)')
+parser.add_argument('--log_every', default=20, type=int)
+parser.add_argument('--checkpoint_dir', default='./checkpoint')
+parser.add_argument('--cpu', action='store_true', help='force the CPU reference path')
+parser.add_argument('--t_max', default=200, type=int, help='cosine schedule length (reference: 200)')
+
+
+def main(argv=None):
+    args = parser.parse_args(argv)
+    device = 'cuda' if torch.cuda.is_available() and not args.cpu else 'cpu'
+    torch.manual_seed(args.seed)
+    best_acc = 0  # best test accuracy
+    start_epoch = 0  # start from epoch 0 or last checkpoint epoch
+
+    print('==> Preparing data..')
+    trainloader, testloader = build_loaders(args.data_dir, args.synthetic, args.batch_size,
+                                            args.test_batch_size, device, seed=args.seed,
+                                            synthetic_size=args.synthetic_size,
+                                            test_synthetic_size=(args.synthetic_size // 5 if args.synthetic_size else None))
+
+    print('==> Building model..')
+    model = models.build_model(args.model).to(device)
+    net = model
+    arena = None
+    if device == 'cuda':
+        arena = ParamArena(model.parameters())
+        net = DataParallel(model)
+
+    ckpt_path = os.path.join(args.checkpoint_dir, 'ckpt.pth')
+    optimizer = SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-4)
+    if arena is not None and len(getattr(net, 'device_ids', [])) <= 1:
+        optimizer.attach_arena(arena)
+    scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=args.t_max)
+    if args.resume:
+        print('==> Resuming from checkpoint..')
+        assert os.path.isdir(args.checkpoint_dir), 'Error: no checkpoint directory found!'
+        best_acc, start_epoch = load_checkpoint(ckpt_path, net, optimizer, scheduler, map_location=device)
+        start_epoch += 1
+
+    trainer = Trainer(net, optimizer, trainloader, testloader, DistContext(device=torch.device(device)),
+                      graph=bool(args.graph) and device == 'cuda', log_every=args.log_every,
+                      progress=progress_bar, max_steps=args.max_steps)
+
+    for epoch in range(start_epoch, start_epoch + args.epochs):
+        print('\nEpoch: %d' % epoch)
+        trainer.train_epoch(epoch)
+        _, acc, _, _ = trainer.test_epoch(epoch)
+        if trainer.images_per_sec:
+            print('Throughput: %.1f img/s' % trainer.images_per_sec)
+        if acc > best_acc:
+            print('Saving..')
+            save_checkpoint(ckpt_path, net, acc, epoch, optimizer, scheduler)
+            best_acc = acc
+        scheduler.step()
+    return best_acc
+
+
+if __name__ == '__main__':
+    sys.exit(0 if main() is not None else 1)

@@ -125,13 +125,14 @@ class DeviceLoader:
         p = self.crop_pad
         n = x.shape[0]
         if p:
+            H, W = x.shape[2], x.shape[3]
             xp = torch.nn.functional.pad(x, (p, p, p, p))
-            dy = (rnd & 0xFF) % (2 * p + 1)
-            dx = ((rnd >> 8) & 0xFF) % (2 * p + 1)
-            out = torch.empty_like(x)
-            for i in range(n):
-                out[i] = xp[i, :, dy[i]: dy[i] + 32, dx[i]: dx[i] + 32]
-            x = out
+            dy = ((rnd & 0xFF) % (2 * p + 1)).long()
+            dx = (((rnd >> 8) & 0xFF) % (2 * p + 1)).long()
+            rows = (dy[:, None] + torch.arange(H)).view(n, 1, H, 1).expand(n, 3, H, W + 2 * p)
+            xr = xp.gather(2, rows)
+            cols = (dx[:, None] + torch.arange(W)).view(n, 1, 1, W).expand(n, 3, H, W)
+            x = xr.gather(3, cols)
         if self.flip:
             f = ((rnd >> 16) & 1).bool()
             x[f] = x[f].flip(3)

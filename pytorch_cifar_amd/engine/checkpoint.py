@@ -1,0 +1,54 @@
+"""Checkpoint save/resume in the reference layout (main.py:137-148, main_dist.py:239-252).
+
+Payload ``{'net': wrapped.state_dict(), 'acc': float percent, 'epoch': int}`` — the same keys,
+``module.``-prefixed parameter names when the net is wrapped, fp32 tensors in the reference's
+NCHW parameter shapes — so reference checkpoints load here and vice versa. Additions (extra keys
+are ignored by reference loaders): optional ``optimizer`` / ``scheduler`` state
+so a resumed run continues the momentum buffers and the cosine schedule.
+
+Writes are atomic (temp file + rename) and done by one rank. Loads use ``weights_only=True``.
+Resume tolerates a ``module.`` prefix mismatch (the reference's resume fails on a bare model).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+
+def _unwrap_keys(sd, want_prefix: bool):
+    has = all(k.startswith("module.") for k in sd) and len(sd) > 0
+    if want_prefix and not has:
+        return {"module." + k: v for k, v in sd.items()}
+    if not want_prefix and has:
+        return {k[len("module."):]: v for k, v in sd.items()}
+    return sd
+
+
+def save_checkpoint(path, net, acc, epoch, optimizer=None, scheduler=None, extra=None):
+    state = {"net": net.state_dict(), "acc": float(acc), "epoch": int(epoch)}
+    if optimizer is not None:
+        state["optimizer"] = optimizer.state_dict()
+    if scheduler is not None:
+        state["scheduler"] = scheduler.state_dict()
+    if extra:
+        state.update(extra)
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    tmp = path + ".tmp"
+    torch.save(state, tmp)
+    os.replace(tmp, path)
+    return path
+
+
+def load_checkpoint(path, net, optimizer=None, scheduler=None, map_location="cpu"):
+    """Restore ``net`` (and optionally optimizer/scheduler); returns (best_acc, epoch)."""
+    ck = torch.load(path, map_location=map_location, weights_only=True)
+    sd = ck["net"]
+    want_prefix = all(k.startswith("module.") for k in net.state_dict())
+    net.load_state_dict(_unwrap_keys(sd, want_prefix))
+    if optimizer is not None and "optimizer" in ck:
+        optimizer.load_state_dict(ck["optimizer"])
+    if scheduler is not None and "scheduler" in ck:
+        scheduler.load_state_dict(ck["scheduler"])
+    return float(ck.get("acc", 0.0)), int(ck.get("epoch", 0))

@@ -96,6 +96,24 @@ class SGD(torch.optim.Optimizer):
             self.state[p]["momentum_buffer"] = v
         return self
 
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        arena = getattr(self, "arena", None)
+        if arena is not None:  # keep momentum buffers as views of the arena
+            mom = arena.ensure_momentum()
+            have = False
+            for p in arena.params:
+                v = arena.view(mom, p)
+                b = self.state[p].get("momentum_buffer")
+                if b is not None and b.data_ptr() != v.data_ptr():
+                    v.copy_(b)
+                    have = True
+                elif b is None:
+                    v.zero_()
+                self.state[p]["momentum_buffer"] = v
+            self._arena_first = not have
+        self._tables = {}
+
     # ----------------------------------------------------------------------------- step
     @torch.no_grad()
     def step(self, closure=None):

@@ -159,3 +159,89 @@ class EpochTimer:
 
     def elapsed(self):
         return time.perf_counter() - self.t0
+
+
+class Trainer:
+    """Epoch driver shared by main.py and main_dist.py.
+
+    train_epoch / test_epoch reproduce the reference loops (main.py:93-148, main_dist.py:166-252)
+    including their console/log formats, with three changes: metrics accumulate on the device and
+    are read every ``log_every`` steps (not two ``.item()`` syncs per step); the test set is sharded
+    across ranks and its counts all-reduced (the reference evaluated the full set on every rank and
+    checkpointed on rank 0's local accuracy); full batches replay a captured
+    hipGraph of the whole step when ``graph`` is on.
+    """
+
+    def __init__(self, net, optimizer, train_loader, test_loader, ctx, ddp=None, graph=False,
+                 log_every=20, progress=None, is_main=True, max_steps=None):
+        self.net = net
+        self.opt = optimizer
+        self.train_loader = train_loader
+        self.test_loader = test_loader
+        self.ctx = ctx
+        self.ddp = ddp
+        self.device = train_loader.device
+        self.log_every = max(1, log_every)
+        self.progress = progress
+        self.is_main = is_main
+        self.max_steps = max_steps
+        self.step = TrainStep(net, optimizer, train_loader, train_loader.batch_size, ddp=ddp,
+                              graph=graph)
+        self.images_per_sec = None
+
+    def _reduce(self, m):
+        t = torch.tensor(m, dtype=torch.float64, device=self.device if self.device.type == "cuda" else "cpu")
+        self.ctx.all_reduce_sum(t)
+        return t.tolist()
+
+    def train_epoch(self, epoch):
+        self.net.train()
+        loader = self.train_loader
+        loader.set_epoch(epoch)
+        metrics = self.step.metrics
+        metrics.zero_()
+        n = len(loader)
+        if self.max_steps:
+            n = min(n, self.max_steps)
+        t0 = time.perf_counter()
+        imgs = 0
+        for b, idx in enumerate(loader.batch_indices()):
+            if b >= n:
+                break
+            if loader.drop_last and idx.numel() < loader.batch_size:
+                break
+            self.step(idx)
+            imgs += idx.numel()
+            if self.progress is not None and (b % self.log_every == 0 or b == n - 1):
+                loss_sum, correct, total = metrics.tolist()
+                self.progress(b, n, "Loss: %.3f | Acc: %.3f%% (%d/%d)"
+                              % (loss_sum / (b + 1), 100.0 * correct / max(total, 1), correct, total))
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        loss_sum, correct, total = metrics.tolist()
+        steps = max(1, min(n, b + 1) if n else 1)
+        self.images_per_sec = imgs * self.ctx.world / dt if dt > 0 else None
+        return loss_sum / steps, 100.0 * correct / max(total, 1), int(correct), int(total)
+
+    @torch.no_grad()
+    def test_epoch(self, epoch):
+        self.net.eval()
+        loader = self.test_loader
+        metrics = torch.zeros(3, dtype=torch.float64, device=self.device)
+        n = len(loader)
+        if self.max_steps:
+            n = min(n, self.max_steps)
+        for b, idx in enumerate(loader.batch_indices()):
+            if b >= n:
+                break
+            x, y = loader.make_batch(idx)
+            out = self.net(x)
+            cross_entropy(out, y, metrics)
+            if self.progress is not None and (b % self.log_every == 0 or b == n - 1):
+                loss_sum, correct, total = metrics.tolist()
+                self.progress(b, n, "Loss: %.3f | Acc: %.3f%% (%d/%d)"
+                              % (loss_sum / (b + 1), 100.0 * correct / max(total, 1), correct, total))
+        loss_sum, correct, total = self._reduce(metrics.tolist())
+        steps = max(1, n) * self.ctx.world
+        return loss_sum / steps, 100.0 * correct / max(total, 1), int(correct), int(total)

@@ -128,8 +128,9 @@ class _ConvMFMA(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
         KH, KW = weight.shape[2], weight.shape[3]
+        dw_ret = db_ret = None
         if weight.requires_grad:
-            buf = None if cin_pad else G.grad_buffer(weight)
+            buf = None if (cin_pad or not weight.is_leaf) else G.grad_buffer(weight)
             if buf is not None:
                 C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, buf)
                 G.fire(weight)
@@ -137,10 +138,17 @@ class _ConvMFMA(torch.autograd.Function):
                 dw = C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, None)
                 if cin_pad:
                     dw = dw[..., : weight.shape[1]]
-                G.accumulate(weight, dw)
+                if weight.is_leaf:
+                    G.accumulate(weight, dw)
+                else:
+                    dw_ret = dw.permute(0, 3, 1, 2)
         if bias is not None and bias.requires_grad:
-            G.accumulate(bias, C.bn_stats(dy)[:, 0].sum(0))
-        return dx, None, None, None, None, None, None, None
+            db = C.bn_stats(dy)[:, 0].sum(0)
+            if bias.is_leaf:
+                G.accumulate(bias, db)
+            else:
+                db_ret = db
+        return dx, dw_ret, db_ret, None, None, None, None, None
 
 
 class _ConvDirect(torch.autograd.Function):
@@ -167,14 +175,22 @@ class _ConvDirect(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = C.direct_dgrad(dy, w_phys, x.shape[1], x.shape[2], stride, padding, groups)
         with_bias = bias is not None and bias.requires_grad
+        dw_ret = db_ret = None
         if weight.requires_grad or with_bias:
             flat = C.direct_wgrad(x, dy, weight.shape[2], weight.shape[3], stride, padding, groups, with_bias)
             nw = w_phys.numel()
             if weight.requires_grad:
-                G.accumulate(weight, flat[:nw].view_as(w_phys))
+                dw = flat[:nw].view_as(w_phys)
+                if weight.is_leaf:
+                    G.accumulate(weight, dw)
+                else:
+                    dw_ret = dw.permute(0, 3, 1, 2)
             if with_bias:
-                G.accumulate(bias, flat[nw:])
-        return dx, None, None, None, None, None
+                if bias.is_leaf:
+                    G.accumulate(bias, flat[nw:])
+                else:
+                    db_ret = flat[nw:]
+        return dx, dw_ret, db_ret, None, None, None
 
 
 class _ConvDepthwise(torch.autograd.Function):
@@ -201,10 +217,14 @@ class _ConvDepthwise(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = C.dw_dgrad(dy, wT, x.shape[1], x.shape[2], x.shape[3], KH, KW, stride, padding)
         w = ctx.weight
+        dw_ret = None
         if w.requires_grad:
             dw = C.dw_wgrad(x, dy, KH, KW, stride, padding)  # [Co, KH*KW]
-            G.accumulate(w, dw.view(w.shape[0], KH, KW, 1))
-        return dx, None, None, None
+            if w.is_leaf:
+                G.accumulate(w, dw.view(w.shape[0], KH, KW, 1))
+            else:
+                dw_ret = dw.view(w.shape)
+        return dx, dw_ret, None, None
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False):
@@ -251,9 +271,14 @@ class _AddBias(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         b = ctx.bias
+        db_ret = None
         if b.requires_grad:
-            G.accumulate(b, _C().bn_stats(dy.contiguous())[:, 0].sum(0))
-        return dy, None
+            db = _C().bn_stats(dy.contiguous())[:, 0].sum(0)
+            if b.is_leaf:
+                G.accumulate(b, db)
+            else:
+                db_ret = db
+        return dy, db_ret
 
 
 def add_bias(y_nhwc, bias):
@@ -310,7 +335,7 @@ class _BatchNormAct(torch.autograd.Function):
         dout = dout.contiguous()
 
         def acc(p):
-            if p is None or not p.requires_grad:
+            if p is None or not p.requires_grad or not p.is_leaf:
                 return None
             return G.grad_buffer(p)
 
@@ -324,15 +349,25 @@ class _BatchNormAct(torch.autograd.Function):
             y2, aux2,
             bn2.weight.detach() if (bn2 is not None and bn2.weight is not None) else None,
             ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2)
-        for p, buf, val in ((bn.weight, g1, dg), (bn.bias, b1, db)):
-            if p is not None and p.requires_grad:
-                G.fire(p) if buf is not None else G.accumulate(p, val)
+        ret = {}
+
+        def deliver(p, buf, val, slot):
+            if p is None or not p.requires_grad:
+                return
+            if not p.is_leaf:          # replicated / functional parameter: hand to autograd
+                ret[slot] = val
+            elif buf is not None:
+                G.fire(p)
+            else:
+                G.accumulate(p, val)
+
+        deliver(bn.weight, g1, dg, 1)
+        deliver(bn.bias, b1, db, 2)
         if bn2 is not None:
-            for p, buf, val in ((bn2.weight, g2, dg2), (bn2.bias, b2, db2)):
-                if p is not None and p.requires_grad:
-                    G.fire(p) if buf is not None else G.accumulate(p, val)
-        return (dy, None, None, dres if ctx.has_res else None, dy2 if y2 is not None else None,
-                None, None, None, None, None)
+            deliver(bn2.weight, g2, dg2, 5)
+            deliver(bn2.bias, b2, db2, 6)
+        return (dy, ret.get(1), ret.get(2), dres if ctx.has_res else None,
+                dy2 if y2 is not None else None, ret.get(5), ret.get(6), None, None, None)
 
 
 def _ref_bn(bn, x, training):

@@ -94,13 +94,13 @@ class DistributedDataParallel(nn.Module):
         limit = first
         for p in self.arena.order:  # reverse registration order = backward order
             off, n = self.arena.slice_of(p)
+            if cur and off + n - start > limit:  # close before overflowing (a lone big param
+                buckets.append((start, end, cur))  # still gets its own bucket)
+                cur, start, limit = [], None, cap
             if start is None:
                 start = off
             cur.append(p)
             end = off + n
-            if end - start >= limit:
-                buckets.append((start, end, cur))
-                cur, start, limit = [], None, cap
         if cur:
             buckets.append((start, end, cur))
         flat = self.arena.grad_flat
@@ -175,8 +175,6 @@ class DistributedDataParallel(nn.Module):
         torch.autograd.Variable._execution_engine.queue_callback(self._finish_pass)
 
     def _on_grad_ready(self, p):
-        if not torch.is_grad_enabled() and not self._pass_active:
-            pass
         if not self._pass_active:
             self._start_pass()
         if id(p) in self._ready:

@@ -1,0 +1,160 @@
+"""Data-parallel engine on CPU ranks (gloo, world_size 2) — the fake-comm-backend strategy of
+SURVEY §4 item 3: bucketing, gradient averaging, unused parameters (EfficientNet-B0), rank-0
+state/buffer broadcast and DistributedSampler-equivalent sharding, without GPUs."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    from pytorch_cifar_amd.parallel.launcher import init_distributed
+
+    ctx = init_distributed(rank, world, rank, backend="gloo")
+    try:
+        res = fn(ctx)
+        torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        ctx.shutdown()
+
+
+def run_ranks(fn, world=2):
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, port, fn, d), nprocs=world, join=True)
+        return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]
+
+
+# ---------------------------------------------------------------------------- scenarios
+def _grad_avg(ctx):
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.ops.functional import cross_entropy
+    from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(100 + ctx.rank)  # different init per rank: DDP must broadcast rank 0's
+    model = models.LeNet()
+    ddp = DistributedDataParallel(model, ctx, bucket_cap_mb=0.01, first_bucket_mb=0.01)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 3, 32, 32, generator=g)
+    y = torch.randint(0, 10, (8,), generator=g)
+    xs, ys = x[ctx.rank * 4:(ctx.rank + 1) * 4], y[ctx.rank * 4:(ctx.rank + 1) * 4]
+    loss = cross_entropy(ddp(xs), ys)
+    loss.backward()
+    return {"params": {n: p.detach().clone() for n, p in model.named_parameters()},
+            "grads": {n: p.grad.detach().clone() for n, p in model.named_parameters()},
+            "buckets": ddp.bucket_sizes_mib(), "x": x, "y": y}
+
+
+def test_ddp_broadcast_and_gradient_average():
+    r0, r1 = run_ranks(_grad_avg)
+    for n in r0["params"]:
+        torch.testing.assert_close(r0["params"][n], r1["params"][n])  # C3 initial broadcast
+        torch.testing.assert_close(r0["grads"][n], r1["grads"][n])    # all-reduced (avg)
+    assert len(r0["buckets"]) > 1
+    # oracle: mean of the two half-batch gradients computed in one process with rank 0's weights
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.ops.functional import cross_entropy
+
+    m = models.LeNet()
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            p.copy_(r0["params"][n])
+    acc = {n: torch.zeros_like(p) for n, p in m.named_parameters()}
+    for r in range(2):
+        m.zero_grad()
+        cross_entropy(m(r0["x"][r * 4:(r + 1) * 4]), r0["y"][r * 4:(r + 1) * 4]).backward()
+        for n, p in m.named_parameters():
+            acc[n] += p.grad / 2
+    for n in acc:
+        torch.testing.assert_close(r0["grads"][n], acc[n], rtol=1e-4, atol=1e-6)
+
+
+def _unused(ctx):
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.ops.functional import cross_entropy
+    from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    model = models.EfficientNetB0()
+    ddp = DistributedDataParallel(model, ctx)
+    x = torch.randn(2, 3, 32, 32)
+    y = torch.randint(0, 10, (2,))
+    for _ in range(2):  # the reference's default DDP crashed on the 2nd iteration
+        model.zero_grad(set_to_none=False)
+        cross_entropy(ddp(x), y).backward()
+    unused = sorted(n for n, p in model.named_parameters() if any(p is q for q in ddp.last_unused))
+    return {"unused": unused,
+            "g": model.layers[0].conv1.weight.grad.abs().max().item(),
+            "bn_buf": model.bn1.running_mean.clone()}
+
+
+def test_ddp_unused_parameters_efficientnet():
+    r0, r1 = run_ranks(_unused)
+    assert r0["unused"] == ["layers.0.bn1.bias", "layers.0.bn1.weight", "layers.0.conv1.weight"]
+    assert r0["g"] == 0.0 and r1["g"] == 0.0
+
+
+def _buffers(ctx):
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    model = models.ResNet18()
+    ddp = DistributedDataParallel(model, ctx)
+    x = torch.randn(2, 3, 32, 32) * (1 + ctx.rank)  # different data -> different local BN stats
+    ddp(x).sum().backward()
+    after_first = model.bn1.running_mean.clone()
+    model.eval()  # eval forward: no local running-stat update after the broadcast
+    with torch.no_grad():
+        ddp(x)  # grad-enabled previous forward -> rank 0's buffers are broadcast first (C4)
+    return {"after_first": after_first, "synced": model.bn1.running_mean.clone()}
+
+
+def test_ddp_broadcast_buffers():
+    r0, r1 = run_ranks(_buffers)
+    assert not torch.allclose(r0["after_first"], r1["after_first"])  # no SyncBN: local stats
+    torch.testing.assert_close(r1["synced"], r0["after_first"])      # rank 0's buffers won
+
+
+def test_bucket_layout_resnet18():
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.parallel.launcher import DistContext
+    from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
+
+    m = models.ResNet18()
+    ddp = DistributedDataParallel(m, DistContext())
+    sizes = ddp.bucket_sizes_mib()
+    assert sizes[0] <= 1.0  # small first bucket: the reduction pipeline starts early in backward
+    assert abs(sum(sizes) - sum(p.numel() for p in m.parameters()) * 4 / 2 ** 20) < 0.5
+    assert all(s <= 25 for s in sizes)
+
+
+def test_shard_sampler_matches_torch_distributed_sampler():
+    from torch.utils.data.distributed import DistributedSampler
+
+    from pytorch_cifar_amd.data.loader import ShardSampler
+
+    ds = list(range(1003))
+    for world in (1, 2, 3, 8):
+        for rank in range(world):
+            for epoch in (0, 5):
+                a = ShardSampler(len(ds), world, rank, shuffle=True, seed=0)
+                b = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=0)
+                a.set_epoch(epoch)
+                b.set_epoch(epoch)
+                assert a.indices().tolist() == list(iter(b))
