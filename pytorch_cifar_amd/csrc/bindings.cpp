@@ -16,12 +16,16 @@ namespace pca {
 // conv_mfma.hip
 void conv_fwd_launch(const bf16*, const bf16*, const float*, bf16*, float*, int, int, int, int, int,
                      int, int, int, int, int, int, int, hipStream_t);
-int conv_fwd_stat_rows(int M, int Cout, int groups);
+int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                       int groups, int Ho, int Wo);
 void set_conv_tile(int kind, int idx);
 void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int, int, int, int,
                        int, int, int, int, hipStream_t);
-void conv_wgrad_launch(const bf16*, const bf16*, float*, int, int, int, int, int, int, int, int,
-                       int, int, int, int, hipStream_t);
+void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
+                       int Cin, int Cout, int KH, int KW, int stride, int pad, int groups, int Ho,
+                       int Wo, hipStream_t st);
+int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                             int pad, int groups, int Ho, int Wo);
 // batchnorm.hip
 int bn_row_blocks(int M, int C);
 void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t);
@@ -127,7 +131,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
   auto y = at::empty({N, Ho, Wo, Cout}, x.options());
   Tensor stats;
   if (want_stats) {
-    const int gm = pca::conv_fwd_stat_rows(N * Ho * Wo, Cout, groups);
+    const int gm = pca::conv_fwd_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
     stats = at::empty({gm, 2, Cout}, x.options().dtype(at::kFloat));
   }
   if (bias.has_value() && bias->defined()) {
@@ -178,8 +182,12 @@ Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride,
   } else {
     dw = at::zeros({Cout, KH, KW, Cin / groups}, x.options().dtype(at::kFloat));
   }
-  pca::conv_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), ptr<float>(dw), N, H, W, Cin, Cout, KH, KW,
-                         stride, pad, groups, Ho, Wo, cur_stream());
+  // slab workspace of the wide kernel (partial tiles, reduced into dw in a fixed order)
+  const int64_t wsn = pca::conv_wgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  Tensor ws;
+  if (wsn > 0) ws = at::empty({wsn}, x.options().dtype(at::kFloat));
+  pca::conv_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), ptr<float>(dw), wsn > 0 ? ptr<float>(ws) : nullptr,
+                         N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, cur_stream());
   return dw;
 }
 

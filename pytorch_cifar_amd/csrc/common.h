@@ -71,6 +71,7 @@ __device__ __forceinline__ T wave_max(T v) {
 }
 
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ __forceinline__ int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, "XCD swizzle must be
 // bijective"): blocks b and b+8 share an XCD, so give each XCD a contiguous chunk of tiles.

@@ -25,55 +25,11 @@
 // staging (the previous register-staged version spilled its staging arrays to scratch).
 // The XOR swizzle of each LDS row is applied on the DMA *source* address (the DMA writes
 // lane-linearly) and on the fragment read address (rule 21: both sides or neither).
-#include "common.h"
+#include "mfma_util.h"
 
 #include <algorithm>
 
 namespace pca {
-
-// Exact unsigned division by a runtime constant (n < 2^31): q = (umulhi(n, m) + n) >> s.
-struct FastDiv {
-  uint32_t d, m, s;
-};
-
-static inline FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  f.d = d;
-  uint32_t s = 0;
-  while ((1ull << s) < d) ++s;
-  f.s = s;
-  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-  return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  const uint64_t t = (uint64_t)__umulhi(n, f.m) + n;
-  return (uint32_t)(t >> f.s);
-}
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
-}
-
-// one 16-byte-per-lane LDS-DMA (1 KiB per wave instruction at lds_base + 16*lane)
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_base, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_base, 16, (int)voff, 0, 0, 0);
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-constexpr uint32_t kOOB = 0x80000000u;  // byte offset past any descriptor range -> zeros
 
 struct ConvGeom {
   int N;                // batch
@@ -97,26 +53,28 @@ struct ConvGeom {
 // the taps kh = (ph+pad)&1 (+2...), so no MFMA work is spent on the 3/4 of taps that a strided
 // transposed convolution would multiply by zero.
 template <int BM, int BN, int WM, int WN, int STAGES, int MODE, bool STATS>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict__ A,
-                                                         const bf16* __restrict__ B,
-                                                         bf16* __restrict__ Y,
-                                                         float* __restrict__ stats,
-                                                         const float* __restrict__ bias,
-                                                         const ConvGeom g) {
+__global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __restrict__ A,
+                                                                  const bf16* __restrict__ B,
+                                                                  bf16* __restrict__ Y,
+                                                                  float* __restrict__ stats,
+                                                                  const float* __restrict__ bias,
+                                                                  const ConvGeom g) {
+  constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BK = 64;                 // K elements per stage: 128-byte LDS rows
   constexpr int RB = BK * 2;
   constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int A_PW = BM / 32;          // DMA instructions (8 rows each) per wave per stage
-  constexpr int B_PW = BN / 32;
+  constexpr int A_PW = BM / (8 * NW);    // DMA instructions (8 rows each) per wave per stage
+  constexpr int B_PW = BN / (8 * NW);
   constexpr int LPS = A_PW + B_PW;       // loads per stage per lane
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int CST = BN + 8;            // padded bf16 row stride of the staged C tile
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(A_PW >= 1 && B_PW >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
   static_assert(STAGES >= 2, "stages");
   static_assert(BM * CST * 2 <= STAGES * STAGE, "C tile must fit the LDS ring");
+  static_assert((BM * (BN / 8)) % NT == 0, "epilogue store loop");
 
   __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
 
@@ -129,7 +87,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict_
   const int cls = PARITY ? (blockIdx.z & 3) : 0;
   const int ph = cls >> 1, pw = cls & 1;
   // tap sets: kh = kh0 + tstep*t for t < nth (all taps unless PARITY)
-  const int tstep = PARITY ? 2 : 1;
   const int kh0 = PARITY ? ((ph + g.pad) & 1) : 0;
   const int kw0 = PARITY ? ((pw + g.pad) & 1) : 0;
   const int nth = PARITY ? ((g.KH - kh0 + 1) >> 1) : g.KH;
@@ -153,6 +110,20 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict_
   const int crg = g.Cr >> 3;
   const int KT = cdiv(Kcls, BK);
 
+  // Fast path: every K-step lies inside ONE tap (Cr % 64 == 0) and the gathered pixel is
+  // (row base + scalar tap offset) — true for the forward, the stride-1 dgrad and every parity
+  // class. The tap walk is then pure SALU and each DMA costs a few VALU ops (bounds + offset).
+  const bool fast = (g.Cr % BK == 0) && (MODE != 1 || g.stride == 1);
+  const int ksub = g.Cr / BK;              // K-steps per tap (fast path)
+
+  // per-lane B row byte offsets (tap-independent part), fixed for the whole kernel
+  int b_off[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int br = n0 + (wid * B_PW + i) * 8 + lrow;
+    b_off[i] = br < g.Cn ? ((grp * g.Cn + br) * kfull + lchunk * 8) * 2 : -1;
+  }
+
   // per-lane BatchNorm partial sums, accumulated over every tile this workgroup owns
   float st_s[TN], st_q[TN];
 #pragma unroll
@@ -163,6 +134,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict_
   for (int tile = blockIdx.x; tile < mtiles; tile += gridDim.x) {
     const int m0 = tile * BM;
     int a_n[A_PW], a_h[A_PW], a_w[A_PW];
+    int f_h[A_PW], f_w[A_PW], f_off[A_PW];   // fast path: gather base row/col and byte offset
 #pragma unroll
     for (int i = 0; i < A_PW; ++i) {
       const int r = m0 + (wid * A_PW + i) * 8 + lrow;
@@ -170,14 +142,67 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict_
       const uint32_t n = fdiv(rr, g.fd_hw);
       const uint32_t rem = rr - n * (rows_h * rows_w);
       const uint32_t h = fdiv(rem, g.fd_w);
+      const uint32_t w = rem - h * rows_w;
       a_n[i] = r < Mrows ? (int)n : -1;
       a_h[i] = PARITY ? (int)(2 * h + ph) : (int)h;
-      a_w[i] = PARITY ? (int)(2 * (rem - h * rows_w) + pw) : (int)(rem - h * rows_w);
+      a_w[i] = PARITY ? (int)(2 * w + pw) : (int)w;
+      int bh, bw;
+      if constexpr (!DGRAD) {
+        bh = (int)h * g.stride - g.pad;
+        bw = (int)w * g.stride - g.pad;
+      } else if constexpr (PARITY) {
+        bh = (int)h + ((ph + g.pad - kh0) >> 1);
+        bw = (int)w + ((pw + g.pad - kw0) >> 1);
+      } else {
+        bh = (int)h + g.pad;
+        bw = (int)w + g.pad;
+      }
+      f_off[i] = ((((int)n * g.Hs + bh) * g.Ws + bw) * g.Cs + grp * g.Cr + lchunk * 8) * 2;
+      if (r >= Mrows) bh = -(1 << 20);      // fails every bounds test (n = 0: no overflow)
+      f_h[i] = bh;
+      f_w[i] = bw;
     }
+
+    // fast-path tap cursor (uniform): K-step kt = (tap, sub) with tap = (th, tw)
+    int cur_sub = 0, cur_th = 0, cur_tw = 0, cur_kt = 0;
 
     auto issue = [&](int kt, int buf) {
       char* As = smem + buf * STAGE;
       char* Bs = As + A_BYTES;
+      if (fast) {
+        const bool kok = cur_kt < KT;
+        int dh, dw, kh, kw;
+        if constexpr (!DGRAD) {
+          dh = cur_th; dw = cur_tw; kh = cur_th; kw = cur_tw;
+        } else if constexpr (PARITY) {
+          dh = -cur_th; dw = -cur_tw; kh = kh0 + 2 * cur_th; kw = kw0 + 2 * cur_tw;
+        } else {
+          dh = -cur_th; dw = -cur_tw; kh = cur_th; kw = cur_tw;
+        }
+        const int a_delta = ((dh * g.Ws + dw) * g.Cs + cur_sub * BK) * 2;
+        const int b_delta = ((kh * g.KW + kw) * g.Cr + cur_sub * BK) * 2;
+#pragma unroll
+        for (int i = 0; i < A_PW; ++i) {
+          const bool ok = kok && (uint32_t)(f_h[i] + dh) < (uint32_t)g.Hs &&
+                          (uint32_t)(f_w[i] + dw) < (uint32_t)g.Ws;
+          dma16(rsA, As + (wid * A_PW + i) * 1024, ok ? (uint32_t)(f_off[i] + a_delta) : kOOB);
+        }
+#pragma unroll
+        for (int i = 0; i < B_PW; ++i) {
+          const bool ok = kok && b_off[i] >= 0;
+          dma16(rsB, Bs + (wid * B_PW + i) * 1024, ok ? (uint32_t)(b_off[i] + b_delta) : kOOB);
+        }
+        // advance the cursor
+        ++cur_kt;
+        if (++cur_sub == ksub) {
+          cur_sub = 0;
+          if (++cur_tw == ntw) {
+            cur_tw = 0;
+            ++cur_th;
+          }
+        }
+        return;
+      }
       const int kg = kt * 8 + lchunk;                  // 8-channel granule along K
       const bool kok = kg * 8 < Kcls;
       const int tap = kok ? (int)fdiv(kg, g.fd_cr8) : 0;
@@ -239,6 +264,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict_
       issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);   // past-the-end stages load zeros
       const char* As = smem + (kt % STAGES) * STAGE;
       const char* Bs = As + A_BYTES;
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
         bf16x8 af[TM], bfv[TN];
@@ -259,6 +285,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict_
           for (int ni = 0; ni < TN; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfv[ni], acc[mi][ni], 0, 0, 0);
       }
+      __builtin_amdgcn_s_setprio(0);
     }
     wait_vmcnt<0>();
     __syncthreads();
@@ -304,8 +331,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict_
     __syncthreads();
     constexpr int CG = BN / 8;
 #pragma unroll
-    for (int it = 0; it < (BM * CG) / 256; ++it) {
-      const int idx = tid + it * 256;
+    for (int it = 0; it < (BM * CG) / NT; ++it) {
+      const int idx = tid + it * NT;
       const int r = idx / CG, c8 = idx % CG;
       const int gm = m0 + r, gc = n0 + c8 * 8;
       if (gm < Mrows && gc < g.Cn) {
@@ -360,16 +387,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const bf16* __restrict_
 // ---------------------------------------------------------------------------------------
 // wgrad: split-K GEMM over pixels with transposed LDS reads
 // ---------------------------------------------------------------------------------------
-// LDS image of a [BKP pixel][COLS channel] tile: 16-byte chunk c of pixel-row r lives at
-// r*RB + 16*(c ^ tr_swz(r)). The XOR spreads the 8 rows one ds_read_b64_tr_b16 half-wave
-// touches (rows k0..k0+3 and k0+8..k0+11) over all 64 banks.
-template <int RB>
-__device__ __forceinline__ int tr_swz(int r) {
-  if constexpr (RB == 256) return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
-  else if constexpr (RB == 128) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
-  else return 2 * ((r >> 3) & 1);
-}
-
 struct WgradGeom {
   int N, H, W, Cx;       // input X dims (NHWC), Cx total channels
   int Ho, Wo, Cy;        // dY dims, Cy total channels
@@ -380,28 +397,10 @@ struct WgradGeom {
   int Ktot;              // KH*KW*cin_g (GEMM N)
   int chunk;             // pixels per split
   int splits;
+  int atomic;            // wide kernel: 1 = fp32 atomics into dW, 0 = slab rows + reduce
   uint32_t x_bytes, dy_bytes;
   FastDiv fd_hw, fd_w, fd_cin8;
 };
-
-template <int COLS>
-__device__ __forceinline__ bf16x8 tr_frag(const char* base, int k0, int c0, int lane) {
-  constexpr int RB = COLS * 2;
-  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-  typedef short i16x8 __attribute__((ext_vector_type(8)));
-  const int li = lane & 15;
-  const int q = li >> 2, p = li & 3;
-  const int col = c0 + 4 * p;
-  const int chunk = col >> 3;
-  const int r0 = k0 + 8 * (lane >> 4) + q;
-  const int r1 = r0 + 4;
-  const int b0 = r0 * RB + ((chunk ^ tr_swz<RB>(r0)) << 4) + ((col & 7) << 1);
-  const int b1 = r1 * RB + ((chunk ^ tr_swz<RB>(r1)) << 4) + ((col & 7) << 1);
-  const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + b0));
-  const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + b1));
-  const i16x8 v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 template <int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(const bf16* __restrict__ X,
@@ -524,6 +523,185 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const bf16* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------
+// wide wgrad: all taps of a 64-channel block per workgroup, blocked LDS images, slab output
+// ---------------------------------------------------------------------------------------
+// For Cin/G % 64 == 0 the GEMM column axis (tap, ci) splits into 64-column blocks that each lie
+// inside ONE tap, so a block's gather is a scalar tap offset on a per-pixel base: the per-DMA
+// cost is a bounds test and an add. Both operands are staged as blocked images
+// [64-channel block][KP pixels][128 B] (the RB = 128 swizzle of tr_frag), so one workgroup can
+// own a wide column tile (up to 9 blocks = all 9 taps of 64 channels) and x / dY are read from
+// memory once per column tile instead of once per 128 columns. Each workgroup walks a contiguous
+// pixel range and writes its fp32 partial tile to a slab row; a reduce kernel then adds the slab
+// rows into dW in a fixed order (deterministic, no atomics).
+template <int MB, int NB, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_wide_kernel(const bf16* __restrict__ X,
+                                                                       const bf16* __restrict__ DY,
+                                                                       float* __restrict__ slab,
+                                                                       const WgradGeom g) {
+  constexpr int NW = WM * WN;
+  constexpr int KP = 32;                         // pixels per stage (one MFMA K step)
+  constexpr int BLK = KP * 128;                  // bytes of one 64-channel block image
+  constexpr int NOPS = MB + NB;                  // operand blocks per stage
+  constexpr int STAGE = NOPS * BLK;
+  constexpr int BM = MB * 64, BN = NB * 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int OPW = (NOPS + NW - 1) / NW;      // operand blocks per wave (last may be idle)
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int split = blockIdx.z % g.splits;
+  const int grp = blockIdx.z / g.splits;
+  const int m0 = blockIdx.x * BM;                // output channel (within group)
+  const int n0 = blockIdx.y * BN;                // (tap, ci) column
+  const int p_begin = split * g.chunk;
+  const int p_end = min(g.P, p_begin + g.chunk);
+
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(X, g.x_bytes);
+  const __amdgpu_buffer_rsrc_t rsD = make_rsrc(DY, g.dy_bytes);
+
+  // lane -> (row (l>>3) + 8i of the stage, logical 16-byte chunk) for the 4 row groups
+  int lch[KP / 8];
+#pragma unroll
+  for (int i = 0; i < KP / 8; ++i) lch[i] = ((lane & 7) ^ tr_swz<128>(8 * i + (lane >> 3))) * 16;
+
+  // scalar per-operand-block gather parameters (this wave's blocks only)
+  int o_kind[OPW], o_col[OPW], o_dh[OPW], o_dw[OPW];
+#pragma unroll
+  for (int j = 0; j < OPW; ++j) {
+    const int o = wid + NW * j;
+    o_kind[j] = o < NOPS ? (o < MB ? 0 : 1) : 2;
+    o_col[j] = 0; o_dh[j] = 0; o_dw[j] = 0;
+    if (o < MB) {
+      const int co = m0 + 64 * o;
+      o_kind[j] = co < g.cout_g ? 0 : 2;
+      o_col[j] = (grp * g.cout_g + co) * 2;
+    } else if (o < NOPS) {
+      const int col = n0 + 64 * (o - MB);
+      if (col >= g.Ktot) {
+        o_kind[j] = 2;
+      } else {
+        const int tap = col / g.cin_g, ci = col - tap * g.cin_g;
+        const int kh = tap / g.KW, kw = tap - kh * g.KW;
+        o_dh[j] = kh;
+        o_dw[j] = kw;
+        o_col[j] = ((kh * g.W + kw) * g.Cx + grp * g.cin_g + ci) * 2;
+      }
+    }
+  }
+
+  auto issue = [&](int pbase, int buf) {
+    char* S = smem + buf * STAGE;
+    int ih0[KP / 8], iw0[KP / 8], xo[KP / 8], dyo[KP / 8];
+    bool pv[KP / 8];
+#pragma unroll
+    for (int i = 0; i < KP / 8; ++i) {
+      const int p = pbase + 8 * i + (lane >> 3);
+      pv[i] = p < p_end;
+      const uint32_t pp = pv[i] ? p : 0;
+      const uint32_t n = fdiv(pp, g.fd_hw);
+      const uint32_t rem = pp - n * (g.Ho * g.Wo);
+      const uint32_t oh = fdiv(rem, g.fd_w);
+      const uint32_t ow = rem - oh * g.Wo;
+      ih0[i] = (int)oh * g.stride - g.pad;
+      iw0[i] = (int)ow * g.stride - g.pad;
+      xo[i] = ((((int)n * g.H + ih0[i]) * g.W + iw0[i]) * g.Cx) * 2 + lch[i];
+      dyo[i] = (int)pp * g.Cy * 2 + lch[i];
+    }
+#pragma unroll
+    for (int j = 0; j < OPW; ++j) {
+      const int o = wid + NW * j;
+      if (o_kind[j] == 2) {
+        if (o < NOPS) {   // column / channel tail: keep the block's image zero
+#pragma unroll
+          for (int i = 0; i < KP / 8; ++i) dma16(rsX, S + o * BLK + i * 1024, kOOB);
+        }
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < KP / 8; ++i) {
+        uint32_t off;
+        if (o_kind[j] == 0) {
+          off = pv[i] ? (uint32_t)(dyo[i] + o_col[j]) : kOOB;
+          dma16(rsD, S + o * BLK + i * 1024, off);
+        } else {
+          const bool ok = pv[i] && (uint32_t)(ih0[i] + o_dh[j]) < (uint32_t)g.H &&
+                          (uint32_t)(iw0[i] + o_dw[j]) < (uint32_t)g.W;
+          off = ok ? (uint32_t)(xo[i] + o_col[j]) : kOOB;
+          dma16(rsX, S + o * BLK + i * 1024, off);
+        }
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = p_end > p_begin ? cdiv(p_end - p_begin, KP) : 0;
+  issue(p_begin, 0);
+  for (int kt = 0; kt < KT; ++kt) {
+    wait_vmcnt<0>();
+    raw_barrier();
+    if (kt + 1 < KT) issue(p_begin + (kt + 1) * KP, (kt + 1) & 1);
+    const char* S = smem + (kt & 1) * STAGE;
+    bf16x8 af[TM];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = wm * WTM + mi * 16;
+      af[mi] = tr_frag<64>(S + (m >> 6) * BLK, 0, m & 63, lane);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int n = wn * WTN + ni * 16;
+      const bf16x8 bfv = tr_frag<64>(S + (MB + (n >> 6)) * BLK, 0, n & 63, lane);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfv, acc[mi][ni], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+
+  // partial tile -> slab row (split), layout [splits][groups*cout_g][Ktot]
+  float* out = slab + (size_t)split * g.groups * g.cout_g * g.Ktot;
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + j;
+        const int n = n0 + wn * WTN + ni * 16 + (lane & 15);
+        if (m < g.cout_g && n < g.Ktot) {
+          const size_t idx = ((size_t)grp * g.cout_g + m) * g.Ktot + n;
+          if (g.atomic) atomicAdd(slab + idx, acc[mi][ni][j]);
+          else out[idx] = acc[mi][ni][j];
+        }
+      }
+}
+
+// dW[i] += sum_s slab[s][i], fixed summation order (float4 lanes)
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab,
+                                                                float* __restrict__ dw, int splits,
+                                                                int64_t n4) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float4* s4 = reinterpret_cast<const float4*>(slab);
+  float4 a = reinterpret_cast<float4*>(dw)[i];
+  for (int s = 0; s < splits; ++s) {
+    const float4 v = s4[(int64_t)s * n4 + i];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  reinterpret_cast<float4*>(dw)[i] = a;
+}
+
+// ---------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------
 static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co, int KH, int KW,
@@ -545,21 +723,67 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   return g;
 }
 
-// persistent grid: at most kMaxTilesX workgroups along M (also the BN slab row count)
+// Persistent grid. grid.x (M-tile walkers, also the BN-statistics slab row count, <= 1024) is
+// sized so that grid.x * grid.y * grid.z fills exactly the resident workgroup slots of the chip
+// (occupancy x CUs): a grid of 1024 walkers over 768 slots would run a second, one-third-full
+// round of blocks (measured: the 64-channel layers lost ~25% to that tail).
 constexpr int kMaxTilesX = 1024;
-static int igemm_grid_x(int M, int BM) { return std::min(cdiv(M, BM), kMaxTilesX); }
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+template <int BM, int BN, int WM, int WN, int ST, int MODE>
+static int igemm_occupancy() {
+  static int occ = 0;
+  if (occ == 0) {
+    int a = 0, b = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &a, (const void*)conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, true>, WM * WN * 64, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &b, (const void*)conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, false>, WM * WN * 64, 0);
+    occ = std::max(1, std::min(a, b));
+  }
+  return occ;
+}
+
+static int persistent_grid_x(int mtiles, int gyz, int occ) {
+  const int slots = occ * num_cus();
+  int gx = std::max(1, slots / std::max(1, gyz));
+  gx = std::min({gx, mtiles, kMaxTilesX});
+  const int per = cdiv(mtiles, gx);   // equalise tiles per walker
+  return cdiv(mtiles, per);
+}
+
+template <int MODE>
+static int igemm_rows(const ConvGeom& g) {
+  return MODE == 2 ? g.N * (g.Ho / 2) * (g.Wo / 2) : g.M;
+}
+
+template <int BM, int BN, int WM, int WN, int ST, int MODE>
+static int igemm_grid_x_t(const ConvGeom& g) {
+  const int gyz = cdiv(g.Cn, BN) * g.groups * (MODE == 2 ? 4 : 1);
+  return persistent_grid_x(cdiv(igemm_rows<MODE>(g), BM), gyz, igemm_occupancy<BM, BN, WM, WN, ST, MODE>());
+}
 
 template <int BM, int BN, int WM, int WN, int ST, int MODE>
 static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, const float* bias,
                          const ConvGeom& g, hipStream_t st) {
-  const int rows = MODE == 2 ? g.N * (g.Ho / 2) * (g.Wo / 2) : g.M;
-  dim3 grid(igemm_grid_x(rows, BM), cdiv(g.Cn, BN), g.groups * (MODE == 2 ? 4 : 1));
+  dim3 grid(igemm_grid_x_t<BM, BN, WM, WN, ST, MODE>(g), cdiv(g.Cn, BN),
+            g.groups * (MODE == 2 ? 4 : 1));
   if (stats)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, true>), grid, dim3(256), 0, st,
-                       A, B, Y, stats, bias, g);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, true>), grid,
+                       dim3(WM * WN * 64), 0, st, A, B, Y, stats, bias, g);
   else
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, false>), grid, dim3(256), 0, st,
-                       A, B, Y, stats, bias, g);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, false>), grid,
+                       dim3(WM * WN * 64), 0, st, A, B, Y, stats, bias, g);
 }
 
 // Tile configurations. The heuristic picks by GEMM N (channels per group); a process-wide
@@ -574,38 +798,60 @@ void set_conv_tile(int kind, int idx) {
 
 static int igemm_select(const ConvGeom& g) {
   if (g_igemm_override >= 0) return g_igemm_override;
-  // measured on MI355X (tools/bench_conv.py, profiles/conv_sweep_r1.md): two-stage rings at
-  // 2-3 workgroups/CU beat deeper rings at one workgroup/CU on every ResNet-18 shape.
+  // measured on MI355X (tools/bench_conv.py, profiles/conv_census_r1.md)
   if (g.Cn > 64) return 3;
   if (g.Cn > 32) return 4;
   return 8;
 }
 
-static int igemm_bm(int cfg) { return cfg == 6 || cfg == 7 ? 256 : 128; }
+// X(cfg, BM, BN, WM, WN, STAGES)
+#define PCA_IGEMM_CFGS(X)            \
+  X(0, 128, 128, 2, 2, 3)            \
+  X(1, 128, 64, 2, 2, 4)             \
+  X(2, 128, 32, 4, 1, 4)             \
+  X(3, 128, 128, 2, 2, 2)            \
+  X(4, 128, 64, 2, 2, 2)             \
+  X(5, 128, 64, 4, 1, 3)             \
+  X(6, 256, 64, 4, 1, 3)             \
+  X(7, 256, 128, 2, 2, 2)            \
+  X(8, 128, 32, 4, 1, 2)             \
+  X(9, 256, 128, 4, 2, 3)            \
+  X(10, 256, 64, 4, 2, 3)            \
+  X(11, 256, 64, 4, 2, 4)            \
+  X(12, 256, 128, 4, 2, 2)           \
+  X(13, 512, 64, 8, 1, 2)            \
+  X(14, 128, 128, 2, 4, 3)           \
+  X(15, 128, 64, 4, 2, 4)
 
 template <int MODE>
 static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, const float* bias,
                            const ConvGeom& g, hipStream_t st) {
   switch (igemm_select(g)) {
-    case 0: launch_igemm<128, 128, 2, 2, 3, MODE>(A, B, Y, stats, bias, g, st); break;
-    case 1: launch_igemm<128, 64, 2, 2, 4, MODE>(A, B, Y, stats, bias, g, st); break;
-    case 2: launch_igemm<128, 32, 4, 1, 4, MODE>(A, B, Y, stats, bias, g, st); break;
-    case 3: launch_igemm<128, 128, 2, 2, 2, MODE>(A, B, Y, stats, bias, g, st); break;
-    case 4: launch_igemm<128, 64, 2, 2, 2, MODE>(A, B, Y, stats, bias, g, st); break;
-    case 5: launch_igemm<128, 64, 4, 1, 3, MODE>(A, B, Y, stats, bias, g, st); break;
-    case 6: launch_igemm<256, 64, 4, 1, 3, MODE>(A, B, Y, stats, bias, g, st); break;
-    case 7: launch_igemm<256, 128, 2, 2, 2, MODE>(A, B, Y, stats, bias, g, st); break;
-    case 8: launch_igemm<128, 32, 4, 1, 2, MODE>(A, B, Y, stats, bias, g, st); break;
-    default: launch_igemm<128, 128, 2, 2, 3, MODE>(A, B, Y, stats, bias, g, st); break;
+#define PCA_CASE(C, BM, BN, WM, WN, ST) \
+    case C: launch_igemm<BM, BN, WM, WN, ST, MODE>(A, B, Y, stats, bias, g, st); break;
+    PCA_IGEMM_CFGS(PCA_CASE)
+#undef PCA_CASE
+    default: launch_igemm<128, 128, 2, 2, 2, MODE>(A, B, Y, stats, bias, g, st); break;
+  }
+}
+
+template <int MODE>
+static int igemm_grid_x(const ConvGeom& g) {
+  switch (igemm_select(g)) {
+#define PCA_CASE(C, BM, BN, WM, WN, ST) \
+    case C: return igemm_grid_x_t<BM, BN, WM, WN, ST, MODE>(g);
+    PCA_IGEMM_CFGS(PCA_CASE)
+#undef PCA_CASE
+    default: return igemm_grid_x_t<128, 128, 2, 2, 2, MODE>(g);
   }
 }
 
 // number of BN-statistics slab rows the forward launch will write (= grid.x)
-int conv_fwd_stat_rows(int M, int Cout, int groups) {
-  ConvGeom g;
-  g.Cn = Cout / groups;
-  g.M = M;
-  return igemm_grid_x(M, igemm_bm(igemm_select(g)));
+int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                       int groups, int Ho, int Wo) {
+  ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
+                         Cout / groups);
+  return igemm_grid_x<0>(g);
 }
 
 void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, float* stats, int N,
@@ -648,9 +894,28 @@ static void launch_wgrad(const bf16* x, const bf16* dy, float* dw, WgradGeom g, 
   hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, ST>), grid, dim3(256), 0, st, x, dy, dw, g);
 }
 
-void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, int N, int H, int W, int Cin,
-                       int Cout, int KH, int KW, int stride, int pad, int groups, int Ho, int Wo,
-                       hipStream_t st) {
+// wide-kernel configurations: X(cfg, MB, NB, WM, WN)  (tile = 64*MB cout x 64*NB columns)
+#define PCA_WIDE_CFGS(X) \
+  X(16, 1, 9, 1, 4)      \
+  X(17, 2, 9, 2, 4)      \
+  X(18, 2, 4, 2, 2)      \
+  X(19, 1, 4, 1, 4)      \
+  X(20, 2, 8, 2, 4)      \
+  X(21, 4, 4, 4, 2)
+
+template <int MB, int NB, int WM, int WN>
+static int wide_occupancy() {
+  static int occ = 0;
+  if (occ == 0) {
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, (const void*)conv_wgrad_wide_kernel<MB, NB, WM, WN>, WM * WN * 64, 0);
+    occ = std::max(1, occ);
+  }
+  return occ;
+}
+
+static WgradGeom wgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                            int pad, int groups, int Ho, int Wo) {
   WgradGeom g;
   g.N = N; g.H = H; g.W = W; g.Cx = Cin;
   g.Ho = Ho; g.Wo = Wo; g.Cy = Cout;
@@ -663,10 +928,95 @@ void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, int N, int H, i
   g.fd_hw = make_fastdiv(Ho * Wo);
   g.fd_w = make_fastdiv(Wo);
   g.fd_cin8 = make_fastdiv(g.cin_g / 8);
+  g.chunk = 0; g.splits = 1; g.atomic = 1;
+  return g;
+}
+
+static int wgrad_select(const WgradGeom& g) {
+  const bool wide_ok = g.cin_g % 64 == 0 && g.cout_g % 64 == 0;
+  int cfg = g_wgrad_override >= 32 ? -1 : g_wgrad_override;
+  if (cfg >= 16 && !wide_ok) cfg = -1;
+  if (cfg < 0) {
+    // measured (tools/bench_conv.py): the wide kernel only pays with all 9 taps in a tile and
+    // a stride of 1; strided / 1x1 wgrad stays on the split-K kernel
+    if (wide_ok && g.Ktot >= 9 * 64 && g.stride == 1) cfg = g.cout_g <= 64 ? 16 : 18;
+    else cfg = (g.cout_g > 64 && g.Ktot > 64) ? 3 : (g.cout_g > 32 ? 6 : 7);
+  }
+  return cfg;
+}
+
+// plan a wide launch: fills chunk/splits/atomic, returns the slab size in floats (0 = atomics)
+template <int MB, int NB, int WM, int WN>
+static int64_t wide_plan(WgradGeom& g) {
+  const int tiles = cdiv(g.cout_g, 64 * MB) * cdiv(g.Ktot, 64 * NB) * g.groups;
+  const int slots = wide_occupancy<MB, NB, WM, WN>() * num_cus();
+  int splits = std::max(1, slots / tiles);
+  splits = std::min(splits, std::max(1, cdiv(g.P, 256)));
+  int chunk = cdiv(cdiv(g.P, splits), 32) * 32;
+  splits = cdiv(g.P, chunk);
+  g.chunk = chunk;
+  g.splits = splits;
+  // few partials per output: atomics; many: slab rows + one ordered reduce
+  g.atomic = splits <= 8 ? 1 : 0;
+  return g.atomic ? 0 : (int64_t)splits * g.groups * g.cout_g * g.Ktot;
+}
+
+template <int MB, int NB, int WM, int WN>
+static void launch_wide(const bf16* x, const bf16* dy, float* dw, float* ws, WgradGeom g,
+                        hipStream_t st) {
+  const int64_t slab = wide_plan<MB, NB, WM, WN>(g);
+  dim3 grid(cdiv(g.cout_g, 64 * MB), cdiv(g.Ktot, 64 * NB), g.splits * g.groups);
+  hipLaunchKernelGGL((conv_wgrad_wide_kernel<MB, NB, WM, WN>), grid, dim3(WM * WN * 64), 0, st, x,
+                     dy, g.atomic ? dw : ws, g);
+  if (!g.atomic) {
+    const int64_t n4 = (int64_t)g.groups * g.cout_g * g.Ktot / 4;
+    (void)slab;
+    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)cdiv64(n4, 256)), dim3(256), 0, st,
+                       ws, dw, g.splits, n4);
+  }
+}
+
+// halo-staged 3x3/s1 wgrad (conv_halo.hip); selected by default where it applies, or forced
+// with set_conv_tile(1, 32 + halo cfg)
+int64_t wgrad_halo_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                             int pad, int groups);
+void wgrad_halo_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
+                       int Cin, int Cout, int groups, hipStream_t st);
+void set_halo_cfg(int cfg);
+
+static bool use_halo() { return g_wgrad_override < 0 || g_wgrad_override >= 32; }
+
+// workspace (floats) conv_wgrad_launch will need for this geometry under the current selection
+int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                             int pad, int groups, int Ho, int Wo) {
+  if (use_halo()) {
+    set_halo_cfg(g_wgrad_override >= 32 ? g_wgrad_override - 32 : -1);
+    const int64_t h = wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups);
+    if (h >= 0) return h;
+  }
+  WgradGeom g = wgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  switch (wgrad_select(g)) {
+#define PCA_CASE(C, MB, NB, WM, WN) \
+    case C: return wide_plan<MB, NB, WM, WN>(g);
+    PCA_WIDE_CFGS(PCA_CASE)
+#undef PCA_CASE
+    default: return 0;
+  }
+}
+
+void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
+                       int Cin, int Cout, int KH, int KW, int stride, int pad, int groups, int Ho,
+                       int Wo, hipStream_t st) {
+  if (use_halo()) {
+    set_halo_cfg(g_wgrad_override >= 32 ? g_wgrad_override - 32 : -1);
+    if (wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) >= 0) {
+      wgrad_halo_launch(x, dy, dw, ws, N, H, W, Cin, Cout, groups, st);
+      return;
+    }
+  }
+  WgradGeom g = wgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   const int target = 1024;
-  int cfg = g_wgrad_override;
-  if (cfg < 0) cfg = (g.cout_g > 64 && g.Ktot > 64) ? 3 : (g.cout_g > 32 ? 6 : 7);
-  switch (cfg) {
+  switch (wgrad_select(g)) {
     case 0: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, g, st, target); break;
     case 1: launch_wgrad<64, 128, 2, 2, 3>(x, dy, dw, g, st, target); break;
     case 2: launch_wgrad<32, 128, 1, 4, 3>(x, dy, dw, g, st, target); break;
@@ -675,6 +1025,10 @@ void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, int N, int H, i
     case 5: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, g, st, 512); break;
     case 6: launch_wgrad<64, 128, 2, 2, 2>(x, dy, dw, g, st, target); break;
     case 7: launch_wgrad<32, 128, 1, 4, 2>(x, dy, dw, g, st, target); break;
+#define PCA_CASE(C, MB, NB, WM, WN) \
+    case C: launch_wide<MB, NB, WM, WN>(x, dy, dw, ws, g, st); break;
+    PCA_WIDE_CFGS(PCA_CASE)
+#undef PCA_CASE
     default: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, g, st, target); break;
   }
 }

@@ -1,0 +1,82 @@
+// Device helpers shared by the MFMA convolution kernels (conv_mfma.hip, conv_halo.hip):
+// exact division by runtime constants, buffer descriptors + LDS-DMA, counted waits, raw
+// barriers and the transposed (ds_read_b64_tr_b16) fragment reads of [k][col] LDS images.
+#pragma once
+#include "common.h"
+
+namespace pca {
+
+// Exact unsigned division by a runtime constant (n < 2^31): q = (umulhi(n, m) + n) >> s.
+struct FastDiv {
+  uint32_t d, m, s;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  const uint64_t t = (uint64_t)__umulhi(n, f.m) + n;
+  return (uint32_t)(t >> f.s);
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+
+// one 16-byte-per-lane LDS-DMA (1 KiB per wave instruction at lds_base + 16*lane)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_base, 16, (int)voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+constexpr uint32_t kOOB = 0x80000000u;  // byte offset past any descriptor range -> zeros
+
+// LDS image of a [BKP pixel][COLS channel] tile: 16-byte chunk c of pixel-row r lives at
+// r*RB + 16*(c ^ tr_swz(r)). The XOR spreads the 8 rows one ds_read_b64_tr_b16 half-wave
+// touches (rows k0..k0+3 and k0+8..k0+11) over all 64 banks.
+template <int RB>
+__device__ __forceinline__ int tr_swz(int r) {
+  if constexpr (RB == 256) return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+  else if constexpr (RB == 128) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+  else return 2 * ((r >> 3) & 1);
+}
+
+template <int COLS>
+__device__ __forceinline__ bf16x8 tr_frag(const char* base, int k0, int c0, int lane) {
+  constexpr int RB = COLS * 2;
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const int li = lane & 15;
+  const int q = li >> 2, p = li & 3;
+  const int col = c0 + 4 * p;
+  const int chunk = col >> 3;
+  const int r0 = k0 + 8 * (lane >> 4) + q;
+  const int r1 = r0 + 4;
+  const int b0 = r0 * RB + ((chunk ^ tr_swz<RB>(r0)) << 4) + ((col & 7) << 1);
+  const int b1 = r1 * RB + ((chunk ^ tr_swz<RB>(r1)) << 4) + ((col & 7) << 1);
+  const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + b0));
+  const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + b1));
+  const i16x8 v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+}  // namespace pca

@@ -442,7 +442,7 @@ class _Act(torch.autograd.Function):
 def activation(x, act):
     if act in (None, "none"):
         return x
-    if _ref(x):
+    if _ref(x) or x.dim() != 4:  # classifier-head [N, F] activations: tiny, library elementwise
         return _ref_act(x, act)
     return to_nchw(_Act.apply(to_nhwc(x), ACT[act]))
 

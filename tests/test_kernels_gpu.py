@@ -80,6 +80,78 @@ def test_conv_fwd_dgrad_wgrad(C, case):
     assert rel_err(dw.permute(0, 3, 1, 2), w.grad) < 2e-2
 
 
+N_IGEMM_CFGS = 16
+
+
+@pytest.mark.parametrize("case", [(3, 64, 16, 64, 3, 1, 1, 1), (2, 128, 8, 256, 3, 2, 1, 1),
+                                  (2, 32, 8, 64, 3, 1, 1, 1), (3, 64, 7, 128, 3, 1, 1, 2),
+                                  (2, 64, 8, 128, 1, 2, 0, 1)])
+def test_conv_every_tile_config(C, case):
+    """Every compiled fwd/dgrad tile configuration (4- and 8-wave, fast scalar-tap path for
+    Cin % 64 == 0 and the generic gather otherwise, stride-2 parity dgrad, odd M tails)."""
+    N, Cin, H, Cout, k, s, p, G = case
+    torch.manual_seed(1)
+    x = bf(torch.randn(N, Cin, H, H, device="cuda"))
+    w = bf(torch.randn(Cout, Cin // G, k, k, device="cuda") * (2.0 / (Cin // G * k * k)) ** 0.5)
+    x.requires_grad_(True)
+    ref = F.conv2d(x, w, stride=s, padding=p, groups=G)
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    x_n = nhwc(x.detach()).to(torch.bfloat16)
+    wb, wt = C.weight_prep(w.permute(0, 2, 3, 1).contiguous(), G, True)
+    dy_n = nhwc(dy).to(torch.bfloat16)
+    bad = []
+    try:
+        for cfg in range(N_IGEMM_CFGS):
+            C.set_conv_tile(0, cfg)
+            y, stats = C.conv_fwd(x_n, wb, None, s, p, G, True)
+            dx = C.conv_dgrad(dy_n, wt, H, H, s, p, G)
+            e1, e2 = rel_err(nchw(y), ref), rel_err(nchw(dx), x.grad)
+            e3 = rel_err(stats[:, 0, :].sum(0), ref.detach().sum((0, 2, 3)))
+            if e1 > 2e-2 or e2 > 2e-2 or e3 > 1.2e-2:
+                bad.append((cfg, e1, e2, e3))
+    finally:
+        C.set_conv_tile(0, -1)
+    assert not bad, bad
+
+
+WGRAD_CFGS = list(range(8)) + list(range(16, 22)) + [32, 33, 34]
+
+
+@pytest.mark.parametrize("case", [(3, 64, 16, 64, 3, 1, 1, 1), (2, 128, 8, 256, 3, 2, 1, 1),
+                                  (2, 64, 32, 128, 1, 2, 0, 1), (3, 128, 7, 64, 3, 1, 1, 2),
+                                  (4, 64, 4, 192, 3, 1, 1, 1), (3, 64, 32, 64, 3, 1, 1, 1),
+                                  (5, 128, 8, 128, 3, 1, 1, 2), (64, 64, 32, 64, 3, 1, 1, 1)])
+def test_wgrad_every_config(C, case):
+    """Every wgrad configuration: split-K atomics, wide slab kernels (deterministic) and their
+    column / channel tails, accumulating into an existing gradient."""
+    N, Cin, H, Cout, k, s, p, G = case
+    torch.manual_seed(2)
+    x = bf(torch.randn(N, Cin, H, H, device="cuda"))
+    w = bf(torch.randn(Cout, Cin // G, k, k, device="cuda") * 0.1).requires_grad_(True)
+    ref = F.conv2d(x, w, stride=s, padding=p, groups=G)
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    x_n = nhwc(x).to(torch.bfloat16)
+    dy_n = nhwc(dy).to(torch.bfloat16)
+    prev = torch.randn(Cout, k, k, Cin // G, device="cuda")
+    want = w.grad.permute(0, 2, 3, 1) + prev
+    bad = []
+    try:
+        for cfg in WGRAD_CFGS:
+            C.set_conv_tile(1, cfg)
+            dw = C.conv_wgrad(x_n, dy_n, k, k, s, p, G, prev.clone())
+            e = rel_err(dw, want)
+            if e > 2e-2:
+                bad.append((cfg, e))
+        C.set_conv_tile(1, 16)
+        a = C.conv_wgrad(x_n, dy_n, k, k, s, p, G, None)
+        b = C.conv_wgrad(x_n, dy_n, k, k, s, p, G, None)
+    finally:
+        C.set_conv_tile(1, -1)
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("C_,act,res", [(64, 1, False), (64, 1, True), (24, 0, False), (116, 1, True), (96, 2, False)])
 def test_bn_fwd_bwd(C, C_, act, res):
     torch.manual_seed(1)

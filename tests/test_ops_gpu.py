@@ -63,9 +63,14 @@ def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True):
             bad.append((name, round(en, 4), round(es, 4)))
     assert not bad, f"grads worse than stock bf16 (name, native, stock): {bad[:10]}"
     if check_buffers:
+        bufs_s = dict(stock.named_buffers())
         for (n, br), (_, bn) in zip(ref.named_buffers(), native.named_buffers()):
             if br.dtype.is_floating_point:
-                assert rel(bn, br) < 0.03, n
+                # running stats: same criterion as the gradients, or absolutely negligible (a BN
+                # fed by a zero-mean producer has running_mean ~1e-9 in fp32, ~1e-6 in bf16)
+                en, es = rel(bn, br), rel(bufs_s[n], br)
+                small = (bn.float().cpu() - br.float()).abs().max().item() < 1e-4
+                assert en <= factor * es + slack or small, (n, en, es)
             else:
                 assert int(bn.item()) == int(br.item()), n
     return e_n, e_s
@@ -102,3 +107,23 @@ def test_resnet18_trains():
     assert step.graph is not None, f"graph capture failed: {step.graph_error!r}"
     assert all(torch.isfinite(torch.tensor(losses))), losses
     assert losses[-1] < losses[0], losses
+
+
+GPU_ZOO = ["LeNet", "VGG11", "PreActResNet18", "GoogLeNet", "densenet_cifar", "ResNeXt29_2x64d",
+           "MobileNet", "MobileNetV2", "DPN26", "SENet18", "EfficientNetB0", "RegNetX_200MF",
+           "RegNetY_400MF", "SimpleDLA", "DLA", "PNASNetA", "PNASNetB", "ShuffleNetG2",
+           "ShuffleNetV2_1", "ResNet50"]
+
+
+@pytest.mark.parametrize("name", GPU_ZOO)
+def test_zoo_matches_reference(name):
+    """Every model family through the native kernels: as close to fp32 as stock bf16."""
+    from pytorch_cifar_amd import models
+
+    def ctor():
+        m = models.MODEL_REGISTRY[name]()
+        if hasattr(m, "cfg") and isinstance(m.cfg, dict) and "dropout_rate" in m.cfg:
+            m.cfg = dict(m.cfg, dropout_rate=0.0)  # CPU and GPU dropout masks differ
+        return m
+
+    compare_model(ctor, batch=16)
