@@ -41,8 +41,34 @@ parser.add_argument('--max_steps', default=None, type=int, help='cap steps per e
 parser.add_argument('--log_every', default=20, type=int)
 parser.add_argument('--checkpoint_dir', default='./checkpoint')
 parser.add_argument('--cpu', action='store_true', help='force the CPU reference path')
+parser.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'],
+                    help='bf16: native MI355X kernels; fp32: stock PyTorch fp32 kernels on the GPU')
+parser.add_argument('--deterministic', action='store_true', help='bitwise-reproducible weight gradients')
+parser.add_argument('--debug_sync', action='store_true',
+                    help='sync + error-check after every native op (locates async GPU faults; disables graphs)')
+parser.add_argument('--profile', default=None, metavar='TRACE.json',
+                    help='torch.profiler Chrome trace of the first training steps')
+parser.add_argument('--no_nan_guard', action='store_true', help='do not stop on a non-finite loss')
 parser.add_argument('--t_max', default=200, type=int, help='cosine schedule length (reference: 200)')
 
+
+
+def _apply_runtime_flags(args, loaders):
+    """--deterministic / --debug_sync / --dtype fp32 (aux subsystems)."""
+    import pytorch_cifar_amd
+    from pytorch_cifar_amd.ops import functional as PF
+
+    on_gpu = torch.cuda.is_available() and not args.cpu
+    if args.deterministic and on_gpu:
+        pytorch_cifar_amd.set_deterministic(True)
+    if args.debug_sync:
+        pytorch_cifar_amd.set_debug_sync(True)
+        args.graph = 0
+    if args.dtype == 'fp32' and on_gpu:
+        PF.set_reference_mode(True)
+        args.graph = 0
+        for ld in loaders:
+            ld.fp32 = True
 
 def main(argv=None):
     args = parser.parse_args(argv)
@@ -56,6 +82,7 @@ def main(argv=None):
                                             args.test_batch_size, device, seed=args.seed,
                                             synthetic_size=args.synthetic_size,
                                             test_synthetic_size=(args.synthetic_size // 5 if args.synthetic_size else None))
+    _apply_runtime_flags(args, (trainloader, testloader))
 
     print('==> Building model..')
     model = models.build_model(args.model).to(device)
@@ -78,7 +105,11 @@ def main(argv=None):
 
     trainer = Trainer(net, optimizer, trainloader, testloader, DistContext(device=torch.device(device)),
                       graph=bool(args.graph) and device == 'cuda', log_every=args.log_every,
-                      progress=progress_bar, max_steps=args.max_steps)
+                      progress=progress_bar, max_steps=args.max_steps, nan_guard=not args.no_nan_guard)
+    if args.profile:
+        from pytorch_cifar_amd.utils.profiling import torch_profile
+        prof_cm = torch_profile(args.profile)
+        trainer.profiler = prof_cm.__enter__()
 
     for epoch in range(start_epoch, start_epoch + args.epochs):
         print('\nEpoch: %d' % epoch)
@@ -91,6 +122,9 @@ def main(argv=None):
             save_checkpoint(ckpt_path, net, acc, epoch, optimizer, scheduler)
             best_acc = acc
         scheduler.step()
+    if args.profile:
+        prof_cm.__exit__(None, None, None)
+        print('Profile trace written to %s' % args.profile)
     return best_acc
 
 

@@ -63,9 +63,35 @@ parser.add_argument('--bucket_mb', default=25.0, type=float)
 parser.add_argument('--log_every', default=20, type=int)
 parser.add_argument('--no_broadcast_buffers', action='store_true')
 parser.add_argument('--cpu', action='store_true', help='gloo/CPU ranks (tests)')
+parser.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'],
+                    help='bf16: native MI355X kernels; fp32: stock PyTorch fp32 kernels on the GPU')
+parser.add_argument('--deterministic', action='store_true', help='bitwise-reproducible weight gradients')
+parser.add_argument('--debug_sync', action='store_true',
+                    help='sync + error-check after every native op (locates async GPU faults; disables graphs)')
+parser.add_argument('--profile', default=None, metavar='TRACE.json',
+                    help='torch.profiler Chrome trace of the first training steps')
+parser.add_argument('--no_nan_guard', action='store_true', help='do not stop on a non-finite loss')
 
 best_acc = 0
 
+
+
+def _apply_runtime_flags(args, loaders):
+    """--deterministic / --debug_sync / --dtype fp32 (aux subsystems)."""
+    import pytorch_cifar_amd
+    from pytorch_cifar_amd.ops import functional as PF
+
+    on_gpu = torch.cuda.is_available() and not args.cpu
+    if args.deterministic and on_gpu:
+        pytorch_cifar_amd.set_deterministic(True)
+    if args.debug_sync:
+        pytorch_cifar_amd.set_debug_sync(True)
+        args.graph = 0
+    if args.dtype == 'fp32' and on_gpu:
+        PF.set_reference_mode(True)
+        args.graph = 0
+        for ld in loaders:
+            ld.fp32 = True
 
 def main(argv=None):
     args = parser.parse_args(argv)
@@ -112,6 +138,7 @@ def main_worker(ctx, args):
                                             world=ctx.world, rank=ctx.rank, crop_pad=0, flip=True,
                                             seed=args.seed, synthetic_size=args.synthetic_size,
                                             test_synthetic_size=(args.synthetic_size // 5 if args.synthetic_size else None))
+    _apply_runtime_flags(args, (trainloader, testloader))
 
     print('==> Building model..')
     model = models.build_model(args.model).to(device)
@@ -147,7 +174,12 @@ def main_worker(ctx, args):
         tqdm_progress = progress_bar
     trainer = Trainer(net, optimizer, trainloader, testloader, ctx, ddp=ddp,
                       graph=bool(args.graph) and device.type == 'cuda', log_every=args.log_every,
-                      progress=tqdm_progress, max_steps=args.max_steps)
+                      progress=tqdm_progress, max_steps=args.max_steps, nan_guard=not args.no_nan_guard)
+    prof_cm = None
+    if args.profile and ctx.rank == 0:
+        from pytorch_cifar_amd.utils.profiling import torch_profile
+        prof_cm = torch_profile(args.profile)
+        trainer.profiler = prof_cm.__enter__()
 
     logging.info("Start training...")
     for epoch in range(start_epoch, args.epochs):
@@ -166,6 +198,9 @@ def main_worker(ctx, args):
                 save_checkpoint(ckpt, net, acc, epoch, optimizer, scheduler)
             best_acc = acc
         scheduler.step()
+    if prof_cm is not None:
+        prof_cm.__exit__(None, None, None)
+        logging.info('Profile trace written to %s' % args.profile)
     ctx.barrier()
     ctx.shutdown()
     return best_acc

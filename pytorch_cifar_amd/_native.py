@@ -3,6 +3,12 @@
 GPU tensors always go through the native kernels: if the extension is missing on a machine with
 a HIP device, ops raise instead of silently falling back to stock PyTorch kernels. CPU tensors use
 the pure-PyTorch reference path (BASELINE config 1: LeNet on CPU).
+
+Debug mode (SURVEY §5 race/fault detection): with ``PCA_DEBUG_SYNC=1`` (or
+:func:`set_debug_sync`) every native entry point is followed by a device synchronisation and a
+``hipGetLastError`` check, so an asynchronous kernel fault or launch error is raised at the op that
+caused it (named in the message) instead of at some later sync point — the HIP analogue of
+``CUDA_LAUNCH_BLOCKING=1`` scoped to this library.
 """
 from __future__ import annotations
 
@@ -10,18 +16,57 @@ import os
 
 _lib = None
 _err: Exception | None = None
+_debug = os.environ.get("PCA_DEBUG_SYNC", "0") == "1"
+
+
+class _DebugProxy:
+    """Wraps the extension: sync + error check after every call (debug mode only)."""
+
+    def __init__(self, mod):
+        self._mod = mod
+        self.__file__ = getattr(mod, "__file__", None)
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn) or isinstance(fn, type) or name in ("last_error",):
+            return fn
+
+        def wrapped(*a, **k):
+            import torch
+
+            out = fn(*a, **k)
+            err = self._mod.last_error()
+            if err:
+                raise RuntimeError(f"pytorch_cifar_amd._C.{name}: launch failed: {err}")
+            if torch.cuda.is_available():
+                try:
+                    torch.cuda.synchronize()
+                except Exception as e:  # device fault surfaced by this op
+                    raise RuntimeError(f"pytorch_cifar_amd._C.{name}: device error: {e}") from e
+            return out
+
+        return wrapped
+
+
+def set_debug_sync(on: bool = True) -> None:
+    global _debug
+    _debug = bool(on)
+
+
+def _wrap(mod):
+    return _DebugProxy(mod) if _debug else mod
 
 
 def lib():
     """Return the ``pytorch_cifar_amd._C`` module, building it in-tree on first use if needed."""
     global _lib, _err
     if _lib is not None:
-        return _lib
+        return _wrap(_lib)
     try:
         from . import _C  # noqa: F401
 
         _lib = _C
-        return _lib
+        return _wrap(_lib)
     except ImportError as e:  # not built yet
         _err = e
     if os.environ.get("PCA_NO_AUTOBUILD", "0") != "1":
@@ -31,7 +76,7 @@ def lib():
         from . import _C  # noqa: F811
 
         _lib = _C
-        return _lib
+        return _wrap(_lib)
     raise RuntimeError(
         "pytorch_cifar_amd native extension is not built; run `python -m pytorch_cifar_amd._build`"
     ) from _err

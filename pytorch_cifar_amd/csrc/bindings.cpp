@@ -83,6 +83,8 @@ void direct_wgrad_launch(const bf16*, const bf16*, int, int, int, int, int, int,
                          int, int, int, int, float*, int, float*, hipStream_t);
 // comm.cpp
 void register_comm(py::module& m);
+void set_deterministic_conv(bool on);
+bool deterministic_conv();
 }  // namespace pca
 
 using at::Tensor;
@@ -596,6 +598,13 @@ Tensor direct_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int strid
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "pytorch_cifar_amd gfx950 kernels";
+  m.def("set_deterministic", &pca::set_deterministic_conv,
+        "weight gradients reduced through ordered slab rows (no fp32 atomics): bitwise-reproducible");
+  m.def("deterministic", &pca::deterministic_conv);
+  m.def("last_error", []() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? std::string() : std::string(hipGetErrorString(e));
+  }, "hipGetLastError() of this thread as a string ('' = no error); clears it");
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);

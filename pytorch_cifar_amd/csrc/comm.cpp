@@ -95,6 +95,22 @@ class RcclComm {
     RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()),
                              comm_, reinterpret_cast<hipStream_t>(stream)));
   }
+  // Asynchronous communicator error (a peer died, a network/xGMI fault, a timeout inside
+  // RCCL): '' when healthy. Polled by DistContext.health_check() at log points.
+  std::string async_error() {
+    if (!comm_) return "communicator destroyed";
+    ncclResult_t r = ncclSuccess;
+    const ncclResult_t q = ncclCommGetAsyncError(comm_, &r);
+    if (q != ncclSuccess) return std::string("ncclCommGetAsyncError failed: ") + ncclGetErrorString(q);
+    return r == ncclSuccess || r == ncclInProgress ? std::string() : std::string(ncclGetErrorString(r));
+  }
+  // Abort in-flight collectives (used on failure so the other ranks' waits return).
+  void abort() {
+    if (comm_) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
   void group_start() { RCCL_CHECK(ncclGroupStart()); }
   void group_end() { RCCL_CHECK(ncclGroupEnd()); }
   int world() const { return world_; }
@@ -125,6 +141,8 @@ void register_comm(py::module& m) {
       .def("group_start", &RcclComm::group_start)
       .def("group_end", &RcclComm::group_end)
       .def("destroy", &RcclComm::destroy)
+      .def("async_error", &RcclComm::async_error)
+      .def("abort", &RcclComm::abort)
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("rank", &RcclComm::rank);
 }

@@ -18,6 +18,7 @@
 #include "mfma_util.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace pca {
 
@@ -31,6 +32,7 @@ struct HaloGeom {
   int HR;                 // halo rows per stage = IMGS * (RS+2) * (W+2)
   int HI;                 // halo DMA instructions per stage = ceil(HR / 8)
   int chunk, splits, atomic;
+  int ablate;             // diagnostics (PCA_HALO_ABLATE): 1 = no DMA, 2 = no MFMA phase
   uint32_t x_bytes, dy_bytes;
   FastDiv fd_hw, fd_w;
 };
@@ -65,25 +67,39 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
   }
 }
 
-constexpr int kHaloMaxHI = 13;                 // W = 32: 3 x 34 = 102 halo rows
-constexpr int kHaloBytes = kHaloMaxHI * 1024;
+// Compile-time stage geometry for a square W x W image (W | 32): a stage is 32 output pixels =
+// RS rows of IMGS images; the halo is IMGS x (RS+2) x W2P rows (row pitch W2P = W+2 rounded up to
+// a multiple of 8 so that a kh*W2P row shift only flips bit 3 of the XOR swizzle key).
+template <int W>
+struct HaloShape {
+  static constexpr int RS = (32 / W) <= W ? 32 / W : W;
+  static constexpr int IMGS = (32 / W) <= W ? 1 : (32 / W) / W;
+  static constexpr int W2P = ((W + 2) + 7) / 8 * 8;
+  static constexpr int HR = IMGS * (RS + 2) * W2P;
+  static constexpr int HI = (HR + 7) / 8;        // halo DMA instructions per stage
+  static constexpr int HBYTES = HI * 1024;
+};
 
-template <int MB, int WM, int WN>
+template <int W, int MB, int WM, int WN>
 __global__ __launch_bounds__(WM * WN * 64) void wgrad_halo_kernel(const bf16* __restrict__ X,
                                                                   const bf16* __restrict__ DY,
                                                                   float* __restrict__ out,
                                                                   const HaloGeom g) {
+  using SH = HaloShape<W>;
   constexpr int NW = WM * WN;
   constexpr int KP = 32;
   constexpr int STAGES = 3;
-  constexpr int A_OFF = kHaloBytes;             // dY blocks follow the halo image
-  constexpr int STAGE = kHaloBytes + MB * KP * 128;
+  constexpr int A_OFF = SH::HBYTES;              // dY blocks follow the halo image
+  constexpr int J_OFF = A_OFF + MB * KP * 128;   // junk KiB for the padding DMA slots
+  constexpr int STAGE = J_OFF + 1024;
   constexpr int BM = MB * 64, BN = 9 * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int TMAX = kHaloMaxHI + 4 * MB;     // DMA instructions per stage (upper bound)
-  constexpr int SLOTS = (TMAX + NW - 1) / NW;   // per wave
+  constexpr int T = SH::HI + 4 * MB;             // real DMA instructions per stage
+  constexpr int SLOTS = (T + NW - 1) / NW;       // every wave issues exactly SLOTS per stage
+  constexpr int W2P = SH::W2P;
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+  static_assert(32 % W == 0, "image width");
   __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -95,89 +111,85 @@ __global__ __launch_bounds__(WM * WN * 64) void wgrad_halo_kernel(const bf16* __
   const int cib = blockIdx.y;                  // 64-channel input block
   const int p_begin = split * g.chunk;
   const int p_end = min(g.P, p_begin + g.chunk);
-  const int W2 = g.W + 2;
 
   const __amdgpu_buffer_rsrc_t rsX = make_rsrc(X, g.x_bytes);
   const __amdgpu_buffer_rsrc_t rsD = make_rsrc(DY, g.dy_bytes);
 
-  // ---- per-lane DMA slots (fixed for the kernel): kind 0 = halo row group, 1 = dY rows ----
-  const int T = g.HI + 4 * MB;
-  int s_kind[SLOTS], s_a[SLOTS], s_b[SLOTS], s_lds[SLOTS];
+  // ---- per-lane DMA slots (fixed for the kernel) ----
+  // halo slot: packed (row ok, image slot, halo row j, halo col c) + swizzled chunk byte offset
+  // dY slot:   stage pixel r + (swizzled chunk + channel) byte offset
+  int s_a[SLOTS], s_b[SLOTS];
 #pragma unroll
   for (int j = 0; j < SLOTS; ++j) {
     const int t = wid + NW * j;
     const int row8 = lane >> 3;
-    s_kind[j] = 2;
-    s_a[j] = 0;
-    s_b[j] = 0;
-    s_lds[j] = 0;
-    if (t < g.HI) {
-      const int hr = 8 * t + row8;               // halo row
-      const int per_img = (g.RS + 2) * W2;
-      const int img = hr / per_img;
-      const int rem = hr - img * per_img;
-      const int jr = rem / W2;
-      const int c = rem - jr * W2;
-      s_kind[j] = 0;                             // (wave-uniform: one DMA per slot)
-      // packed (row-valid, image slot, halo row, halo col); halo (jr, c) = input
-      // (h0 + jr - 1, c - 1); rows past the halo (the last instruction's tail) load zeros
-      s_a[j] = ((hr < g.HR) << 24) | (img << 16) | (jr << 8) | c;
-      s_b[j] = (((lane & 7) ^ tr_swz<128>(hr)) << 4);
-      s_lds[j] = t * 1024;
+    if (t < SH::HI) {
+      const int hr = 8 * t + row8;
+      const int img = hr / ((SH::RS + 2) * W2P);
+      const int rem = hr - img * ((SH::RS + 2) * W2P);
+      const int jr = rem / W2P, c = rem - jr * W2P;
+      const bool ok = hr < SH::HR && c < W + 2;
+      s_a[j] = (ok << 24) | (img << 16) | (jr << 8) | c;
+      s_b[j] = (((lane & 7) ^ tr_swz<128>(hr)) << 4) + (grp * g.cin_g + cib * 64) * 2;
     } else if (t < T) {
-      const int q = t - g.HI;                    // dY instruction: block q>>2, row group q&3
-      const int r = 8 * (q & 3) + row8;          // stage pixel
-      s_kind[j] = 1;
+      const int q = t - SH::HI;
+      const int r = 8 * (q & 3) + row8;
       s_a[j] = r;
       s_b[j] = (((lane & 7) ^ tr_swz<128>(r)) << 4) + (grp * g.cout_g + m0 + 64 * (q >> 2)) * 2;
-      s_lds[j] = A_OFF + (q >> 2) * KP * 128 + (q & 3) * 1024;
+    } else {
+      s_a[j] = 0;
+      s_b[j] = 0;
     }
   }
-  // loads this wave issues per stage (wave-uniform)
-  const int my_loads = (T - wid + NW - 1) / NW;
 
   auto issue = [&](int pbase, int buf) {
+    if (g.ablate & 1) return;
     char* S = smem + buf * STAGE;
     const bool live = pbase < p_end;
-    // stage geometry (uniform): first image and first row of the stage
-    const uint32_t pp = live ? (uint32_t)pbase : 0u;
-    const int n0 = (int)fdiv(pp, g.fd_hw);
-    const int h0 = (int)fdiv(pp - (uint32_t)n0 * (uint32_t)(g.H * g.W), g.fd_w);
+    // first image / row of the stage (W power of two: shifts)
+    const int n0 = pbase / (W * W);
+    const int h0 = (pbase / W) % W;
 #pragma unroll
     for (int j = 0; j < SLOTS; ++j) {
-      const int kind = s_kind[j];
-      if (kind == 2) continue;
+      const int t = wid + NW * j;                // wave-uniform slot kind
       uint32_t off = kOOB;
-      if (kind == 0) {
+      if (t < SH::HI) {
         const int n = n0 + ((s_a[j] >> 16) & 0xff);
         const int ih = h0 + ((s_a[j] >> 8) & 0xff) - 1;
         const int iw = (s_a[j] & 0xff) - 1;
-        const bool ok = live && (s_a[j] >> 24) && n < g.N && (uint32_t)ih < (uint32_t)g.H &&
-                        (uint32_t)iw < (uint32_t)g.W;
-        if (ok)
-          off = (uint32_t)((((n * g.H + ih) * g.W + iw) * g.Cx + grp * g.cin_g + cib * 64) * 2 + s_b[j]);
-        dma16(rsX, S + s_lds[j], off);
-      } else {
+        const bool ok = live && (s_a[j] >> 24) && n < g.N && (uint32_t)ih < (uint32_t)W &&
+                        (uint32_t)iw < (uint32_t)W;
+        if (ok) off = (uint32_t)((((n * W + ih) * W + iw) * g.Cx) * 2 + s_b[j]);
+        dma16(rsX, S + t * 1024, off);
+      } else if (t < T) {
+        const int q = t - SH::HI;
         const int p = pbase + s_a[j];
         if (live && p < p_end) off = (uint32_t)(p * g.Cy * 2 + s_b[j]);
-        dma16(rsD, S + s_lds[j], off);
+        dma16(rsD, S + A_OFF + (q >> 2) * KP * 128 + (q & 3) * 1024, off);
+      } else {
+        dma16(rsD, S + J_OFF, kOOB);              // keeps vmcnt per wave uniform
       }
     }
   };
 
-  // per-lane halo rows of the pixels this lane's B fragments cover (tap (0,0))
-  int prow0, prow1;
+  // ---- per-lane B-fragment addressing: halo rows of this lane's two pixel rows ----
+  // B frag (tap kh,kw; columns c0..c0+15 of the 64-channel block) for the lane lives at
+  //   row R = prow + kh*W2P + kw,  byte = R*128 + ((c0/8 ^ swz(R)) << 4) + L
+  // and swz(R) = swz(prow + kw) ^ (kh*W2P/8 odd ? 4 : 0) because W2P % 8 == 0.
+  int rbase[2], swk[2][3];
   {
-    const int q = (lane & 15) >> 2;
-    const int r0 = 8 * (lane >> 4) + q, r1 = r0 + 4;
-    const int rsw = g.RS * g.W;
-    auto hrow = [&](int r) {
-      const int img = r / rsw, rr = r - img * rsw;
-      const int j = rr / g.W, ow = rr - j * g.W;
-      return img * (g.RS + 2) * W2 + j * W2 + ow;
-    };
-    prow0 = hrow(r0);
-    prow1 = hrow(r1);
+    const int q = (lane & 15) >> 2, pq = lane & 3;
+    const int L = ((pq >> 1) << 4) + ((pq & 1) << 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 8 * (lane >> 4) + q + 4 * h;
+      const int img = r / (SH::RS * W), rr = r - img * (SH::RS * W);
+      const int jj = rr / W, ow = rr - jj * W;
+      const int prow = img * (SH::RS + 2) * W2P + jj * W2P + ow;
+      rbase[h] = prow * 128 + L;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) swk[h][kw] = tr_swz<128>(prow + kw) << 4;
+    }
   }
 
   f32x4 acc[TM][TN];
@@ -186,13 +198,16 @@ __global__ __launch_bounds__(WM * WN * 64) void wgrad_halo_kernel(const bf16* __
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
   const int KT = p_end > p_begin ? cdiv(p_end - p_begin, KP) : 0;
   issue(p_begin, 0);
   issue(p_begin + KP, 1);
   for (int kt = 0; kt < KT; ++kt) {
-    wait_vmcnt_rt<8>(my_loads);     // stage kt landed (stage kt+1 may still be in flight)
+    wait_vmcnt<SLOTS>();            // stage kt landed (stage kt+1 may still be in flight)
     raw_barrier();
     issue(p_begin + (kt + 2) * KP, (kt + 2) % STAGES);
+    if (g.ablate & 2) continue;
     const char* S = smem + (kt % STAGES) * STAGE;
     bf16x8 af[TM];
 #pragma unroll
@@ -204,9 +219,15 @@ __global__ __launch_bounds__(WM * WN * 64) void wgrad_halo_kernel(const bf16* __
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = wn * WTN + ni * 16;
-      const int tap = n >> 6;
-      const int toff = (tap / 3) * W2 + (tap % 3);
-      const bf16x8 bfv = tr_frag_rows(S, prow0 + toff, prow1 + toff, n & 63, lane);
+      const int tap = n >> 6, kh = tap / 3, kw = tap % 3;
+      const int c0 = n & 63;
+      const int cx = ((c0 >> 3) ^ (((kh * W2P / 8) & 1) ? 4 : 0)) << 4;
+      const int rsh = (kh * W2P + kw) * 128;
+      const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_i16x4*)(S + rbase[0] + rsh + (cx ^ swk[0][kw])));
+      const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_i16x4*)(S + rbase[1] + rsh + (cx ^ swk[1][kw])));
+      const bf16x8 bfv = __builtin_bit_cast(bf16x8, (i16x8)__builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi)
         acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfv, acc[mi][ni], 0, 0, 0);
@@ -283,12 +304,12 @@ static int halo_cus() {
   X(1, 2, 2, 4)          \
   X(2, 1, 2, 4)
 
-template <int MB, int WM, int WN>
+template <int W, int MB, int WM, int WN>
 static int halo_occupancy() {
   static int occ = 0;
   if (occ == 0) {
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)wgrad_halo_kernel<MB, WM, WN>,
-                                                 WM * WN * 64, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, (const void*)wgrad_halo_kernel<W, MB, WM, WN>, WM * WN * 64, 0);
     occ = std::max(1, occ);
   }
   return occ;
@@ -297,28 +318,45 @@ static int halo_occupancy() {
 static int g_halo_override = -1;
 void set_halo_cfg(int cfg) { g_halo_override = cfg; }
 
+// Deterministic mode: every weight gradient is reduced through slab rows in a fixed order
+// (no fp32 atomics), so repeated runs are bitwise identical.
+static bool g_deterministic = false;
+void set_deterministic_conv(bool on) { g_deterministic = on; }
+bool deterministic_conv() { return g_deterministic; }
+
+// dW[i] += sum_s slab[s][i] over `splits` rows of n floats (two-level, fixed order); the
+// workspace must hold splits*n + cdiv(splits,16)*n floats.
+void slab_reduce_launch(float* ws, float* dw, int splits, int64_t n, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  const int per = 16, nparts = cdiv(splits, per);
+  float* part = ws + (int64_t)splits * n;
+  const unsigned gx = (unsigned)cdiv64(n4, 256);
+  hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, nparts), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(part), splits,
+                     per, n4);
+  hipLaunchKernelGGL(slab_final_kernel, dim3(gx), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(part), reinterpret_cast<float4*>(dw), nparts, n4);
+}
+
+int64_t slab_ws_floats(int splits, int64_t n) { return (int64_t)splits * n + (int64_t)cdiv(splits, 16) * n; }
+
 // Is the halo kernel applicable? 3x3 s1 p1, 64-channel blocks, whole rows (or images) per stage.
 static bool halo_geom(HaloGeom& g, int N, int H, int W, int Cin, int Cout, int groups) {
   g.N = N; g.H = H; g.W = W; g.Cx = Cin; g.Cy = Cout;
   g.groups = groups; g.cin_g = Cin / groups; g.cout_g = Cout / groups;
   g.P = N * H * W;
   g.Ktot = 9 * g.cin_g;
-  if (g.cin_g % 64 || g.cout_g % 64 || 32 % W) return false;
-  const int rows = 32 / W;                    // image rows per stage
-  if (rows <= H) {
-    if (H % rows) return false;
-    g.RS = rows; g.IMGS = 1;
-  } else {
-    if (rows % H) return false;
-    g.RS = H; g.IMGS = rows / H;
-  }
-  g.HR = g.IMGS * (g.RS + 2) * (W + 2);
-  g.HI = cdiv(g.HR, 8);
-  if (g.HI > kHaloMaxHI) return false;
+  if (g.cin_g % 64 || g.cout_g % 64) return false;
+  if (H != W || (W != 4 && W != 8 && W != 16 && W != 32)) return false;
   g.x_bytes = (uint32_t)((size_t)N * H * W * Cin * 2);
   g.dy_bytes = (uint32_t)((size_t)N * H * W * Cout * 2);
   g.fd_hw = make_fastdiv(H * W);
   g.fd_w = make_fastdiv(W);
+  static const int abl = [] {
+    const char* e = getenv("PCA_HALO_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  g.ablate = abl;
   return true;
 }
 
@@ -327,30 +365,57 @@ static int halo_select(const HaloGeom& g) {
   return g.cout_g <= 64 ? 0 : 1;
 }
 
-template <int MB, int WM, int WN>
+template <int W, int MB, int WM, int WN>
 static int64_t halo_plan(HaloGeom& g) {
   const int tiles = cdiv(g.cout_g, 64 * MB) * (g.cin_g / 64) * g.groups;
-  const int slots = halo_occupancy<MB, WM, WN>() * halo_cus();
+  const int slots = halo_occupancy<W, MB, WM, WN>() * halo_cus();
   int splits = std::max(1, slots / tiles);
   splits = std::min(splits, std::max(1, cdiv(g.P, 256)));
   int chunk = cdiv(cdiv(g.P, splits), 32) * 32;
   splits = cdiv(g.P, chunk);
   g.chunk = chunk;
   g.splits = splits;
-  g.atomic = splits <= 4 ? 1 : 0;
+  g.atomic = (!g_deterministic && splits <= 4) ? 1 : 0;
   if (g.atomic) return 0;
-  const int64_t n = (int64_t)g.groups * g.cout_g * g.Ktot;
-  const int nparts = cdiv(splits, 16);
-  return (int64_t)splits * n + (int64_t)nparts * n;   // slab rows + partial sums
+  return slab_ws_floats(splits, (int64_t)g.groups * g.cout_g * g.Ktot);
 }
 
-static int64_t halo_plan_any(HaloGeom& g) {
+template <int W, int MB, int WM, int WN>
+static void launch_halo(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom g,
+                        hipStream_t st) {
+  halo_plan<W, MB, WM, WN>(g);
+  dim3 grid(cdiv(g.cout_g, 64 * MB), g.cin_g / 64, g.splits * g.groups);
+  hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN>), grid, dim3(WM * WN * 64), 0, st, x, dy,
+                     g.atomic ? dw : ws, g);
+  if (!g.atomic) slab_reduce_launch(ws, dw, g.splits, (int64_t)g.groups * g.cout_g * g.Ktot, st);
+}
+
+// One dispatcher for planning (ws == nullptr && plan_only) and launching.
+template <int W>
+static int64_t halo_dispatch_w(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom& g,
+                               hipStream_t st, bool plan_only) {
   switch (halo_select(g)) {
-#define PCA_CASE(C, MB, WM, WN) \
-    case C: return halo_plan<MB, WM, WN>(g);
+#define PCA_CASE(C, MB, WM, WN)                                        \
+    case C:                                                            \
+      if (plan_only) return halo_plan<W, MB, WM, WN>(g);               \
+      launch_halo<W, MB, WM, WN>(x, dy, dw, ws, g, st);                \
+      return 0;
     PCA_HALO_CFGS(PCA_CASE)
 #undef PCA_CASE
-    default: return halo_plan<1, 1, 4>(g);
+    default:
+      if (plan_only) return halo_plan<W, 1, 1, 4>(g);
+      launch_halo<W, 1, 1, 4>(x, dy, dw, ws, g, st);
+      return 0;
+  }
+}
+
+static int64_t halo_dispatch(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom& g,
+                             hipStream_t st, bool plan_only) {
+  switch (g.W) {
+    case 4: return halo_dispatch_w<4>(x, dy, dw, ws, g, st, plan_only);
+    case 8: return halo_dispatch_w<8>(x, dy, dw, ws, g, st, plan_only);
+    case 16: return halo_dispatch_w<16>(x, dy, dw, ws, g, st, plan_only);
+    default: return halo_dispatch_w<32>(x, dy, dw, ws, g, st, plan_only);
   }
 }
 
@@ -360,42 +425,14 @@ int64_t wgrad_halo_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int
   if (KH != 3 || KW != 3 || stride != 1 || pad != 1) return -1;
   HaloGeom g;
   if (!halo_geom(g, N, H, W, Cin, Cout, groups)) return -1;
-  return halo_plan_any(g);
-}
-
-template <int MB, int WM, int WN>
-static void launch_halo(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom g,
-                        hipStream_t st) {
-  halo_plan<MB, WM, WN>(g);
-  dim3 grid(cdiv(g.cout_g, 64 * MB), g.cin_g / 64, g.splits * g.groups);
-  hipLaunchKernelGGL((wgrad_halo_kernel<MB, WM, WN>), grid, dim3(WM * WN * 64), 0, st, x, dy,
-                     g.atomic ? dw : ws, g);
-  if (!g.atomic) {
-    const int64_t n = (int64_t)g.groups * g.cout_g * g.Ktot;
-    const int64_t n4 = n / 4;
-    const int per = 16, nparts = cdiv(g.splits, per);
-    float* part = ws + (int64_t)g.splits * n;
-    const unsigned gx = (unsigned)cdiv64(n4, 256);
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, nparts), dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(part),
-                       g.splits, per, n4);
-    hipLaunchKernelGGL(slab_final_kernel, dim3(gx), dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(part), reinterpret_cast<float4*>(dw), nparts,
-                       n4);
-  }
+  return halo_dispatch(nullptr, nullptr, nullptr, nullptr, g, nullptr, true);
 }
 
 void wgrad_halo_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
                        int Cin, int Cout, int groups, hipStream_t st) {
   HaloGeom g;
   halo_geom(g, N, H, W, Cin, Cout, groups);
-  switch (halo_select(g)) {
-#define PCA_CASE(C, MB, WM, WN) \
-    case C: launch_halo<MB, WM, WN>(x, dy, dw, ws, g, st); break;
-    PCA_HALO_CFGS(PCA_CASE)
-#undef PCA_CASE
-    default: launch_halo<1, 1, 4>(x, dy, dw, ws, g, st); break;
-  }
+  halo_dispatch(x, dy, dw, ws, g, st, false);
 }
 
 }  // namespace pca

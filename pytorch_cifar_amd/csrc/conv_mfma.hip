@@ -517,8 +517,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const bf16* __restrict_
       for (int j = 0; j < 4; ++j) {
         const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + j;
         const int n = n0 + wn * WTN + ni * 16 + (lane & 15);
-        if (m < g.cout_g && n < g.Ktot)
-          atomicAdd(DW + ((size_t)grp * g.cout_g + m) * g.Ktot + n, acc[mi][ni][j]);
+        if (m < g.cout_g && n < g.Ktot) {
+          const size_t idx = ((size_t)grp * g.cout_g + m) * g.Ktot + n;
+          if (g.atomic) atomicAdd(DW + idx, acc[mi][ni][j]);
+          else DW[(size_t)split * g.groups * g.cout_g * g.Ktot + idx] = acc[mi][ni][j];
+        }
       }
 }
 
@@ -878,9 +881,14 @@ void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, i
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ST>
-static void launch_wgrad(const bf16* x, const bf16* dy, float* dw, WgradGeom g, hipStream_t st,
-                         int target_blocks) {
+void set_deterministic_conv(bool on);
+bool deterministic_conv();
+void slab_reduce_launch(float* ws, float* dw, int splits, int64_t n, hipStream_t st);
+int64_t slab_ws_floats(int splits, int64_t n);
+
+// split-K plan of the generic wgrad kernel; returns the slab size (0 = atomics)
+template <int BM, int BN>
+static int64_t splitk_plan(WgradGeom& g, int target_blocks) {
   const int tiles = cdiv(g.cout_g, BM) * cdiv(g.Ktot, BN) * g.groups;
   int splits = cdiv(target_blocks, tiles);
   const int min_chunk = 512;
@@ -890,8 +898,18 @@ static void launch_wgrad(const bf16* x, const bf16* dy, float* dw, WgradGeom g, 
   splits = cdiv(g.P, chunk);
   g.chunk = chunk;
   g.splits = splits;
-  dim3 grid(cdiv(g.cout_g, BM), cdiv(g.Ktot, BN), splits * g.groups);
-  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, ST>), grid, dim3(256), 0, st, x, dy, dw, g);
+  g.atomic = deterministic_conv() ? 0 : 1;
+  return g.atomic ? 0 : slab_ws_floats(splits, (int64_t)g.groups * g.cout_g * g.Ktot);
+}
+
+template <int BM, int BN, int WM, int WN, int ST>
+static void launch_wgrad(const bf16* x, const bf16* dy, float* dw, float* ws, WgradGeom g,
+                         hipStream_t st, int target_blocks) {
+  splitk_plan<BM, BN>(g, target_blocks);
+  dim3 grid(cdiv(g.cout_g, BM), cdiv(g.Ktot, BN), g.splits * g.groups);
+  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, ST>), grid, dim3(256), 0, st, x, dy,
+                     g.atomic ? dw : ws, g);
+  if (!g.atomic) slab_reduce_launch(ws, dw, g.splits, (int64_t)g.groups * g.cout_g * g.Ktot, st);
 }
 
 // wide-kernel configurations: X(cfg, MB, NB, WM, WN)  (tile = 64*MB cout x 64*NB columns)
@@ -957,8 +975,8 @@ static int64_t wide_plan(WgradGeom& g) {
   g.chunk = chunk;
   g.splits = splits;
   // few partials per output: atomics; many: slab rows + one ordered reduce
-  g.atomic = splits <= 8 ? 1 : 0;
-  return g.atomic ? 0 : (int64_t)splits * g.groups * g.cout_g * g.Ktot;
+  g.atomic = (!deterministic_conv() && splits <= 8) ? 1 : 0;
+  return g.atomic ? 0 : slab_ws_floats(splits, (int64_t)g.groups * g.cout_g * g.Ktot);
 }
 
 template <int MB, int NB, int WM, int WN>
@@ -968,12 +986,8 @@ static void launch_wide(const bf16* x, const bf16* dy, float* dw, float* ws, Wgr
   dim3 grid(cdiv(g.cout_g, 64 * MB), cdiv(g.Ktot, 64 * NB), g.splits * g.groups);
   hipLaunchKernelGGL((conv_wgrad_wide_kernel<MB, NB, WM, WN>), grid, dim3(WM * WN * 64), 0, st, x,
                      dy, g.atomic ? dw : ws, g);
-  if (!g.atomic) {
-    const int64_t n4 = (int64_t)g.groups * g.cout_g * g.Ktot / 4;
-    (void)slab;
-    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)cdiv64(n4, 256)), dim3(256), 0, st,
-                       ws, dw, g.splits, n4);
-  }
+  if (!g.atomic) slab_reduce_launch(ws, dw, g.splits, (int64_t)g.groups * g.cout_g * g.Ktot, st);
+  (void)slab;
 }
 
 // halo-staged 3x3/s1 wgrad (conv_halo.hip); selected by default where it applies, or forced
@@ -995,12 +1009,18 @@ int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int
     if (h >= 0) return h;
   }
   WgradGeom g = wgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  const int target = 1024;
   switch (wgrad_select(g)) {
+    case 4: return splitk_plan<128, 128>(g, 2048);
+    case 5: return splitk_plan<128, 128>(g, 512);
+    case 0: case 3: return splitk_plan<128, 128>(g, target);
+    case 1: case 6: return splitk_plan<64, 128>(g, target);
+    case 2: case 7: return splitk_plan<32, 128>(g, target);
 #define PCA_CASE(C, MB, NB, WM, WN) \
     case C: return wide_plan<MB, NB, WM, WN>(g);
     PCA_WIDE_CFGS(PCA_CASE)
 #undef PCA_CASE
-    default: return 0;
+    default: return splitk_plan<128, 128>(g, target);
   }
 }
 
@@ -1017,19 +1037,19 @@ void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int 
   WgradGeom g = wgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   const int target = 1024;
   switch (wgrad_select(g)) {
-    case 0: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, g, st, target); break;
-    case 1: launch_wgrad<64, 128, 2, 2, 3>(x, dy, dw, g, st, target); break;
-    case 2: launch_wgrad<32, 128, 1, 4, 3>(x, dy, dw, g, st, target); break;
-    case 3: launch_wgrad<128, 128, 2, 2, 2>(x, dy, dw, g, st, target); break;
-    case 4: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, g, st, 2048); break;
-    case 5: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, g, st, 512); break;
-    case 6: launch_wgrad<64, 128, 2, 2, 2>(x, dy, dw, g, st, target); break;
-    case 7: launch_wgrad<32, 128, 1, 4, 2>(x, dy, dw, g, st, target); break;
+    case 0: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, ws, g, st, target); break;
+    case 1: launch_wgrad<64, 128, 2, 2, 3>(x, dy, dw, ws, g, st, target); break;
+    case 2: launch_wgrad<32, 128, 1, 4, 3>(x, dy, dw, ws, g, st, target); break;
+    case 3: launch_wgrad<128, 128, 2, 2, 2>(x, dy, dw, ws, g, st, target); break;
+    case 4: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, ws, g, st, 2048); break;
+    case 5: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, ws, g, st, 512); break;
+    case 6: launch_wgrad<64, 128, 2, 2, 2>(x, dy, dw, ws, g, st, target); break;
+    case 7: launch_wgrad<32, 128, 1, 4, 2>(x, dy, dw, ws, g, st, target); break;
 #define PCA_CASE(C, MB, NB, WM, WN) \
     case C: launch_wide<MB, NB, WM, WN>(x, dy, dw, ws, g, st); break;
     PCA_WIDE_CFGS(PCA_CASE)
 #undef PCA_CASE
-    default: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, g, st, target); break;
+    default: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, ws, g, st, target); break;
   }
 }
 

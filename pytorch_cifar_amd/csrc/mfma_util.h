@@ -32,9 +32,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
 
-// one 16-byte-per-lane LDS-DMA (1 KiB per wave instruction at lds_base + 16*lane)
+// one 16-byte-per-lane LDS-DMA (1 KiB per wave instruction at lds_base + 16*lane).
+// Issued from inline asm (M0 saved/set/restored inside the statement, cdna_hip_programming.md
+// §5.7) so the compiler does not see an LDS write in flight: with the builtin, hipcc (ROCm 7.2)
+// emits `s_waitcnt vmcnt(0)` before every ds_read_b64_tr_b16 that follows a DMA issue, which
+// drained the whole prefetch pipeline each K-step of the transposed-read (wgrad) kernels.
+// Completion is ordered by the kernels' own counted vmcnt waits + barriers.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_base, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_base, 16, (int)voff, 0, 0, 0);
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_char*)lds_base);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(voff), "s"(rs)
+      : "memory");
 }
 
 template <int N>

@@ -74,6 +74,7 @@ class DeviceLoader:
         self.train = train
         self.crop_pad = crop_pad if train else 0
         self.flip = flip if train else False
+        self.fp32 = False
         self.mean, self.std = tuple(mean), tuple(std)
         self.drop_last = drop_last
         self.sampler = ShardSampler(len(labels), world, rank, shuffle, seed, drop_last=False)
@@ -117,7 +118,10 @@ class DeviceLoader:
         targets = self.labels.index_select(0, idx)
         if self.device.type == "cuda":
             out = _native.lib().augment(self.images, idx, rnd, self.crop_pad, list(self.mean), list(self.std))
-            return padded_input(out, 3), targets
+            x = padded_input(out, 3)
+            if self.fp32:   # --dtype fp32: stock fp32 kernels consume an fp32 channels_last batch
+                x = x.float()
+            return x, targets
         return self._cpu_batch(idx, rnd), targets
 
     def _cpu_batch(self, idx, rnd):

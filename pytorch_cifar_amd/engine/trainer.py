@@ -18,6 +18,11 @@ import time
 import torch
 
 from ..ops.functional import cross_entropy
+from ..utils.profiling import trace_range
+
+
+class NonFiniteLossError(FloatingPointError):
+    """Raised by the trainer's loss guard (SURVEY §5 failure detection: NaN/inf loss guard)."""
 
 
 class TrainStep:
@@ -37,14 +42,18 @@ class TrainStep:
 
     # one eager step on a given index batch
     def _body(self, idx):
-        x, y = self.loader.make_batch(idx)
+        with trace_range("data"):
+            x, y = self.loader.make_batch(idx)
         self.opt.zero_grad()
-        out = self.net(x)
-        loss = cross_entropy(out, y, self.metrics)
-        loss.backward()
-        if self.ddp is not None:
-            self.ddp.finish()
-        self.opt.step()
+        with trace_range("forward"):
+            out = self.net(x)
+            loss = cross_entropy(out, y, self.metrics)
+        with trace_range("backward"):
+            loss.backward()
+            if self.ddp is not None:
+                self.ddp.finish()
+        with trace_range("optimizer"):
+            self.opt.step()
         return loss
 
     def _capture(self):
@@ -173,7 +182,8 @@ class Trainer:
     """
 
     def __init__(self, net, optimizer, train_loader, test_loader, ctx, ddp=None, graph=False,
-                 log_every=20, progress=None, is_main=True, max_steps=None):
+                 log_every=20, progress=None, is_main=True, max_steps=None, nan_guard=True,
+                 profiler=None):
         self.net = net
         self.opt = optimizer
         self.train_loader = train_loader
@@ -188,6 +198,15 @@ class Trainer:
         self.step = TrainStep(net, optimizer, train_loader, train_loader.batch_size, ddp=ddp,
                               graph=graph)
         self.images_per_sec = None
+        self.nan_guard = nan_guard
+        self.profiler = profiler   # torch.profiler session stepped once per train step
+
+    def _check_finite(self, loss_sum, b, epoch):
+        # the metrics buffer is read at every log point anyway: the guard costs no extra sync
+        if self.nan_guard and not (loss_sum == loss_sum and abs(loss_sum) != float("inf")):
+            raise NonFiniteLossError(
+                f"non-finite training loss at epoch {epoch}, step {b} (rank {self.ctx.rank}); "
+                "lower the learning rate or resume from the last checkpoint")
 
     def _reduce(self, m):
         t = torch.tensor(m, dtype=torch.float64, device=self.device if self.device.type == "cuda" else "cpu")
@@ -210,16 +229,24 @@ class Trainer:
                 break
             if loader.drop_last and idx.numel() < loader.batch_size:
                 break
-            self.step(idx)
+            with trace_range("train_step"):
+                self.step(idx)
+            if self.profiler is not None:
+                self.profiler.step()
             imgs += idx.numel()
-            if self.progress is not None and (b % self.log_every == 0 or b == n - 1):
+            if b % self.log_every == 0 or b == n - 1:
                 loss_sum, correct, total = metrics.tolist()
-                self.progress(b, n, "Loss: %.3f | Acc: %.3f%% (%d/%d)"
-                              % (loss_sum / (b + 1), 100.0 * correct / max(total, 1), correct, total))
+                self._check_finite(loss_sum, b, epoch)
+                if hasattr(self.ctx, "health_check"):
+                    self.ctx.health_check()
+                if self.progress is not None:
+                    self.progress(b, n, "Loss: %.3f | Acc: %.3f%% (%d/%d)"
+                                  % (loss_sum / (b + 1), 100.0 * correct / max(total, 1), correct, total))
         if self.device.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         loss_sum, correct, total = metrics.tolist()
+        self._check_finite(loss_sum, n, epoch)
         steps = max(1, min(n, b + 1) if n else 1)
         self.images_per_sec = imgs * self.ctx.world / dt if dt > 0 else None
         return loss_sum / steps, 100.0 * correct / max(total, 1), int(correct), int(total)
@@ -235,9 +262,10 @@ class Trainer:
         for b, idx in enumerate(loader.batch_indices()):
             if b >= n:
                 break
-            x, y = loader.make_batch(idx)
-            out = self.net(x)
-            cross_entropy(out, y, metrics)
+            with trace_range("eval_step"):
+                x, y = loader.make_batch(idx)
+                out = self.net(x)
+                cross_entropy(out, y, metrics)
             if self.progress is not None and (b % self.log_every == 0 or b == n - 1):
                 loss_sum, correct, total = metrics.tolist()
                 self.progress(b, n, "Loss: %.3f | Acc: %.3f%% (%d/%d)"

@@ -30,6 +30,12 @@ def _C():
 _FORCE_REFERENCE = False
 
 
+def set_reference_mode(on: bool) -> None:
+    """Process-wide: GPU tensors take the stock-PyTorch path too (``--dtype fp32`` runs)."""
+    global _FORCE_REFERENCE
+    _FORCE_REFERENCE = bool(on)
+
+
 def _ref(x: torch.Tensor) -> bool:
     """True when ``x`` takes the pure-PyTorch reference path (CPU, or reference mode forced)."""
     return _FORCE_REFERENCE or not x.is_cuda

@@ -46,6 +46,20 @@ class DistContext:
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t
 
+    def health_check(self):
+        """Raise if the native RCCL communicator reports an asynchronous error (failure
+        detection); the communicator is aborted first so peers blocked in a
+        collective are released instead of hanging until the process-group timeout."""
+        if self.comm is None:
+            return
+        err = self.comm.async_error()
+        if err:
+            try:
+                self.comm.abort()
+            finally:
+                self.comm = None
+            raise RuntimeError(f"RCCL communicator error on rank {self.rank}: {err}")
+
     def shutdown(self):
         if self.comm is not None:
             try:

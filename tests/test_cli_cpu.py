@@ -109,3 +109,56 @@ def test_main_dist_torchrun_two_ranks_cpu(tmp_path):
     log = open(tmp_path / "o" / "train.log").read()
     assert "Eval Loss" in log or "Eval Loss" in out
     assert os.path.exists(tmp_path / "o" / "ckpt.pth")
+
+
+def test_profiling_utils(tmp_path):
+    from pytorch_cifar_amd.utils.profiling import StepTimer, range_pop, range_push, torch_profile, trace_range
+
+    range_push("x")   # ROCTX ranges are safe with or without libroctx64
+    range_pop()
+    with trace_range("y"):
+        pass
+    t = StepTimer("cpu")
+    for _ in range(3):
+        t.start()
+        torch.ones(10).sum()
+        t.stop()
+    assert t.summary()["steps"] == 3
+    path = str(tmp_path / "trace.json")
+    with torch_profile(path, active=2, warmup=1) as prof:
+        for _ in range(4):
+            torch.randn(8, 8) @ torch.randn(8, 8)
+            prof.step()
+    assert os.path.getsize(path) > 0
+
+
+def test_nan_guard_stops_training():
+    from pytorch_cifar_amd.data.loader import DeviceLoader
+    from pytorch_cifar_amd.data.synthetic import synthetic_cifar10
+    from pytorch_cifar_amd.engine.optim import SGD
+    from pytorch_cifar_amd.engine.trainer import NonFiniteLossError, Trainer
+    from pytorch_cifar_amd.parallel.launcher import DistContext
+
+    class Bad(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = torch.nn.Linear(3 * 32 * 32, 10)
+
+        def forward(self, x):
+            return self.fc(x.flatten(1)) * float("nan")
+
+    imgs, labs = synthetic_cifar10(64, seed=0)
+    ld = DeviceLoader(imgs, labs, 16, "cpu", crop_pad=0, flip=False)
+    net = Bad()
+    tr = Trainer(net, SGD(net.parameters(), lr=0.1), ld, ld, DistContext(), log_every=1)
+    with pytest.raises(NonFiniteLossError):
+        tr.train_epoch(0)
+
+
+def test_main_py_aux_flags_cpu(tmp_path):
+    out = _run([os.path.join(ROOT, "main.py"), "--model", "LeNet", "--epochs", "1", "--synthetic",
+                "--synthetic_size", "256", "--max_steps", "2", "--cpu", "--batch_size", "64",
+                "--deterministic", "--debug_sync", "--dtype", "fp32", "--no_nan_guard",
+                "--profile", str(tmp_path / "p.json"), "--checkpoint_dir", str(tmp_path / "ck")],
+               cwd=str(tmp_path))
+    assert "Profile trace written" in out

@@ -56,3 +56,14 @@ def test_native_rccl_single_rank():
     torch.cuda.synchronize()
     torch.testing.assert_close(t, ref)
     comm.destroy()
+
+
+def test_main_py_gpu_fp32_and_deterministic(tmp_path):
+    out = _run([os.path.join(ROOT, "main.py"), "--model", "ResNet18", "--epochs", "1",
+                "--synthetic", "--synthetic_size", "2048", "--max_steps", "4", "--dtype", "fp32",
+                "--checkpoint_dir", str(tmp_path / "a")], cwd=str(tmp_path))
+    assert "Saving.." in out, out[-2000:]
+    out = _run([os.path.join(ROOT, "main.py"), "--model", "ResNet18", "--epochs", "1",
+                "--synthetic", "--synthetic_size", "2048", "--max_steps", "4", "--deterministic",
+                "--debug_sync", "--checkpoint_dir", str(tmp_path / "b")], cwd=str(tmp_path))
+    assert "Saving.." in out, out[-2000:]

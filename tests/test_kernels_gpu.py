@@ -334,3 +334,38 @@ def test_sgd_multi_tensor(C):
         ropt.step()
     for p, r in zip(ps, ref):
         assert rel_err(p.detach(), r.detach()) < 1e-5
+
+
+@pytest.mark.parametrize("case", [(8, 64, 32, 64, 3, 1, 1, 1), (4, 128, 16, 256, 3, 2, 1, 1),
+                                  (16, 256, 8, 256, 3, 1, 1, 1), (2, 24, 16, 16, 1, 1, 0, 1)])
+def test_wgrad_deterministic_mode_bitwise(C, case):
+    """set_deterministic: every wgrad path (halo, wide, split-K) reduces through ordered slab
+    rows -> two runs are bitwise identical (atomics make the default mode order-dependent)."""
+    N, Cin, H, Cout, k, s, p, G = case
+    torch.manual_seed(3)
+    x = nhwc(torch.randn(N, Cin, H, H, device="cuda")).to(torch.bfloat16)
+    Ho = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Ho, Ho, Cout, device="cuda").to(torch.bfloat16)
+    C.set_deterministic(True)
+    try:
+        for cfg in [-1, 3, 16, 32]:
+            C.set_conv_tile(1, cfg)
+            a = C.conv_wgrad(x, dy, k, k, s, p, G, None)
+            b = C.conv_wgrad(x, dy, k, k, s, p, G, None)
+            assert torch.equal(a, b), cfg
+    finally:
+        C.set_deterministic(False)
+        C.set_conv_tile(1, -1)
+
+
+def test_debug_sync_proxy_runs_ops():
+    from pytorch_cifar_amd import _native
+
+    _native.set_debug_sync(True)
+    try:
+        C = _native.lib()
+        x = torch.randn(2, 8, 8, 16, device="cuda").to(torch.bfloat16)
+        y = C.gap_fwd(x)
+        assert y.shape[-1] == 16 and C.last_error() == ""
+    finally:
+        _native.set_debug_sync(False)
