@@ -175,7 +175,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
                                                        size_t total, const bf16* __restrict__ res,
                                                        const bf16* __restrict__ y2,
                                                        const float* __restrict__ aux2, int act,
-                                                       bf16* __restrict__ out) {
+                                                       bf16* __restrict__ out,
+                                                       uint8_t* __restrict__ mask) {
   const size_t nvec = total / VEC;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 256) {
     const size_t e = i * VEC;
@@ -199,16 +200,30 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int v = 0; v < VEC; ++v) f[v] = apply_act(f[v], act);
     store_vec<VEC>(out + e, f);
+    if constexpr (VEC == 8) {
+      // ReLU mask as bits (1 byte per 8 channels): the backward reads T/16 bytes instead of the
+      // bf16 output (T), which it only needs for the sign
+      if (mask) {
+        uint32_t b = 0;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) b |= (f[v] > 0.f ? 1u : 0u) << v;
+        mask[i] = (uint8_t)b;
+      }
+    }
   }
 }
 
 // dz from the incoming gradient: relu uses the saved output as mask; swish/sigmoid recompute z.
 template <int VEC>
-__device__ __forceinline__ void compute_dz(const bf16* dout, const bf16* out, const bf16* y,
-                                           const float* aux, int C, int c0, size_t e, int act,
-                                           float* dz) {
+__device__ __forceinline__ void compute_dz(const bf16* dout, const bf16* out, const uint8_t* mask,
+                                           const bf16* y, const float* aux, int C, int c0, size_t e,
+                                           int act, float* dz) {
   load_vec<VEC>(dout + e, dz);
-  if (act == ACT_RELU) {
+  if (act == ACT_RELU && VEC == 8 && mask) {
+    const uint32_t b = mask[e >> 3];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) dz[v] = ((b >> v) & 1u) ? dz[v] : 0.f;
+  } else if (act == ACT_RELU) {
     float o[VEC];
     load_vec<VEC>(out + e, o);
 #pragma unroll
@@ -227,9 +242,10 @@ __device__ __forceinline__ void compute_dz(const bf16* dout, const bf16* out, co
 // ---- backward reduce: partial[P][NS][C] with sums of dz, dz*xhat, (dz*xhat2) ----
 template <int VEC, int NS>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
-    const bf16* __restrict__ dout, const bf16* __restrict__ out, const bf16* __restrict__ y,
-    const float* __restrict__ aux, const bf16* __restrict__ y2, const float* __restrict__ aux2,
-    int act, int M, RowPar rp, int rows_per_block, float* __restrict__ partial) {
+    const bf16* __restrict__ dout, const bf16* __restrict__ out, const uint8_t* __restrict__ mask,
+    const bf16* __restrict__ y, const float* __restrict__ aux, const bf16* __restrict__ y2,
+    const float* __restrict__ aux2, int act, int M, RowPar rp, int rows_per_block,
+    float* __restrict__ partial) {
   __shared__ float red[256 * VEC * NS];
   const int t = threadIdx.x;
   const int gx = t % rp.TPR, ry = t / rp.TPR;
@@ -258,7 +274,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
       for (int r = r0 + ry; r < r1; r += rp.RPP) {
         const size_t e = (size_t)r * C + c0;
         float dz[VEC], yy[VEC];
-        compute_dz<VEC>(dout, out, y, aux, C, c0, e, act, dz);
+        compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz);
         load_vec<VEC>(y + e, yy);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
@@ -355,8 +371,9 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
 // ---- backward apply: dy = a*dz + b*y + d ; dres = dz ; dy2 = a2*dz + b2*y2 + d2 ----
 template <int VEC>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const bf16* __restrict__ dout, const bf16* __restrict__ out, const bf16* __restrict__ y,
-    const float* __restrict__ aux, const float* __restrict__ coef, int act, int C, size_t total,
+    const bf16* __restrict__ dout, const bf16* __restrict__ out, const uint8_t* __restrict__ mask,
+    const bf16* __restrict__ y, const float* __restrict__ aux, const float* __restrict__ coef,
+    int act, int C, size_t total,
     bf16* __restrict__ dy, bf16* __restrict__ dres, const bf16* __restrict__ y2,
     bf16* __restrict__ dy2) {
   const size_t nvec = total / VEC;
@@ -364,7 +381,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const size_t e = i * VEC;
     const int c0 = (int)(e % C);
     float dz[VEC], yy[VEC], o[VEC];
-    compute_dz<VEC>(dout, out, y, aux, C, c0, e, act, dz);
+    compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz);
     load_vec<VEC>(y + e, yy);
 #pragma unroll
     for (int v = 0; v < VEC; ++v) o[v] = coef[c0 + v] * dz[v] + coef[C + c0 + v] * yy[v] + coef[2 * C + c0 + v];
@@ -426,35 +443,37 @@ void bn_finalize_launch(const float* stat, int R, int C, double count, const flo
 }
 
 void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const bf16* res,
-                     const bf16* y2, const float* aux2, int act, bf16* out, hipStream_t st) {
+                     const bf16* y2, const float* aux2, int act, bf16* out, uint8_t* mask,
+                     hipStream_t st) {
   if (C % 8 == 0) {
     hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, y, aux, C,
-                       total, res, y2, aux2, act, out);
+                       total, res, y2, aux2, act, out, mask);
   } else {
     hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(total)), dim3(256), 0, st, y, aux, C,
-                       total, res, y2, aux2, act, out);
+                       total, res, y2, aux2, act, out, (uint8_t*)nullptr);
   }
 }
 
-void bn_bwd_reduce_launch(const bf16* dout, const bf16* out, const bf16* y, const float* aux,
+void bn_bwd_reduce_launch(const bf16* dout, const bf16* out, const uint8_t* mask, const bf16* y,
+                          const float* aux,
                           const bf16* y2, const float* aux2, int act, int M, int C,
                           float* partial, int P, hipStream_t st) {
   const int rows = cdiv(M, P);
   if (C % 8 == 0) {
     RowPar rp = make_rowpar(C, 8);
     if (y2)
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<8, 3>), dim3(P), dim3(256), 0, st, dout, out, y, aux,
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<8, 3>), dim3(P), dim3(256), 0, st, dout, out, mask, y, aux,
                          y2, aux2, act, M, rp, rows, partial);
     else
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<8, 2>), dim3(P), dim3(256), 0, st, dout, out, y, aux,
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<8, 2>), dim3(P), dim3(256), 0, st, dout, out, mask, y, aux,
                          y2, aux2, act, M, rp, rows, partial);
   } else {
     RowPar rp = make_rowpar(C, 1);
     if (y2)
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, 3>), dim3(P), dim3(256), 0, st, dout, out, y, aux,
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, 3>), dim3(P), dim3(256), 0, st, dout, out, mask, y, aux,
                          y2, aux2, act, M, rp, rows, partial);
     else
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, 2>), dim3(P), dim3(256), 0, st, dout, out, y, aux,
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, 2>), dim3(P), dim3(256), 0, st, dout, out, mask, y, aux,
                          y2, aux2, act, M, rp, rows, partial);
   }
 }
@@ -474,15 +493,15 @@ void bn_bwd_finalize_launch(const float* stat, int R, int NS, int C, float count
                        coef, accumulate);
 }
 
-void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const bf16* y, const float* aux,
-                         const float* coef, int act, int C, size_t total, bf16* dy, bf16* dres,
-                         const bf16* y2, bf16* dy2, hipStream_t st) {
+void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask, const bf16* y,
+                         const float* aux, const float* coef, int act, int C, size_t total,
+                         bf16* dy, bf16* dres, const bf16* y2, bf16* dy2, hipStream_t st) {
   if (C % 8 == 0) {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, dout,
-                       out, y, aux, coef, act, C, total, dy, dres, y2, dy2);
+                       out, mask, y, aux, coef, act, C, total, dy, dres, y2, dy2);
   } else {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(grid_for(total)), dim3(256), 0, st, dout, out,
-                       y, aux, coef, act, C, total, dy, dres, y2, dy2);
+                       (const uint8_t*)nullptr, y, aux, coef, act, C, total, dy, dres, y2, dy2);
   }
 }
 

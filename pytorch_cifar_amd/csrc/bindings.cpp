@@ -33,14 +33,15 @@ int colsum_launch(const float*, int, int, float*, hipStream_t);
 void bn_finalize_launch(const float*, int, int, double, const float*, const float*, float*, float*,
                         int64_t*, float, float, int, int, float*, hipStream_t);
 void bn_apply_launch(const bf16*, const float*, int, size_t, const bf16*, const bf16*,
-                     const float*, int, bf16*, hipStream_t);
-void bn_bwd_reduce_launch(const bf16*, const bf16*, const bf16*, const float*, const bf16*,
-                          const float*, int, int, int, float*, int, hipStream_t);
+                     const float*, int, bf16*, uint8_t*, hipStream_t);
+void bn_bwd_reduce_launch(const bf16*, const bf16*, const uint8_t*, const bf16*, const float*,
+                          const bf16*, const float*, int, int, int, float*, int, hipStream_t);
 void bn_bwd_finalize_launch(const float*, int, int, int, float, const float*, const float*,
                             const float*, const float*, int, float*, float*, float*, float*,
                             float*, int, hipStream_t);
-void bn_bwd_apply_launch(const bf16*, const bf16*, const bf16*, const float*, const float*, int,
-                         int, size_t, bf16*, bf16*, const bf16*, bf16*, hipStream_t);
+void bn_bwd_apply_launch(const bf16*, const bf16*, const uint8_t*, const bf16*, const float*,
+                         const float*, int, int, size_t, bf16*, bf16*, const bf16*, bf16*,
+                         hipStream_t);
 // misc.hip
 void nchw_to_nhwc_launch(const float*, int, int, int, int, bf16*, hipStream_t);
 void nhwc_to_nchw_launch(const bf16*, int, int, int, int, float*, hipStream_t);
@@ -246,8 +247,9 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
   return aux;
 }
 
-Tensor bn_apply(const Tensor& y, const Tensor& aux, const optional<Tensor>& res,
-                const optional<Tensor>& y2, const optional<Tensor>& aux2, int act) {
+std::vector<Tensor> bn_apply(const Tensor& y, const Tensor& aux, const optional<Tensor>& res,
+                             const optional<Tensor>& y2, const optional<Tensor>& aux2, int act,
+                             bool want_mask) {
   check_bf16(y, "y");
   const int C = y.size(-1);
   TORCH_CHECK(aux.size(1) == C, "aux channel mismatch");
@@ -260,13 +262,19 @@ Tensor bn_apply(const Tensor& y, const Tensor& aux, const optional<Tensor>& res,
     TORCH_CHECK(y2->sizes() == y.sizes(), "second BN input shape mismatch");
   }
   auto out = at::empty_like(y);
+  // ReLU sign bits (1 byte / 8 channels) for the backward, when C allows the 8-wide path
+  Tensor mask;
+  if (want_mask && act == 1 && C % 8 == 0)
+    mask = at::empty({(int64_t)(y.numel() / 8)}, y.options().dtype(at::kByte));
   pca::bn_apply_launch(ptr<bf16>(y), ptr<float>(aux), C, y.numel(), optr<bf16>(res), optr<bf16>(y2),
-                       optr<float>(aux2), act, ptr<bf16>(out), cur_stream());
-  return out;
+                       optr<float>(aux2), act, ptr<bf16>(out),
+                       mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return {out, mask};
 }
 
 // Full BN backward: returns {dy, dres, dy2, dgamma, dbeta, dgamma2, dbeta2}
-std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out, const Tensor& y,
+std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
+                                const optional<Tensor>& mask, const Tensor& y,
                                 const Tensor& aux, const optional<Tensor>& gamma,
                                 const optional<Tensor>& y2, const optional<Tensor>& aux2,
                                 const optional<Tensor>& gamma2, int act, bool training,
@@ -280,12 +288,16 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
   const int M = y.numel() / C;
   const bool dual = y2.has_value() && y2->defined();
   const int NS = dual ? 3 : 2;
-  if (act == 1) TORCH_CHECK(out.has_value() && out->defined(), "relu backward needs the output");
+  const bool has_mask = mask.has_value() && mask->defined();
+  if (act == 1)
+    TORCH_CHECK((out.has_value() && out->defined()) || (has_mask && C % 8 == 0),
+                "relu backward needs the output or its sign mask");
+  const uint8_t* mk = has_mask ? mask->data_ptr<uint8_t>() : nullptr;
   auto st = cur_stream();
   const int P = pca::bn_row_blocks(M, C);
   auto fopt = y.options().dtype(at::kFloat);
   auto partial = at::empty({P, NS, C}, fopt);
-  pca::bn_bwd_reduce_launch(ptr<bf16>(dout), optr<bf16>(out), ptr<bf16>(y), ptr<float>(aux),
+  pca::bn_bwd_reduce_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
                             optr<bf16>(y2), optr<float>(aux2), act, M, C, ptr<float>(partial), P,
                             st);
   const float* stat = ptr<float>(partial);
@@ -322,7 +334,7 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
   Tensor dres, dy2;
   if (need_dres) dres = at::empty_like(y);
   if (dual) dy2 = at::empty_like(y);
-  pca::bn_bwd_apply_launch(ptr<bf16>(dout), optr<bf16>(out), ptr<bf16>(y), ptr<float>(aux),
+  pca::bn_bwd_apply_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
                            ptr<float>(coef), act, C, y.numel(), ptr<bf16>(dy),
                            need_dres ? ptr<bf16>(dres) : nullptr, optr<bf16>(y2),
                            dual ? ptr<bf16>(dy2) : nullptr, st);

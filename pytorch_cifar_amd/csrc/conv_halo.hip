@@ -18,6 +18,7 @@
 #include "mfma_util.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 namespace pca {
@@ -81,7 +82,7 @@ struct HaloShape {
 };
 
 template <int W, int MB, int WM, int WN>
-__global__ __launch_bounds__(WM * WN * 64) void wgrad_halo_kernel(const bf16* __restrict__ X,
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wgrad_halo_kernel(const bf16* __restrict__ X,
                                                                   const bf16* __restrict__ DY,
                                                                   float* __restrict__ out,
                                                                   const HaloGeom g) {
@@ -308,9 +309,7 @@ template <int W, int MB, int WM, int WN>
 static int halo_occupancy() {
   static int occ = 0;
   if (occ == 0) {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, (const void*)wgrad_halo_kernel<W, MB, WM, WN>, WM * WN * 64, 0);
-    occ = std::max(1, occ);
+occ = blocks_per_cu((const void*)wgrad_halo_kernel<W, MB, WM, WN>, WM * WN * 64, "wgrad_halo");
   }
   return occ;
 }
@@ -376,6 +375,10 @@ static int64_t halo_plan(HaloGeom& g) {
   g.chunk = chunk;
   g.splits = splits;
   g.atomic = (!g_deterministic && splits <= 4) ? 1 : 0;
+  static const bool verbose = getenv("PCA_CONV_VERBOSE") != nullptr;
+  if (verbose)
+    fprintf(stderr, "[pca] halo wgrad W=%d MB=%d waves=%d: occ=%d cus=%d tiles=%d splits=%d chunk=%d atomic=%d\n",
+            W, MB, WM * WN, halo_occupancy<W, MB, WM, WN>(), halo_cus(), tiles, splits, chunk, g.atomic);
   if (g.atomic) return 0;
   return slab_ws_floats(splits, (int64_t)g.groups * g.cout_g * g.Ktot);
 }

@@ -747,12 +747,9 @@ template <int BM, int BN, int WM, int WN, int ST, int MODE>
 static int igemm_occupancy() {
   static int occ = 0;
   if (occ == 0) {
-    int a = 0, b = 0;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &a, (const void*)conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, true>, WM * WN * 64, 0);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &b, (const void*)conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, false>, WM * WN * 64, 0);
-    occ = std::max(1, std::min(a, b));
+occ = std::min(
+        blocks_per_cu((const void*)conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, true>, WM * WN * 64, "igemm"),
+        blocks_per_cu((const void*)conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, false>, WM * WN * 64, "igemm"));
   }
   return occ;
 }
@@ -925,9 +922,7 @@ template <int MB, int NB, int WM, int WN>
 static int wide_occupancy() {
   static int occ = 0;
   if (occ == 0) {
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, (const void*)conv_wgrad_wide_kernel<MB, NB, WM, WN>, WM * WN * 64, 0);
-    occ = std::max(1, occ);
+occ = blocks_per_cu((const void*)conv_wgrad_wide_kernel<MB, NB, WM, WN>, WM * WN * 64, "wgrad_wide");
   }
   return occ;
 }

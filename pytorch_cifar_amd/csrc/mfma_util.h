@@ -4,7 +4,37 @@
 #pragma once
 #include "common.h"
 
+#include <algorithm>
+
+#include <cstdio>
+#include <cstdlib>
+
 namespace pca {
+
+// Resident workgroups per CU of a kernel on gfx950 (160 KiB LDS, 512 VGPR+AGPR per lane per SIMD,
+// 8 waves per SIMD), from the code object's attributes. hipOccupancyMaxActiveBlocksPerMultiprocessor
+// is not used: on this stack it reported 1 block/CU for every kernel with > 32 KiB of LDS, which
+// sized the persistent grids for a quarter of the machine.
+inline int blocks_per_cu(const void* fn, int threads, const char* name) {
+  hipFuncAttributes a{};
+  (void)hipFuncGetAttributes(&a, fn);
+  const int waves = (threads + 63) / 64;                 // per block
+  const int wps = (waves + 3) / 4;                       // waves per SIMD per block
+  int regs = a.numRegs > 0 ? a.numRegs : 256;
+  regs = (regs + 7) / 8 * 8;
+  int by_regs = std::max(1, 512 / regs);                 // waves per SIMD
+  by_regs = std::min(by_regs, 8) / wps;
+  const int lds = (int)a.sharedSizeBytes;
+  const int by_lds = lds > 0 ? (160 * 1024) / lds : 32;
+  int occ = std::max(1, std::min({by_regs, by_lds, 32 / waves}));
+  int api = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, fn, threads, 0);
+  static const bool verbose = getenv("PCA_CONV_VERBOSE") != nullptr;
+  if (verbose)
+    fprintf(stderr, "[pca] occupancy %s: regs=%d lds=%d threads=%d -> %d blocks/CU (hip api %d)\n",
+            name, a.numRegs, lds, threads, occ, api);
+  return occ;
+}
 
 // Exact unsigned division by a runtime constant (n < 2^31): q = (umulhi(n, m) + n) >> s.
 struct FastDiv {

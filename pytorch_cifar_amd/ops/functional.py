@@ -326,16 +326,21 @@ class _BatchNormAct(torch.autograd.Function):
         aux2 = None
         if y2 is not None:
             aux2 = _bn_aux(C, cfg.bn2, y2, stats2 if stats2 is not None and stats2.numel() else None, cfg.training, cfg.count)
-        out = C.bn_apply(y, aux, res, y2, aux2, ACT[cfg.act])
+        relu = ACT[cfg.act] == 1
+        out, mask = C.bn_apply(y, aux, res, y2, aux2, ACT[cfg.act], relu)
         ctx.cfg = cfg
         ctx.has_res = res is not None
-        ctx.save_for_backward(y, out if ACT[cfg.act] == 1 else None, aux, y2, aux2)
+        # ReLU backward needs only the sign of the output: keep the 1-bit mask when the kernel
+        # produced one (C % 8 == 0), else the output itself
+        has_mask = mask is not None and mask.numel() > 0
+        ctx.save_for_backward(y, out if (relu and not has_mask) else None, mask if has_mask else None,
+                              aux, y2, aux2)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         C = _C()
-        y, out, aux, y2, aux2 = ctx.saved_tensors
+        y, out, mask, aux, y2, aux2 = ctx.saved_tensors
         cfg = ctx.cfg
         bn, bn2 = cfg.bn, cfg.bn2
         dout = dout.contiguous()
@@ -350,7 +355,7 @@ class _BatchNormAct(torch.autograd.Function):
         if bn2 is not None:
             g2, b2 = acc(bn2.weight), acc(bn2.bias)
         dy, dres, dy2, dg, db, dg2, db2 = C.bn_backward(
-            dout, out, y, aux,
+            dout, out, mask, y, aux,
             bn.weight.detach() if bn.weight is not None else None,
             y2, aux2,
             bn2.weight.detach() if (bn2 is not None and bn2.weight is not None) else None,

@@ -176,12 +176,17 @@ def test_bn_fwd_bwd(C, C_, act, res):
     nbt = torch.zeros((), dtype=torch.long, device="cuda")
     partial = C.bn_stats(yn)
     aux = C.bn_finalize(partial, float(N * H * H), gamma.detach(), beta.detach(), rm, rv, nbt, 0.1, 1e-5, True, True)
-    out = C.bn_apply(yn, aux, rn, None, None, act)
+    out, mask = C.bn_apply(yn, aux, rn, None, None, act, act == 1)
     assert rel_err(nchw(out), out_ref) < 2e-2
+    if act == 1 and C_ % 8 == 0:   # ReLU sign bits, one byte per 8 channels
+        bits = ((mask.view(-1, 1).int() >> torch.arange(8, device="cuda")) & 1).view(-1)
+        assert torch.equal(bits.bool(), (out.reshape(-1) > 0))
     assert rel_err(rm, rm_ref) < 1e-4 and rel_err(rv, rv_ref) < 1e-4
     assert nbt.item() == 1
     dn = nhwc(dout).to(torch.bfloat16)
-    dy, dres, _, dg, db, _, _ = C.bn_backward(dn, out, yn, aux, gamma.detach(), None, None, None, act, True, res, None, None, None, None)
+    use_mask = mask is not None and mask.numel() > 0
+    dy, dres, _, dg, db, _, _ = C.bn_backward(dn, None if use_mask else out, mask if use_mask else None, yn, aux,
+                                              gamma.detach(), None, None, None, act, True, res, None, None, None, None)
     assert rel_err(nchw(dy), y.grad) < 3e-2
     assert rel_err(dg, gamma.grad) < 1e-2
     assert rel_err(db, beta.grad) < 1e-2
@@ -208,9 +213,9 @@ def test_bn_dual_shortcut(C):
     o_ = torch.ones(Ch, device="cuda")
     a1 = C.bn_finalize(C.bn_stats(y1n), cnt, g1.detach(), b1.detach(), z_.clone(), o_.clone(), None, 0.1, 1e-5, True, False)
     a2 = C.bn_finalize(C.bn_stats(y2n), cnt, g2.detach(), b2.detach(), z_.clone(), o_.clone(), None, 0.1, 1e-5, True, False)
-    out = C.bn_apply(y1n, a1, None, y2n, a2, 1)
+    out, _ = C.bn_apply(y1n, a1, None, y2n, a2, 1, False)
     assert rel_err(nchw(out), out_ref) < 2e-2
-    dy1, _, dy2, dg1, db1, dg2, db2 = C.bn_backward(nhwc(dout).bfloat16(), out, y1n, a1, g1.detach(), y2n, a2, g2.detach(), 1, True, False, None, None, None, None)
+    dy1, _, dy2, dg1, db1, dg2, db2 = C.bn_backward(nhwc(dout).bfloat16(), out, None, y1n, a1, g1.detach(), y2n, a2, g2.detach(), 1, True, False, None, None, None, None)
     assert rel_err(nchw(dy1), y1.grad) < 3e-2
     assert rel_err(nchw(dy2), y2.grad) < 3e-2
     assert rel_err(dg1, g1.grad) < 1e-2 and rel_err(dg2, g2.grad) < 1e-2
