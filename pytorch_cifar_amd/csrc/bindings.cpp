@@ -20,7 +20,7 @@ int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
                        int groups, int Ho, int Wo);
 void set_conv_tile(int kind, int idx);
 void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int, int, int, int,
-                       int, int, int, int, hipStream_t);
+                       int, int, int, int, hipStream_t, const bf16* addend);
 void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
                        int Cin, int Cout, int KH, int KW, int stride, int pad, int groups, int Ho,
                        int Wo, hipStream_t st);
@@ -148,7 +148,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
 }
 
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, int pad,
-                  int groups) {
+                  int groups, const optional<Tensor>& addend) {
   check_bf16(dy, "dy");
   check_bf16(wt, "wt");
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
@@ -158,8 +158,14 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, 
   TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo,
               "dgrad geometry mismatch");
   auto dx = at::empty({N, H, W, Cin}, dy.options());
+  const bf16* add = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    check_bf16(*addend, "addend");
+    TORCH_CHECK(addend->numel() == dx.numel() && addend->is_contiguous(), "addend must match dx (NHWC)");
+    add = ptr<bf16>(*addend);
+  }
   pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dx), N, H, W, Cin, Cout, KH, KW,
-                         stride, pad, groups, Ho, Wo, cur_stream());
+                         stride, pad, groups, Ho, Wo, cur_stream(), add);
   return dx;
 }
 
@@ -618,7 +624,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return e == hipSuccess ? std::string() : std::string(hipGetErrorString(e));
   }, "hipGetLastError() of this thread as a string ('' = no error); clears it");
   m.def("conv_fwd", &conv_fwd);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"),
+        py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("set_conv_tile", &pca::set_conv_tile, "override tile config (kind 0: fwd/dgrad, 1: wgrad; -1 = heuristic)");
   m.def("weight_prep", &weight_prep);

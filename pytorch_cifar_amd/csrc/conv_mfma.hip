@@ -58,6 +58,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
                                                                   bf16* __restrict__ Y,
                                                                   float* __restrict__ stats,
                                                                   const float* __restrict__ bias,
+                                                                  const bf16* __restrict__ addend,
                                                                   const ConvGeom g) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BK = 64;                 // K elements per stage: 128-byte LDS rows
@@ -344,8 +345,18 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
           const uint32_t w = rem - h * rows_w;
           pix = ((size_t)n * g.Ho + 2 * h + ph) * g.Wo + 2 * w + pw;
         }
-        const uint4 v = *reinterpret_cast<const uint4*>(Cs + r * CST + c8 * 8);
-        *reinterpret_cast<uint4*>(Y + pix * g.Co + (size_t)grp * g.Cn + gc) = v;
+        uint4 v = *reinterpret_cast<const uint4*>(Cs + r * CST + c8 * 8);
+        const size_t o = pix * g.Co + (size_t)grp * g.Cn + gc;
+        if (addend) {
+          // fused gradient accumulation (dgrad): dX = conv^T(dY) + the other branch's dX
+          float a[8], b[8];
+          unpack8(v, a);
+          unpack8(*reinterpret_cast<const uint4*>(addend + o), b);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) a[q] += b[q];
+          v = pack8(a);
+        }
+        *reinterpret_cast<uint4*>(Y + o) = v;
       }
     }
     __syncthreads();   // the C tile aliases the ring the next tile's prologue refills
@@ -775,15 +786,15 @@ static int igemm_grid_x_t(const ConvGeom& g) {
 
 template <int BM, int BN, int WM, int WN, int ST, int MODE>
 static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, const float* bias,
-                         const ConvGeom& g, hipStream_t st) {
+                         const ConvGeom& g, hipStream_t st, const bf16* addend = nullptr) {
   dim3 grid(igemm_grid_x_t<BM, BN, WM, WN, ST, MODE>(g), cdiv(g.Cn, BN),
             g.groups * (MODE == 2 ? 4 : 1));
   if (stats)
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, true>), grid,
-                       dim3(WM * WN * 64), 0, st, A, B, Y, stats, bias, g);
+                       dim3(WM * WN * 64), 0, st, A, B, Y, stats, bias, addend, g);
   else
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, false>), grid,
-                       dim3(WM * WN * 64), 0, st, A, B, Y, stats, bias, g);
+                       dim3(WM * WN * 64), 0, st, A, B, Y, stats, bias, addend, g);
 }
 
 // Tile configurations. The heuristic picks by GEMM N (channels per group); a process-wide
@@ -825,13 +836,13 @@ static int igemm_select(const ConvGeom& g) {
 
 template <int MODE>
 static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, const float* bias,
-                           const ConvGeom& g, hipStream_t st) {
+                           const ConvGeom& g, hipStream_t st, const bf16* addend = nullptr) {
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
-    case C: launch_igemm<BM, BN, WM, WN, ST, MODE>(A, B, Y, stats, bias, g, st); break;
+    case C: launch_igemm<BM, BN, WM, WN, ST, MODE>(A, B, Y, stats, bias, g, st, addend); break;
     PCA_IGEMM_CFGS(PCA_CASE)
 #undef PCA_CASE
-    default: launch_igemm<128, 128, 2, 2, 2, MODE>(A, B, Y, stats, bias, g, st); break;
+    default: launch_igemm<128, 128, 2, 2, 2, MODE>(A, B, Y, stats, bias, g, st, addend); break;
   }
 }
 
@@ -865,16 +876,16 @@ void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, f
 // dx = conv^T(dy, W); wt is W transposed to [Cin][KH][KW][Cout/G].
 void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, int W, int Cin,
                        int Cout, int KH, int KW, int stride, int pad, int groups, int Ho, int Wo,
-                       hipStream_t st) {
+                       hipStream_t st, const bf16* addend) {
   ConvGeom g = make_geom(N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, groups, Cout / groups,
                          Cin / groups);
   if (stride == 2 && H % 2 == 0 && W % 2 == 0 && Ho == H / 2 && Wo == W / 2) {
     // parity-class decomposition: rows are one class's (H/2) x (W/2) pixels
     g.fd_hw = make_fastdiv((H / 2) * (W / 2));
     g.fd_w = make_fastdiv(W / 2);
-    igemm_dispatch<2>(dy, wt, dx, nullptr, nullptr, g, st);
+    igemm_dispatch<2>(dy, wt, dx, nullptr, nullptr, g, st, addend);
   } else {
-    igemm_dispatch<1>(dy, wt, dx, nullptr, nullptr, g, st);
+    igemm_dispatch<1>(dy, wt, dx, nullptr, nullptr, g, st, addend);
   }
 }
 

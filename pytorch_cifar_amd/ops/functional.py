@@ -12,6 +12,7 @@ except pure data movement (cat/slice/shuffle views) which has no arithmetic.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -100,12 +101,64 @@ def _round8(c: int) -> int:
     return (c + 7) // 8 * 8
 
 
+# ------------------------------------------------------------- gradient hand-off slots
+# An activation read by several ops (a residual block's input: conv1 and the skip path) gets its
+# gradient summed by autograd with a separate elementwise add (3 tensor passes). A GradSlot on the
+# activation lets the first MFMA conv that read it ("owner") fold the other contribution into its
+# dgrad epilogue instead: a producer (the residual BN or another conv on the same input) whose
+# backward runs first deposits its gradient and returns None; the owner's dgrad adds it while
+# storing dX. Order-safe: a producer that runs after the owner returns its gradient normally.
+_FUSE_GRAD = os.environ.get("PCA_FUSE_RESIDUAL_GRAD", "1") != "0"
+
+
+class GradSlot:
+    __slots__ = ("grad", "closed")
+
+    def __init__(self):
+        self.grad = None
+        self.closed = False
+
+    def offer(self, g) -> bool:
+        if self.closed or self.grad is not None or g is None:
+            return False
+        self.grad = g
+        return True
+
+    def take(self):
+        g, self.grad = self.grad, None
+        self.closed = True
+        return g
+
+
+def _slot_for_conv(x):
+    """(slot, is_owner) for an MFMA conv reading the user-level activation ``x``."""
+    if not (_FUSE_GRAD and x.requires_grad and torch.is_grad_enabled()):
+        return None, False
+    s = getattr(x, "_pca_slot", None)
+    if s is None:
+        s = GradSlot()
+        try:
+            x._pca_slot = s
+        except Exception:
+            return None, False
+        return s, True
+    return s, False
+
+
+def _slot_for_residual(x):
+    if not (_FUSE_GRAD and x is not None and x.requires_grad):
+        return None
+    return getattr(x, "_pca_slot", None)
+
+
 class _ConvMFMA(torch.autograd.Function):
     """Implicit-GEMM MFMA conv (fwd + BN-stat epilogue, dgrad, split-K wgrad)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, groups, want_stats, cin_pad):
+    def forward(ctx, x, weight, bias, stride, padding, groups, want_stats, cin_pad, slot=None,
+                owner=False):
         C = _C()
+        ctx.slot, ctx.owner = slot, owner
         w_phys = G.physical(weight)
         if not w_phys.is_contiguous():
             w_phys = w_phys.contiguous()
@@ -132,7 +185,14 @@ class _ConvMFMA(torch.autograd.Function):
         weight, bias = ctx.weight, ctx.bias
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
+            slot = ctx.slot
+            if slot is not None and ctx.owner:
+                add = slot.take()            # the other branch's dX, summed in the epilogue
+                dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups, add)
+            else:
+                dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
+                if slot is not None and slot.offer(dx):
+                    dx = None                # delivered through the owner's epilogue
         KH, KW = weight.shape[2], weight.shape[3]
         dw_ret = db_ret = None
         if weight.requires_grad:
@@ -154,7 +214,7 @@ class _ConvMFMA(torch.autograd.Function):
                 G.accumulate(bias, db)
             else:
                 db_ret = db
-        return dx, dw_ret, db_ret, None, None, None, None, None
+        return dx, dw_ret, db_ret, None, None, None, None, None, None, None
 
 
 class _ConvDirect(torch.autograd.Function):
@@ -257,7 +317,9 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
             y = add_bias(y, bias)
         return to_nchw(y), None
     if Cg % 8 == 0 and cout_g % 8 == 0:
-        y, stats = _ConvMFMA.apply(to_nhwc(x), weight, bias, stride, padding, groups, want_stats, 0)
+        slot, owner = _slot_for_conv(x)
+        y, stats = _ConvMFMA.apply(to_nhwc(x), weight, bias, stride, padding, groups, want_stats, 0,
+                                   slot, owner)
         return to_nchw(y), (stats if want_stats else None)
     if groups == 1 and cout_g % 8 == 0 and Cin < 8 * 2 and Cout >= 16:
         # stem conv on 3-channel images: pad channels to 8 and run on MFMA
@@ -320,8 +382,9 @@ class _BatchNormAct(torch.autograd.Function):
     """out = act(BN(y) [+ residual | + BN2(y2)]) with stats from the conv epilogue when given."""
 
     @staticmethod
-    def forward(ctx, y, gamma, beta, res, y2, gamma2, beta2, stats, stats2, cfg):
+    def forward(ctx, y, gamma, beta, res, y2, gamma2, beta2, stats, stats2, cfg, slot=None):
         C = _C()
+        ctx.slot = slot
         aux = _bn_aux(C, cfg.bn, y, stats if stats is not None and stats.numel() else None, cfg.training, cfg.count)
         aux2 = None
         if y2 is not None:
@@ -377,8 +440,10 @@ class _BatchNormAct(torch.autograd.Function):
         if bn2 is not None:
             deliver(bn2.weight, g2, dg2, 5)
             deliver(bn2.bias, b2, db2, 6)
+        if ctx.has_res and ctx.slot is not None and ctx.slot.offer(dres):
+            dres = None                      # summed into the block input's dX by its owner conv
         return (dy, ret.get(1), ret.get(2), dres if ctx.has_res else None,
-                dy2 if y2 is not None else None, ret.get(5), ret.get(6), None, None, None)
+                dy2 if y2 is not None else None, ret.get(5), ret.get(6), None, None, None, None)
 
 
 def _ref_bn(bn, x, training):
@@ -432,7 +497,8 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
     cfg = _BNCfg(bn, bn2, act, training, N * H * W)
     out = _BatchNormAct.apply(y, bn.weight, bn.bias, res, y2,
                               bn2.weight if bn2 is not None else None,
-                              bn2.bias if bn2 is not None else None, stats, st2, cfg)
+                              bn2.bias if bn2 is not None else None, stats, st2, cfg,
+                              _slot_for_residual(residual))
     return to_nchw(out)
 
 
