@@ -13,6 +13,8 @@
 // Every reduction is a deterministic slab fold (no float atomics).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace pca {
 
 // Row-parallel geometry for an [M][C] NHWC matrix: TPR threads cover a row's granules
@@ -397,6 +399,148 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// ---- row-tiled fast paths (C % 8 == 0, C <= 2048) ----
+// Thread t owns the 8-channel group g = t % TPR for every row it visits, so the per-channel
+// coefficients live in registers for the whole kernel (the generic grid-stride kernels re-load
+// them per vector); consecutive threads still read consecutive 16-byte chunks of NHWC rows, and
+// two rows are in flight per thread.
+template <bool RES, bool DUAL, int ACT>
+__global__ __launch_bounds__(256) void bn_apply_rows_kernel(
+    const bf16* __restrict__ y, const float* __restrict__ aux, int C, int M,
+    const bf16* __restrict__ res, const bf16* __restrict__ y2, const float* __restrict__ aux2,
+    bf16* __restrict__ out, uint8_t* __restrict__ mask) {
+  const int TPR = C >> 3, RPB = 256 / TPR;
+  const int g = threadIdx.x % TPR, ro = threadIdx.x / TPR;
+  if (ro >= RPB) return;
+  const int c0 = g * 8;
+  float sc[8], sh[8], sc2[8], sh2[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) {
+    sc[v] = aux[2 * C + c0 + v];
+    sh[v] = aux[3 * C + c0 + v];
+    if constexpr (DUAL) {
+      sc2[v] = aux2[2 * C + c0 + v];
+      sh2[v] = aux2[3 * C + c0 + v];
+    }
+  }
+  const int rstep = gridDim.x * RPB;
+  for (int r = blockIdx.x * RPB + ro; r < M; r += 2 * rstep) {
+    const int r2 = r + rstep;
+    const bool two = r2 < M;
+    const size_t e = (size_t)r * C + c0, e2 = (size_t)r2 * C + c0;
+    float f[8], f2[8], t[8], t2[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + e), f);
+    if (two) unpack8(*reinterpret_cast<const uint4*>(y + e2), f2);
+    if constexpr (RES) {
+      unpack8(*reinterpret_cast<const uint4*>(res + e), t);
+      if (two) unpack8(*reinterpret_cast<const uint4*>(res + e2), t2);
+    }
+    if constexpr (DUAL) {
+      unpack8(*reinterpret_cast<const uint4*>(y2 + e), t);
+      if (two) unpack8(*reinterpret_cast<const uint4*>(y2 + e2), t2);
+    }
+    uint32_t b = 0, b2 = 0;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      float a = f[v] * sc[v] + sh[v], a2 = f2[v] * sc[v] + sh[v];
+      if constexpr (RES) { a += t[v]; a2 += t2[v]; }
+      if constexpr (DUAL) { a += t[v] * sc2[v] + sh2[v]; a2 += t2[v] * sc2[v] + sh2[v]; }
+      a = apply_act(a, ACT);
+      a2 = apply_act(a2, ACT);
+      b |= (a > 0.f ? 1u : 0u) << v;
+      b2 |= (a2 > 0.f ? 1u : 0u) << v;
+      f[v] = a;
+      f2[v] = a2;
+    }
+    *reinterpret_cast<uint4*>(out + e) = pack8(f);
+    if (two) *reinterpret_cast<uint4*>(out + e2) = pack8(f2);
+    if (mask) {
+      mask[e >> 3] = (uint8_t)b;
+      if (two) mask[e2 >> 3] = (uint8_t)b2;
+    }
+  }
+}
+
+template <bool RES, bool DUAL, bool MASK>
+__global__ __launch_bounds__(256) void bn_bwd_apply_rows_kernel(
+    const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
+    const float* __restrict__ coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2) {
+  const int TPR = C >> 3, RPB = 256 / TPR;
+  const int g = threadIdx.x % TPR, ro = threadIdx.x / TPR;
+  if (ro >= RPB) return;
+  const int c0 = g * 8;
+  float ca[8], cb[8], cd[8], ca2[8], cb2[8], cd2[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) {
+    ca[v] = coef[c0 + v];
+    cb[v] = coef[C + c0 + v];
+    cd[v] = coef[2 * C + c0 + v];
+    if constexpr (DUAL) {
+      ca2[v] = coef[3 * C + c0 + v];
+      cb2[v] = coef[4 * C + c0 + v];
+      cd2[v] = coef[5 * C + c0 + v];
+    }
+  }
+  const int rstep = gridDim.x * RPB;
+  for (int r = blockIdx.x * RPB + ro; r < M; r += 2 * rstep) {
+    const int r2 = r + rstep;
+    const bool two = r2 < M;
+    const size_t e = (size_t)r * C + c0, e2 = (size_t)r2 * C + c0;
+    float dz[8], dz2[8], yy[8], yy2[8];
+    unpack8(*reinterpret_cast<const uint4*>(dout + e), dz);
+    if (two) unpack8(*reinterpret_cast<const uint4*>(dout + e2), dz2);
+    unpack8(*reinterpret_cast<const uint4*>(y + e), yy);
+    if (two) unpack8(*reinterpret_cast<const uint4*>(y + e2), yy2);
+    if constexpr (MASK) {
+      const uint32_t m = mask[e >> 3];
+      const uint32_t m2 = two ? mask[e2 >> 3] : 0u;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        dz[v] = ((m >> v) & 1u) ? dz[v] : 0.f;
+        dz2[v] = ((m2 >> v) & 1u) ? dz2[v] : 0.f;
+      }
+    }
+    float o[8], o2[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      o[v] = ca[v] * dz[v] + cb[v] * yy[v] + cd[v];
+      o2[v] = ca[v] * dz2[v] + cb[v] * yy2[v] + cd[v];
+    }
+    *reinterpret_cast<uint4*>(dy + e) = pack8(o);
+    if (two) *reinterpret_cast<uint4*>(dy + e2) = pack8(o2);
+    if constexpr (RES) {
+      *reinterpret_cast<uint4*>(dres + e) = pack8(dz);
+      if (two) *reinterpret_cast<uint4*>(dres + e2) = pack8(dz2);
+    }
+    if constexpr (DUAL) {
+      unpack8(*reinterpret_cast<const uint4*>(y2 + e), yy);
+      if (two) unpack8(*reinterpret_cast<const uint4*>(y2 + e2), yy2);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        o[v] = ca2[v] * dz[v] + cb2[v] * yy[v] + cd2[v];
+        o2[v] = ca2[v] * dz2[v] + cb2[v] * yy2[v] + cd2[v];
+      }
+      *reinterpret_cast<uint4*>(dy2 + e) = pack8(o);
+      if (two) *reinterpret_cast<uint4*>(dy2 + e2) = pack8(o2);
+    }
+  }
+}
+
+static bool rows_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PCA_BN_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static int rows_grid(int M, int C) {
+  const int RPB = 256 / (C >> 3);
+  int b = cdiv(M, RPB * 2);
+  return b < 2048 ? (b ? b : 1) : 2048;
+}
+
 // =========================================== host ========================================
 
 static int grid_for(size_t nvec) {
@@ -445,6 +589,23 @@ void bn_finalize_launch(const float* stat, int R, int C, double count, const flo
 void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const bf16* res,
                      const bf16* y2, const float* aux2, int act, bf16* out, uint8_t* mask,
                      hipStream_t st) {
+  if (rows_enabled() && C % 8 == 0 && C <= 2048 && (act == ACT_RELU || act == ACT_NONE) && !(res && y2)) {
+    const int M = (int)(total / C);
+    const dim3 gr(rows_grid(M, C)), bl(256);
+#define PCA_APPLY(R, D, A) \
+    hipLaunchKernelGGL((bn_apply_rows_kernel<R, D, A>), gr, bl, 0, st, y, aux, C, M, res, y2, aux2, out, mask)
+    if (act == ACT_RELU) {
+      if (res) PCA_APPLY(true, false, ACT_RELU);
+      else if (y2) PCA_APPLY(false, true, ACT_RELU);
+      else PCA_APPLY(false, false, ACT_RELU);
+    } else {
+      if (res) PCA_APPLY(true, false, ACT_NONE);
+      else if (y2) PCA_APPLY(false, true, ACT_NONE);
+      else PCA_APPLY(false, false, ACT_NONE);
+    }
+#undef PCA_APPLY
+    return;
+  }
   if (C % 8 == 0) {
     hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, y, aux, C,
                        total, res, y2, aux2, act, out, mask);
@@ -496,6 +657,26 @@ void bn_bwd_finalize_launch(const float* stat, int R, int NS, int C, float count
 void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask, const bf16* y,
                          const float* aux, const float* coef, int act, int C, size_t total,
                          bf16* dy, bf16* dres, const bf16* y2, bf16* dy2, hipStream_t st) {
+  const bool masked = act == ACT_RELU && mask != nullptr;
+  if (rows_enabled() && C % 8 == 0 && C <= 2048 && (masked || act == ACT_NONE)) {
+    const int M = (int)(total / C);
+    const dim3 gr(rows_grid(M, C)), bl(256);
+#define PCA_BWD(R, D, K) \
+    hipLaunchKernelGGL((bn_bwd_apply_rows_kernel<R, D, K>), gr, bl, 0, st, dout, mask, y, coef, C, M, dy, dres, y2, dy2)
+    if (masked) {
+      if (dres && y2) PCA_BWD(true, true, true);
+      else if (dres) PCA_BWD(true, false, true);
+      else if (y2) PCA_BWD(false, true, true);
+      else PCA_BWD(false, false, true);
+    } else {
+      if (dres && y2) PCA_BWD(true, true, false);
+      else if (dres) PCA_BWD(true, false, false);
+      else if (y2) PCA_BWD(false, true, false);
+      else PCA_BWD(false, false, false);
+    }
+#undef PCA_BWD
+    return;
+  }
   if (C % 8 == 0) {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, dout,
                        out, mask, y, aux, coef, act, C, total, dy, dres, y2, dy2);

@@ -53,13 +53,18 @@ def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True):
     e_n, e_s = rel(out_n, out_r), rel(out_s, out_r)
     assert e_n <= factor * e_s + slack, f"logits: native {e_n:.4f} vs stock-bf16 {e_s:.4f}"
     gr, gn, gs = _grads(ref), _grads(native), _grads(stock)
+    # absolute floor: a parameter whose gradient nearly cancels over the batch (tiny norm, e.g.
+    # an SE bias) has a meaningless relative error; compare it against the typical grad norm
+    norms = sorted(g.norm().item() for g in gr.values() if g is not None)
+    scale = norms[len(norms) // 2] if norms else 0.0
     bad = []
     for name, g in gr.items():
         if g is None:
             assert gn[name] is None or gn[name].abs().max().item() == 0, name
             continue
         en, es = rel(gn[name], g), rel(gs[name], g)
-        if en > factor * es + slack:
+        small = (gn[name].detach().float().cpu() - g).norm().item() <= 0.02 * scale
+        if en > factor * es + slack and not small:
             bad.append((name, round(en, 4), round(es, 4)))
     assert not bad, f"grads worse than stock bf16 (name, native, stock): {bad[:10]}"
     if check_buffers:
