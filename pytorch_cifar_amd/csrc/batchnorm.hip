@@ -273,7 +273,29 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
           istd2[v] = aux2[C + c0 + v];
         }
       }
-      for (int r = r0 + ry; r < r1; r += rp.RPP) {
+      int r = r0 + ry;
+      if constexpr (VEC == 8 && NS == 2) {
+        // masked-ReLU / no-act fast path: two rows in flight per thread
+        if (mask || act == ACT_NONE) {
+          for (; r + rp.RPP < r1; r += 2 * rp.RPP) {
+            const size_t e = (size_t)r * C + c0, e2 = e + (size_t)rp.RPP * C;
+            float dz[8], dz2[8], yy[8], yy2[8];
+            unpack8(*reinterpret_cast<const uint4*>(dout + e), dz);
+            unpack8(*reinterpret_cast<const uint4*>(dout + e2), dz2);
+            unpack8(*reinterpret_cast<const uint4*>(y + e), yy);
+            unpack8(*reinterpret_cast<const uint4*>(y + e2), yy2);
+            const uint32_t m = mask ? mask[e >> 3] : 0xffu, m2 = mask ? mask[e2 >> 3] : 0xffu;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+              const float a = ((m >> v) & 1u) ? dz[v] : 0.f;
+              const float b = ((m2 >> v) & 1u) ? dz2[v] : 0.f;
+              acc[0][v] += a + b;
+              acc[1][v] += (a * (yy[v] - mean[v]) + b * (yy2[v] - mean[v])) * istd[v];
+            }
+          }
+        }
+      }
+      for (; r < r1; r += rp.RPP) {
         const size_t e = (size_t)r * C + c0;
         float dz[VEC], yy[VEC];
         compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz);
