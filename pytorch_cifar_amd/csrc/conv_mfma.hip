@@ -858,8 +858,17 @@ static int igemm_grid_x(const ConvGeom& g) {
 }
 
 // number of BN-statistics slab rows the forward launch will write (= grid.x)
+// ResNet layer-1 specialisation (conv3x3_c64.hip)
+bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                         int pad, int groups);
+int conv_c64_stat_rows(int N, int H);
+void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const bf16* addend,
+                     int N, int H, bool dgrad, hipStream_t st);
+
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo) {
+  if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return conv_c64_stat_rows(N, H);
   ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
                          Cout / groups);
   return igemm_grid_x<0>(g);
@@ -868,6 +877,11 @@ int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
 void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, float* stats, int N,
                      int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                      int groups, int Ho, int Wo, hipStream_t st) {
+  if (g_igemm_override < 0 && bias == nullptr &&
+      conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
+    conv_c64_launch(x, w, y, stats, nullptr, N, H, false, st);
+    return;
+  }
   ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
                          Cout / groups);
   igemm_dispatch<0>(x, w, y, stats, bias, g, st);
@@ -877,6 +891,10 @@ void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, f
 void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, int W, int Cin,
                        int Cout, int KH, int KW, int stride, int pad, int groups, int Ho, int Wo,
                        hipStream_t st, const bf16* addend) {
+  if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
+    conv_c64_launch(dy, wt, dx, nullptr, addend, N, H, true, st);
+    return;
+  }
   ConvGeom g = make_geom(N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, groups, Cout / groups,
                          Cin / groups);
   if (stride == 2 && H % 2 == 0 && W % 2 == 0 && Ho == H / 2 && Wo == W / 2) {
