@@ -106,10 +106,14 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
 
   float st_s[4] = {0.f, 0.f, 0.f, 0.f}, st_q[4] = {0.f, 0.f, 0.f, 0.f};
 
+  constexpr int STORES = (TILE * 8) / 256;      // global stores per thread per tile
+  wait_vmcnt<0>();                                // weights + first halo
   int it = 0;
   for (int t = blockIdx.x; t < g.tiles; t += gridDim.x, ++it) {
     const int buf = it & 1;
-    wait_vmcnt<0>();                              // this tile's halo (and last tile's stores)
+    // this tile's halo landed; the previous tile's output stores (issued after it, retired in
+    // order) may stay in flight
+    wait_vmcnt<STORES>();
     raw_barrier();
     if (t + (int)gridDim.x < g.tiles) issue(t + gridDim.x, buf ^ 1);
     const char* S = smem + buf * HBYTES;
@@ -120,12 +124,11 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 18; ++s) {
+    // K loop with the fragments of step s+1 read while step s's 16 MFMAs run (one wave per
+    // SIMD: the LDS latency has to hide behind this wave's own MFMAs)
+    auto load_step = [&](int s, bf16x8* af, bf16x8* bv) {
       const int tap = s >> 1, kh = tap / 3, kw = tap % 3;
       const int chunk = (s & 1) * 4 + kq;
-      bf16x8 af[4], bv[4];
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const int R = rbase[mi] + kh * W2 + kw;
@@ -138,11 +141,19 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
         const int pc = (lc & ~7) | ((lc ^ n) & 7);
         bv[ni] = *reinterpret_cast<const bf16x8*>(Bs + n * 1152 + pc * 16);
       }
+    };
+    bf16x8 fa[2][4], fb[2][4];
+    load_step(0, fa[0], fb[0]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < 18) load_step(s + 1, fa[cur ^ 1], fb[cur ^ 1]);
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cur][mi], fb[cur][ni], acc[mi][ni], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
 
