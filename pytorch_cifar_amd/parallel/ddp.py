@@ -61,11 +61,15 @@ class Bucket:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, ctx, bucket_cap_mb: float = 25.0,
                  first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
-                 find_unused_parameters: bool = True, arena: ParamArena | None = None):
+                 find_unused_parameters: bool = True, arena: ParamArena | None = None,
+                 force_collectives: bool = False):
         super().__init__()
         self.module = module
         self.ctx = ctx
         self.world = ctx.world
+        # issue every collective even on a 1-rank clique (GPU tests exercise the RCCL-in-hipGraph
+        # path on a single-GPU box this way; a world-1 RCCL all-reduce is a device copy)
+        self._collectives = self.world > 1 or force_collectives
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters
         params = [p for p in module.parameters() if p.requires_grad]
@@ -141,7 +145,7 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def _sync_initial_state(self):
-        if self.world == 1:
+        if not self._collectives:
             return
         self._fork()
         with self._stream_ctx():
@@ -153,7 +157,7 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
-        if self.broadcast_buffers and self.world > 1 and self.buffers_arena is not None \
+        if self.broadcast_buffers and self._collectives and self.buffers_arena is not None \
                 and self._require_forward_param_sync:
             with torch.no_grad():
                 self._fork()
@@ -189,7 +193,7 @@ class DistributedDataParallel(nn.Module):
         if b.launched:
             return
         b.launched = True
-        if self.world == 1:
+        if not self._collectives:
             return
         self._fork()
         with self._stream_ctx():

@@ -67,3 +67,52 @@ def test_main_py_gpu_fp32_and_deterministic(tmp_path):
                 "--synthetic", "--synthetic_size", "2048", "--max_steps", "4", "--deterministic",
                 "--debug_sync", "--checkpoint_dir", str(tmp_path / "b")], cwd=str(tmp_path))
     assert "Saving.." in out, out[-2000:]
+
+
+def test_ddp_rccl_inside_hipgraph_matches_eager():
+    """The multi-GPU step path on a 1-rank RCCL clique: bucketed all-reduces issued from the
+    gradient-ready hooks on the comm stream, captured into the step's hipGraph together with the
+    backward, must leave parameters identical to the same steps without the data-parallel engine
+    (a world-1 average is the identity). This is the code the 8-GPU bench replays."""
+    from pytorch_cifar_amd import _native, models
+    from pytorch_cifar_amd.data.loader import DeviceLoader
+    from pytorch_cifar_amd.data.synthetic import synthetic_cifar10
+    from pytorch_cifar_amd.engine.arena import ParamArena
+    from pytorch_cifar_amd.engine.optim import SGD
+    from pytorch_cifar_amd.engine.trainer import TrainStep
+    from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_cifar_amd.parallel.launcher import DistContext
+
+    import pytorch_cifar_amd
+
+    C = _native.lib()
+    pytorch_cifar_amd.set_deterministic(True)   # bitwise-comparable weight gradients
+    comm = C.RcclComm(C.rccl_unique_id(), 1, 0, 0)
+    ctx = DistContext(rank=0, world=1, local_rank=0, device=torch.device("cuda", 0),
+                      backend="nccl", comm=comm)
+    imgs, labs = synthetic_cifar10(256, seed=5)
+    finals = []
+    for use_ddp in (False, True):
+        torch.manual_seed(0)
+        model = models.ResNet18().cuda()
+        arena = ParamArena(model.parameters())
+        opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4).attach_arena(arena)
+        net, ddp = model, None
+        if use_ddp:
+            ddp = DistributedDataParallel(model, ctx, bucket_cap_mb=4.0, arena=arena,
+                                          force_collectives=True)
+            net = ddp
+            assert len(ddp.buckets) > 2
+        loader = DeviceLoader(imgs, labs, 64, "cuda", crop_pad=4, flip=True, drop_last=True, seed=0)
+        step = TrainStep(net, opt, loader, 64, ddp=ddp, graph=True)
+        loader.set_epoch(0)
+        for idx in loader.batch_indices():
+            step(idx)
+        torch.cuda.synchronize()
+        assert step.graph is not None, f"graph capture failed: {step.graph_error!r}"
+        finals.append(arena.param_flat.detach().clone())
+    comm.destroy()
+    pytorch_cifar_amd.set_deterministic(False)
+    # same seeds -> same batches and augmentation draws; deterministic wgrad and a world-1 average
+    # (sum / 1) make the two runs bitwise comparable
+    torch.testing.assert_close(finals[1], finals[0], rtol=0, atol=0)
