@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
 #include <vector>
 
 typedef __bf16 bf16;
@@ -15,12 +16,26 @@ typedef __bf16 bf16;
 namespace pca {
 // conv_mfma.hip
 void conv_fwd_launch(const bf16*, const bf16*, const float*, bf16*, float*, int, int, int, int, int,
-                     int, int, int, int, int, int, int, hipStream_t);
+                     int, int, int, int, int, int, int, hipStream_t, float* ws);
+int64_t conv_fwd_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                           int pad, int groups, int Ho, int Wo, bool has_bias);
+int64_t conv_dgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                             int pad, int groups, int Ho, int Wo);
+bool conv_needs_tune(int kind, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                     int pad, int groups, int Ho, int Wo, bool has_bias);
+std::vector<std::pair<int, int>> conv_tune_candidates(int kind, int N, int H, int W, int Cin,
+                                                      int Cout, int KH, int KW, int stride,
+                                                      int pad, int groups, int Ho, int Wo);
+void conv_set_trial(int cfg, int split);
+void conv_record_tuned(int kind, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                       int stride, int pad, int groups, int Ho, int Wo, int cfg, int split);
+int conv_tuned_count();
+void conv_clear_tuned();
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
 void set_conv_tile(int kind, int idx);
 void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int, int, int, int,
-                       int, int, int, int, hipStream_t, const bf16* addend);
+                       int, int, int, int, hipStream_t, const bf16* addend, float* ws);
 void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
                        int Cin, int Cout, int KH, int KW, int stride, int pad, int groups, int Ho,
                        int Wo, hipStream_t st);
@@ -118,6 +133,61 @@ void check_f32(const Tensor& t, const char* name) {
 int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
 
 // ------------------------------------------------------------------------------ conv
+// Autotuning of the MFMA conv tile / split-K choice per geometry (cudnn.benchmark analogue,
+// reference main.py:75). On by default; PCA_CONV_AUTOTUNE=0 or conv_autotune(False) disables.
+static bool g_autotune = [] {
+  const char* e = std::getenv("PCA_CONV_AUTOTUNE");
+  return !(e && e[0] == '0');
+}();
+
+static bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &s) != hipSuccess) return true;   // be conservative
+  return s != hipStreamCaptureStatusNone;
+}
+
+// mean time (ms) of `reps` launches after one warm-up launch, HIP events on stream st
+template <class F>
+static float time_launches(F&& f, hipStream_t st, int reps) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  f();
+  hipEventRecord(a, st);
+  for (int i = 0; i < reps; ++i) f();
+  hipEventRecord(b, st);
+  hipEventSynchronize(b);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  return ms / reps;
+}
+
+// time every candidate (cfg, split) of a conv geometry and record the fastest. `run` launches
+// the conv once with the trial selection active, allocating its own scratch outputs.
+template <class F>
+static void autotune_conv(int kind, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                          int stride, int pad, int groups, int Ho, int Wo, F&& run) {
+  auto cands = pca::conv_tune_candidates(kind, N, H, W, Cin, Cout, KH, KW, stride, pad, groups,
+                                         Ho, Wo);
+  if (cands.empty()) return;
+  const hipStream_t st = cur_stream();
+  float best = 1e30f;
+  std::pair<int, int> pick = cands.front();
+  for (const auto& c : cands) {
+    pca::conv_set_trial(c.first, c.second);
+    const float t = time_launches(run, st, 3);
+    if (t < best) {
+      best = t;
+      pick = c;
+    }
+  }
+  pca::conv_set_trial(-1, -1);
+  pca::conv_record_tuned(kind, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo,
+                         pick.first, pick.second);
+}
+
 std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<Tensor>& bias,
                              int stride, int pad, int groups, bool want_stats) {
   check_bf16(x, "x");
@@ -131,6 +201,25 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
               "MFMA conv path needs Cin/G and Cout/G multiples of 8");
   const int Ho = out_dim(H, KH, stride, pad), Wo = out_dim(W, KW, stride, pad);
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
+  const bool has_bias0 = bias.has_value() && bias->defined();
+  if (g_autotune && !stream_capturing(cur_stream()) &&
+      pca::conv_needs_tune(0, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, has_bias0)) {
+    autotune_conv(0, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, [&] {
+      auto yt = at::empty({N, Ho, Wo, Cout}, x.options());
+      Tensor stt, wst;
+      if (want_stats) {
+        const int gm = pca::conv_fwd_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+        stt = at::empty({gm, 2, Cout}, x.options().dtype(at::kFloat));
+      }
+      const int64_t n = pca::conv_fwd_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups,
+                                                Ho, Wo, has_bias0);
+      if (n > 0) wst = at::empty({n}, x.options().dtype(at::kFloat));
+      pca::conv_fwd_launch(ptr<bf16>(x), ptr<bf16>(wb), optr<float>(bias), ptr<bf16>(yt),
+                           want_stats ? ptr<float>(stt) : nullptr, N, H, W, Cin, Cout, KH, KW,
+                           stride, pad, groups, Ho, Wo, cur_stream(),
+                           n > 0 ? ptr<float>(wst) : nullptr);
+    });
+  }
   auto y = at::empty({N, Ho, Wo, Cout}, x.options());
   Tensor stats;
   if (want_stats) {
@@ -141,9 +230,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
     check_f32(*bias, "bias");
     TORCH_CHECK(bias->numel() == Cout, "bias size");
   }
+  const bool has_bias = bias.has_value() && bias->defined();
+  const int64_t wsn = pca::conv_fwd_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho,
+                                              Wo, has_bias);
+  Tensor ws;
+  if (wsn > 0) ws = at::empty({wsn}, x.options().dtype(at::kFloat));
   pca::conv_fwd_launch(ptr<bf16>(x), ptr<bf16>(wb), optr<float>(bias), ptr<bf16>(y),
                        want_stats ? ptr<float>(stats) : nullptr, N, H, W, Cin, Cout, KH, KW,
-                       stride, pad, groups, Ho, Wo, cur_stream());
+                       stride, pad, groups, Ho, Wo, cur_stream(),
+                       wsn > 0 ? ptr<float>(ws) : nullptr);
   return {y, stats};
 }
 
@@ -157,15 +252,34 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, 
   TORCH_CHECK(Cog % 8 == 0 && (Cin / groups) % 8 == 0, "MFMA dgrad needs multiples of 8");
   TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo,
               "dgrad geometry mismatch");
-  auto dx = at::empty({N, H, W, Cin}, dy.options());
   const bf16* add = nullptr;
   if (addend.has_value() && addend->defined()) {
     check_bf16(*addend, "addend");
-    TORCH_CHECK(addend->numel() == dx.numel() && addend->is_contiguous(), "addend must match dx (NHWC)");
+    TORCH_CHECK(addend->numel() == (int64_t)N * H * W * Cin && addend->is_contiguous(),
+                "addend must match dx (NHWC)");
     add = ptr<bf16>(*addend);
   }
+  if (g_autotune && !stream_capturing(cur_stream()) &&
+      pca::conv_needs_tune(1, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, false)) {
+    autotune_conv(1, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, [&] {
+      auto dxt = at::empty({N, H, W, Cin}, dy.options());
+      Tensor wst;
+      const int64_t n = pca::conv_dgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups,
+                                                  Ho, Wo);
+      if (n > 0) wst = at::empty({n}, dy.options().dtype(at::kFloat));
+      pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dxt), N, H, W, Cin, Cout, KH,
+                             KW, stride, pad, groups, Ho, Wo, cur_stream(), add,
+                             n > 0 ? ptr<float>(wst) : nullptr);
+    });
+  }
+  auto dx = at::empty({N, H, W, Cin}, dy.options());
+  const int64_t wsn = pca::conv_dgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups,
+                                                Ho, Wo);
+  Tensor ws;
+  if (wsn > 0) ws = at::empty({wsn}, dy.options().dtype(at::kFloat));
   pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dx), N, H, W, Cin, Cout, KH, KW,
-                         stride, pad, groups, Ho, Wo, cur_stream(), add);
+                         stride, pad, groups, Ho, Wo, cur_stream(), add,
+                         wsn > 0 ? ptr<float>(ws) : nullptr);
   return dx;
 }
 
@@ -627,6 +741,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
+  m.def("conv_autotune_enabled", []() { return g_autotune; });
+  m.def("conv_tuned_count", &pca::conv_tuned_count);
+  m.def("conv_clear_tuned", &pca::conv_clear_tuned);
   m.def("set_conv_tile", &pca::set_conv_tile, "override tile config (kind 0: fwd/dgrad, 1: wgrad; -1 = heuristic)");
   m.def("weight_prep", &weight_prep);
   m.def("bn_stats", &bn_stats);

@@ -28,8 +28,12 @@
 #include "mfma_util.h"
 
 #include <algorithm>
+#include <map>
+#include <vector>
 
 namespace pca {
+
+bool deterministic_conv();   // conv_halo.hip
 
 struct ConvGeom {
   int N;                // batch
@@ -43,6 +47,9 @@ struct ConvGeom {
   int Ktot;             // KH*KW*Cr
   uint32_t a_bytes, b_bytes;
   FastDiv fd_hw, fd_w, fd_cr8, fd_kw, fd_s;
+  int ksplit;           // split-K factor (1 = off): grid.z = ksplit * groups * classes
+  float* ws;            // split-K fp32 partials [ksplit][N*Ho*Wo][Co]
+  int mode;             // 0 fwd, 1 dgrad, 2 parity dgrad (autotune cache key)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -52,7 +59,7 @@ struct ConvGeom {
 // into its 4 output parity classes (blockIdx.z = group*4 + class): class (ph, pw) only meets
 // the taps kh = (ph+pad)&1 (+2...), so no MFMA work is spent on the 3/4 of taps that a strided
 // transposed convolution would multiply by zero.
-template <int BM, int BN, int WM, int WN, int STAGES, int MODE, bool STATS>
+template <int BM, int BN, int WM, int WN, int STAGES, int MODE, bool STATS, bool SPLITK = false>
 __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __restrict__ A,
                                                                   const bf16* __restrict__ B,
                                                                   bf16* __restrict__ Y,
@@ -84,8 +91,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
   const int wm = wid / WN, wn = wid % WN;
   constexpr bool DGRAD = MODE != 0;
   constexpr bool PARITY = MODE == 2;
-  const int grp = PARITY ? (blockIdx.z >> 2) : blockIdx.z;
-  const int cls = PARITY ? (blockIdx.z & 3) : 0;
+  // split-K: blockIdx.z = split * (groups * classes) + (group, class)
+  const int gzb = g.groups * (PARITY ? 4 : 1);
+  const int zb = SPLITK ? (int)(blockIdx.z % gzb) : (int)blockIdx.z;
+  const int split = SPLITK ? (int)(blockIdx.z / gzb) : 0;
+  const int grp = PARITY ? (zb >> 2) : zb;
+  const int cls = PARITY ? (zb & 3) : 0;
   const int ph = cls >> 1, pw = cls & 1;
   // tap sets: kh = kh0 + tstep*t for t < nth (all taps unless PARITY)
   const int kh0 = PARITY ? ((ph + g.pad) & 1) : 0;
@@ -109,7 +120,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
   const int lrow = lane >> 3;
   const int lchunk = (lane & 7) ^ lrow;
   const int crg = g.Cr >> 3;
-  const int KT = cdiv(Kcls, BK);
+  const int KT_all = cdiv(Kcls, BK);
+  // this block's K-step range [kt_begin, KT)
+  const int kper = SPLITK ? cdiv(KT_all, g.ksplit) : KT_all;
+  const int kt_begin = SPLITK ? min(KT_all, split * kper) : 0;
+  const int KT = SPLITK ? min(KT_all, kt_begin + kper) : KT_all;
 
   // Fast path: every K-step lies inside ONE tap (Cr % 64 == 0) and the gathered pixel is
   // (row base + scalar tap offset) — true for the forward, the stride-1 dgrad and every parity
@@ -165,7 +180,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
     }
 
     // fast-path tap cursor (uniform): K-step kt = (tap, sub) with tap = (th, tw)
-    int cur_sub = 0, cur_th = 0, cur_tw = 0, cur_kt = 0;
+    int cur_sub = 0, cur_th = 0, cur_tw = 0, cur_kt = kt_begin;
+    if (SPLITK && fast && kt_begin > 0) {
+      const int tap0 = kt_begin / ksub;
+      cur_sub = kt_begin - tap0 * ksub;
+      cur_th = tap0 / ntw;
+      cur_tw = tap0 - cur_th * ntw;
+    }
 
     auto issue = [&](int kt, int buf) {
       char* As = smem + buf * STAGE;
@@ -205,7 +226,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         return;
       }
       const int kg = kt * 8 + lchunk;                  // 8-channel granule along K
-      const bool kok = kg * 8 < Kcls;
+      const bool kok = kg * 8 < Kcls && kt < KT;
       const int tap = kok ? (int)fdiv(kg, g.fd_cr8) : 0;
       const int c8 = kg - tap * crg;
       int kh, kw;
@@ -257,13 +278,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s) issue(s, s);
+    for (int s = 0; s < STAGES - 1; ++s) issue(kt_begin + s, s);
 
-    for (int kt = 0; kt < KT; ++kt) {
+    for (int kt = kt_begin; kt < KT; ++kt) {
+      const int rel = kt - kt_begin;
       wait_vmcnt<(STAGES - 2) * LPS>();
       raw_barrier();
-      issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);   // past-the-end stages load zeros
-      const char* As = smem + (kt % STAGES) * STAGE;
+      issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);   // past-the-end stages load zeros
+      const char* As = smem + (rel % STAGES) * STAGE;
       const char* Bs = As + A_BYTES;
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -290,6 +312,33 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
     }
     wait_vmcnt<0>();
     __syncthreads();
+
+    if constexpr (SPLITK) {
+      // fp32 partial tile straight from the accumulators (16 lanes = 64 contiguous bytes);
+      // bias / addend / BN statistics / bf16 conversion happen in splitk_reduce_kernel
+      float* wsp = g.ws + (size_t)split * g.N * g.Ho * g.Wo * g.Co;
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int gm = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + j;
+          if (gm >= Mrows) continue;
+          size_t pix = gm;
+          if constexpr (PARITY) {
+            const uint32_t n = fdiv(gm, g.fd_hw);
+            const uint32_t rem = gm - n * (rows_h * rows_w);
+            const uint32_t h = fdiv(rem, g.fd_w);
+            const uint32_t w = rem - h * rows_w;
+            pix = ((size_t)n * g.Ho + 2 * h + ph) * g.Wo + 2 * w + pw;
+          }
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni) {
+            const int c = n0 + wn * WTN + ni * 16 + (lane & 15);
+            if (c < g.Cn) wsp[pix * g.Co + (size_t)grp * g.Cn + c] = acc[mi][ni][j];
+          }
+        }
+      continue;   // no LDS reuse before the next tile's prologue: the ring was drained above
+    }
 
     // ---- epilogue: bias, BN partials, bf16 tile through LDS for 16-byte row stores ----
     if (bias) {
@@ -362,7 +411,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
     __syncthreads();   // the C tile aliases the ring the next tile's prologue refills
   }
 
-  if constexpr (STATS) {
+  if constexpr (STATS && !SPLITK) {
     float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
@@ -716,6 +765,82 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
 }
 
 // ---------------------------------------------------------------------------------------
+// split-K reduction: sum the fp32 partials in a fixed order (deterministic), add bias or the
+// fused dgrad addend, store bf16 and emit one BN-statistics slab row per block (the same slab
+// format the igemm epilogue writes, so bn_finalize is unchanged).
+// ---------------------------------------------------------------------------------------
+template <bool STATS>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S,
+                                                           int M, int Co, int rows_per_block,
+                                                           const float* __restrict__ bias,
+                                                           const bf16* __restrict__ addend,
+                                                           bf16* __restrict__ Y,
+                                                           float* __restrict__ stats) {
+  __shared__ float red[2 * 2048];
+  const int CG = Co >> 3;             // 8-channel groups per row (Co <= 2048: CG <= 256)
+  const int RP = 256 / CG;            // rows per pass
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, rr = tid / CG;
+  const bool active = rr < RP;
+  float sm[8], sq[8], b[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) sm[q] = sq[q] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) b[q] = bias ? bias[cg * 8 + q] : 0.f;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  const size_t plane = (size_t)M * Co;
+  if (active) {
+    for (int r = r0 + rr; r < r1; r += RP) {
+      const size_t o = (size_t)r * Co + cg * 8;
+      float a[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = b[q];
+      for (int k = 0; k < S; ++k) {
+        const float4 v0 = *reinterpret_cast<const float4*>(ws + k * plane + o);
+        const float4 v1 = *reinterpret_cast<const float4*>(ws + k * plane + o + 4);
+        a[0] += v0.x; a[1] += v0.y; a[2] += v0.z; a[3] += v0.w;
+        a[4] += v1.x; a[5] += v1.y; a[6] += v1.z; a[7] += v1.w;
+      }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          sm[q] += a[q];
+          sq[q] += a[q] * a[q];
+        }
+      }
+      if (addend) {
+        float d[8];
+        unpack8(*reinterpret_cast<const uint4*>(addend + o), d);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] += d[q];
+      }
+      *reinterpret_cast<uint4*>(Y + o) = pack8(a);
+    }
+  }
+  if constexpr (STATS) {
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        red[(rr * Co + cg * 8 + q) * 2 + 0] = sm[q];
+        red[(rr * Co + cg * 8 + q) * 2 + 1] = sq[q];
+      }
+    }
+    __syncthreads();
+    float* srow = stats + (size_t)blockIdx.x * 2 * Co;
+    for (int c = tid; c < Co; c += 256) {
+      float s0 = 0.f, q0 = 0.f;
+      for (int k = 0; k < RP; ++k) {
+        s0 += red[(k * Co + c) * 2 + 0];
+        q0 += red[(k * Co + c) * 2 + 1];
+      }
+      srow[c] = s0;
+      srow[Co + c] = q0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------
 static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co, int KH, int KW,
@@ -734,6 +859,9 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   g.fd_cr8 = make_fastdiv(Cr / 8);
   g.fd_kw = make_fastdiv(KW);
   g.fd_s = make_fastdiv(stride);
+  g.ksplit = 1;
+  g.ws = nullptr;
+  g.mode = 0;
   return g;
 }
 
@@ -778,15 +906,114 @@ static int igemm_rows(const ConvGeom& g) {
   return MODE == 2 ? g.N * (g.Ho / 2) * (g.Wo / 2) : g.M;
 }
 
+// process-wide overrides (set_conv_tile) used by tools/bench_conv.py sweeps and the tests
+static int g_igemm_override = -1;
+static int g_wgrad_override = -1;
+
+// ---- autotuning (the analogue of the reference's cudnn.benchmark = True, main.py:75) ----
+// The first eager call of each conv geometry times a candidate set of (tile config, split-K)
+// pairs with HIP events (bindings.cpp drives it, outside stream capture) and caches the
+// fastest; later calls and hipGraph captures use the cached choice.
+struct TuneKey {
+  int v[13];
+  bool operator<(const TuneKey& o) const { return std::lexicographical_compare(v, v + 13, o.v, o.v + 13); }
+};
+static std::map<TuneKey, std::pair<int, int>> g_tuned;   // key -> (cfg, split)
+static int g_trial_cfg = -1, g_trial_split = -1;
+
+static TuneKey tune_key(const ConvGeom& g) {
+  return TuneKey{{g.mode, g.N, g.Hs, g.Ws, g.Cs, g.Ho, g.Wo, g.Co, g.KH, g.KW, g.stride, g.pad,
+                  g.groups}};
+}
+
+static const std::pair<int, int>* tuned_choice(const ConvGeom& g) {
+  auto it = g_tuned.find(tune_key(g));
+  return it == g_tuned.end() ? nullptr : &it->second;
+}
+
+// Split-K (small-M layers: a per-GPU batch of 128 gives layer-4 M = 2048, i.e. 64 tiles of
+// 128x128 for 256 CUs). When the output tiles fill less than half the resident slots, the K
+// loop is split S ways (each split keeps >= 4 K-steps), partials go to an fp32 workspace and
+// splitk_reduce_kernel finishes the epilogue. set_conv_tile(2, S) forces S (sweeps).
+static int g_splitk_override = -1;
+constexpr int kMaxSplitCo = 2048;
+
+template <int MODE>
+static int igemm_ksteps(const ConvGeom& g) {
+  const int taps = MODE == 2 ? cdiv(g.KH, 2) * cdiv(g.KW, 2) : g.KH * g.KW;
+  return cdiv(taps * g.Cr, 64);
+}
+
+template <int BM, int BN, int WM, int WN, int ST, int MODE>
+static int igemm_ksplit_t(const ConvGeom& g) {
+  if (g.Co % 8 != 0 || g.Co > kMaxSplitCo) return 1;
+  const int KT = igemm_ksteps<MODE>(g);
+  if (g_splitk_override >= 1) return std::max(1, std::min(g_splitk_override, KT));
+  if (g_splitk_override == 0) return 1;
+  if (g_trial_split >= 1) return std::max(1, std::min(g_trial_split, KT));
+  if (g_igemm_override < 0 && g_trial_cfg < 0) {
+    if (const auto* t = tuned_choice(g)) return std::max(1, std::min(t->second, KT));
+  }
+  const int gzb = g.groups * (MODE == 2 ? 4 : 1);
+  const int tiles = cdiv(igemm_rows<MODE>(g), BM) * cdiv(g.Cn, BN) * gzb;
+  const int slots = igemm_occupancy<BM, BN, WM, WN, ST, MODE>() * num_cus();
+  // split only when the tiles leave most CUs idle: the fp32 partial round trip costs
+  // ~S*M*Co*8 bytes of HBM traffic (measured: a 2-way split of 128->128 @16x16, bs128, lost 45%)
+  if (2 * tiles > num_cus()) return 1;
+  const int S = std::min({slots / tiles, KT / 4, 8});
+  return S >= 2 ? S : 1;
+}
+
+static int splitk_reduce_grid(int M, int Co, int* rows_per_block) {
+  const int RP = 256 / (Co / 8);
+  int gx = std::min(cdiv(M, RP), 2 * num_cus());
+  const int rpb = cdiv(M, gx);
+  *rows_per_block = rpb;
+  return cdiv(M, rpb);
+}
+
 template <int BM, int BN, int WM, int WN, int ST, int MODE>
 static int igemm_grid_x_t(const ConvGeom& g) {
+  const int S = igemm_ksplit_t<BM, BN, WM, WN, ST, MODE>(g);
+  if (S > 1) {   // stats rows come from the reduce kernel
+    int rpb;
+    return splitk_reduce_grid(g.N * g.Ho * g.Wo, g.Co, &rpb);
+  }
   const int gyz = cdiv(g.Cn, BN) * g.groups * (MODE == 2 ? 4 : 1);
   return persistent_grid_x(cdiv(igemm_rows<MODE>(g), BM), gyz, igemm_occupancy<BM, BN, WM, WN, ST, MODE>());
 }
 
 template <int BM, int BN, int WM, int WN, int ST, int MODE>
+static int64_t igemm_ws_floats_t(const ConvGeom& g) {
+  const int S = igemm_ksplit_t<BM, BN, WM, WN, ST, MODE>(g);
+  return S > 1 ? (int64_t)S * g.N * g.Ho * g.Wo * g.Co : 0;
+}
+
+template <int BM, int BN, int WM, int WN, int ST, int MODE>
 static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, const float* bias,
-                         const ConvGeom& g, hipStream_t st, const bf16* addend = nullptr) {
+                         const ConvGeom& g0, hipStream_t st, const bf16* addend = nullptr,
+                         float* ws = nullptr) {
+  const int S = ws ? igemm_ksplit_t<BM, BN, WM, WN, ST, MODE>(g0) : 1;
+  if (S > 1) {
+    ConvGeom g = g0;
+    g.ksplit = S;
+    g.ws = ws;
+    const int gzb = g.groups * (MODE == 2 ? 4 : 1);
+    dim3 grid(cdiv(igemm_rows<MODE>(g), BM), cdiv(g.Cn, BN), gzb * S);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, ST, MODE, false, true>), grid,
+                       dim3(WM * WN * 64), 0, st, A, B, Y, nullptr, nullptr, nullptr, g);
+    const int M = g.N * g.Ho * g.Wo;
+    int rpb;
+    const int gx = splitk_reduce_grid(M, g.Co, &rpb);
+    if (stats)
+      hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
+                         rpb, bias, addend, Y, stats);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
+                         rpb, bias, addend, Y, stats);
+    return;
+  }
+  const ConvGeom& g = g0;
   dim3 grid(igemm_grid_x_t<BM, BN, WM, WN, ST, MODE>(g), cdiv(g.Cn, BN),
             g.groups * (MODE == 2 ? 4 : 1));
   if (stats)
@@ -799,16 +1026,17 @@ static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, co
 
 // Tile configurations. The heuristic picks by GEMM N (channels per group); a process-wide
 // override (set_conv_tile) lets tools/bench_conv.py sweep them on the GPU.
-static int g_igemm_override = -1;
-static int g_wgrad_override = -1;
 
 void set_conv_tile(int kind, int idx) {
   if (kind == 0) g_igemm_override = idx;
-  else g_wgrad_override = idx;
+  else if (kind == 1) g_wgrad_override = idx;
+  else g_splitk_override = idx;
 }
 
 static int igemm_select(const ConvGeom& g) {
   if (g_igemm_override >= 0) return g_igemm_override;
+  if (g_trial_cfg >= 0) return g_trial_cfg;
+  if (const auto* t = tuned_choice(g)) return t->first;
   // measured on MI355X (tools/bench_conv.py, profiles/conv_census_r1.md)
   if (g.Cn > 64) return 3;
   if (g.Cn > 32) return 4;
@@ -832,17 +1060,32 @@ static int igemm_select(const ConvGeom& g) {
   X(12, 256, 128, 4, 2, 2)           \
   X(13, 512, 64, 8, 1, 2)            \
   X(14, 128, 128, 2, 4, 3)           \
-  X(15, 128, 64, 4, 2, 4)
+  X(15, 128, 64, 4, 2, 4)            \
+  X(16, 64, 128, 1, 4, 3)            \
+  X(17, 64, 64, 2, 2, 3)             \
+  X(18, 64, 64, 1, 4, 4)
 
 template <int MODE>
 static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, const float* bias,
-                           const ConvGeom& g, hipStream_t st, const bf16* addend = nullptr) {
+                           const ConvGeom& g, hipStream_t st, const bf16* addend = nullptr,
+                           float* ws = nullptr) {
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
-    case C: launch_igemm<BM, BN, WM, WN, ST, MODE>(A, B, Y, stats, bias, g, st, addend); break;
+    case C: launch_igemm<BM, BN, WM, WN, ST, MODE>(A, B, Y, stats, bias, g, st, addend, ws); break;
     PCA_IGEMM_CFGS(PCA_CASE)
 #undef PCA_CASE
-    default: launch_igemm<128, 128, 2, 2, 2, MODE>(A, B, Y, stats, bias, g, st, addend); break;
+    default: launch_igemm<128, 128, 2, 2, 2, MODE>(A, B, Y, stats, bias, g, st, addend, ws); break;
+  }
+}
+
+template <int MODE>
+static int64_t igemm_ws_floats(const ConvGeom& g) {
+  switch (igemm_select(g)) {
+#define PCA_CASE(C, BM, BN, WM, WN, ST) \
+    case C: return igemm_ws_floats_t<BM, BN, WM, WN, ST, MODE>(g);
+    PCA_IGEMM_CFGS(PCA_CASE)
+#undef PCA_CASE
+    default: return igemm_ws_floats_t<128, 128, 2, 2, 2, MODE>(g);
   }
 }
 
@@ -865,6 +1108,107 @@ int conv_c64_stat_rows(int N, int H);
 void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const bf16* addend,
                      int N, int H, bool dgrad, hipStream_t st);
 
+// split-K workspace (floats) the forward / dgrad launch of this geometry will need (0 = none)
+int64_t conv_fwd_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                           int pad, int groups, int Ho, int Wo, bool has_bias) {
+  if (g_igemm_override < 0 && !has_bias &&
+      conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return 0;
+  ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
+                         Cout / groups);
+  return igemm_ws_floats<0>(g);
+}
+
+// geometry of a dgrad launch (mode 1 generic / 2 parity classes)
+static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                           int pad, int groups, int Ho, int Wo);
+
+static bool dgrad_parity(int H, int W, int stride, int Ho, int Wo) {
+  return stride == 2 && H % 2 == 0 && W % 2 == 0 && Ho == H / 2 && Wo == W / 2;
+}
+
+int64_t conv_dgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                             int pad, int groups, int Ho, int Wo) {
+  if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return 0;
+  const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  return g.mode == 2 ? igemm_ws_floats<2>(g) : igemm_ws_floats<1>(g);
+}
+
+static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                           int pad, int groups, int Ho, int Wo) {
+  ConvGeom g = make_geom(N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, groups, Cout / groups,
+                         Cin / groups);
+  g.mode = 1;
+  if (dgrad_parity(H, W, stride, Ho, Wo)) {
+    // parity-class decomposition: rows are one class's (H/2) x (W/2) pixels
+    g.mode = 2;
+    g.fd_hw = make_fastdiv((H / 2) * (W / 2));
+    g.fd_w = make_fastdiv(W / 2);
+  }
+  return g;
+}
+
+// ---- autotune API (bindings.cpp) ----
+// kind 0: forward, 1: dgrad. Returns false when the geometry is not autotunable (c64 path,
+// an explicit override is active) or is already tuned.
+static bool tunable(const ConvGeom& g, bool c64) {
+  return !c64 && g_igemm_override < 0 && g_splitk_override < 0 && !deterministic_conv() &&
+         !tuned_choice(g);
+}
+
+bool conv_needs_tune(int kind, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                     int pad, int groups, int Ho, int Wo, bool has_bias) {
+  const bool c64 = conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) &&
+                   !(kind == 0 && has_bias);
+  if (kind == 0) {
+    ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
+                           Cout / groups);
+    return tunable(g, c64);
+  }
+  return tunable(dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo), c64);
+}
+
+// candidate (cfg, split) list for a geometry: tile shapes from 64x64 to 128x128, split-K 1..8
+std::vector<std::pair<int, int>> conv_tune_candidates(int kind, int N, int H, int W, int Cin,
+                                                      int Cout, int KH, int KW, int stride,
+                                                      int pad, int groups, int Ho, int Wo) {
+  ConvGeom g = kind == 0 ? make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups,
+                                     Cin / groups, Cout / groups)
+                         : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  const int taps = g.mode == 2 ? cdiv(KH, 2) * cdiv(KW, 2) : KH * KW;
+  const int KT = cdiv(taps * g.Cr, 64);
+  const bool can_split = g.Co % 8 == 0 && g.Co <= kMaxSplitCo;
+  std::vector<std::pair<int, int>> c;
+  const int cfgs[] = {3, 0, 4, 1, 16, 17, 18};
+  for (int cfg : cfgs) {
+    if (cfg == 3 || cfg == 0 || cfg == 16) {
+      if (g.Cn <= 64) continue;          // 128-wide N tiles on <= 64 channels waste half
+    }
+    for (int sp : {1, 2, 4, 8}) {
+      if (sp > 1 && (!can_split || KT / sp < 2)) continue;
+      c.emplace_back(cfg, sp);
+    }
+  }
+  return c;
+}
+
+void conv_set_trial(int cfg, int split) {
+  g_trial_cfg = cfg;
+  g_trial_split = split;
+}
+
+void conv_record_tuned(int kind, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                       int stride, int pad, int groups, int Ho, int Wo, int cfg, int split) {
+  ConvGeom g = kind == 0 ? make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups,
+                                     Cin / groups, Cout / groups)
+                         : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  g_tuned[tune_key(g)] = {cfg, split};
+}
+
+int conv_tuned_count() { return (int)g_tuned.size(); }
+void conv_clear_tuned() { g_tuned.clear(); }
+
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo) {
   if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
@@ -876,7 +1220,7 @@ int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
 
 void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, float* stats, int N,
                      int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                     int groups, int Ho, int Wo, hipStream_t st) {
+                     int groups, int Ho, int Wo, hipStream_t st, float* ws) {
   if (g_igemm_override < 0 && bias == nullptr &&
       conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
     conv_c64_launch(x, w, y, stats, nullptr, N, H, false, st);
@@ -884,26 +1228,22 @@ void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, f
   }
   ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
                          Cout / groups);
-  igemm_dispatch<0>(x, w, y, stats, bias, g, st);
+  igemm_dispatch<0>(x, w, y, stats, bias, g, st, nullptr, ws);
 }
 
 // dx = conv^T(dy, W); wt is W transposed to [Cin][KH][KW][Cout/G].
 void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, int W, int Cin,
                        int Cout, int KH, int KW, int stride, int pad, int groups, int Ho, int Wo,
-                       hipStream_t st, const bf16* addend) {
+                       hipStream_t st, const bf16* addend, float* ws) {
   if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
     conv_c64_launch(dy, wt, dx, nullptr, addend, N, H, true, st);
     return;
   }
-  ConvGeom g = make_geom(N, Ho, Wo, Cout, H, W, Cin, KH, KW, stride, pad, groups, Cout / groups,
-                         Cin / groups);
-  if (stride == 2 && H % 2 == 0 && W % 2 == 0 && Ho == H / 2 && Wo == W / 2) {
-    // parity-class decomposition: rows are one class's (H/2) x (W/2) pixels
-    g.fd_hw = make_fastdiv((H / 2) * (W / 2));
-    g.fd_w = make_fastdiv(W / 2);
-    igemm_dispatch<2>(dy, wt, dx, nullptr, nullptr, g, st, addend);
+  const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  if (g.mode == 2) {
+    igemm_dispatch<2>(dy, wt, dx, nullptr, nullptr, g, st, addend, ws);
   } else {
-    igemm_dispatch<1>(dy, wt, dx, nullptr, nullptr, g, st, addend);
+    igemm_dispatch<1>(dy, wt, dx, nullptr, nullptr, g, st, addend, ws);
   }
 }
 

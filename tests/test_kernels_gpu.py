@@ -76,11 +76,15 @@ def test_conv_fwd_dgrad_wgrad(C, case):
     dy_n = nhwc(dy).to(torch.bfloat16)
     dx = C.conv_dgrad(dy_n, wt, H, H, s, p, G)
     assert rel_err(nchw(dx), x.grad) < 2e-2
+    # fused gradient hand-off: dX + addend in the epilogue (or the split-K reduce)
+    add = torch.randn_like(dx)
+    dx2 = C.conv_dgrad(dy_n, wt, H, H, s, p, G, add)
+    assert rel_err(nchw(dx2).float(), x.grad + nchw(add).float()) < 2e-2
     dw = C.conv_wgrad(x_n, dy_n, k, k, s, p, G, None)
     assert rel_err(dw.permute(0, 3, 1, 2), w.grad) < 2e-2
 
 
-N_IGEMM_CFGS = 16
+N_IGEMM_CFGS = 19
 
 
 @pytest.mark.parametrize("case", [(3, 64, 16, 64, 3, 1, 1, 1), (2, 128, 8, 256, 3, 2, 1, 1),
@@ -103,15 +107,18 @@ def test_conv_every_tile_config(C, case):
     bad = []
     try:
         for cfg in range(N_IGEMM_CFGS):
-            C.set_conv_tile(0, cfg)
-            y, stats = C.conv_fwd(x_n, wb, None, s, p, G, True)
-            dx = C.conv_dgrad(dy_n, wt, H, H, s, p, G)
-            e1, e2 = rel_err(nchw(y), ref), rel_err(nchw(dx), x.grad)
-            e3 = rel_err(stats[:, 0, :].sum(0), ref.detach().sum((0, 2, 3)))
-            if e1 > 2e-2 or e2 > 2e-2 or e3 > 1.2e-2:
-                bad.append((cfg, e1, e2, e3))
+            for split in (0, 3):   # 0: no split-K; 3: K loop split 3 ways + reduce kernel
+                C.set_conv_tile(0, cfg)
+                C.set_conv_tile(2, split)
+                y, stats = C.conv_fwd(x_n, wb, None, s, p, G, True)
+                dx = C.conv_dgrad(dy_n, wt, H, H, s, p, G)
+                e1, e2 = rel_err(nchw(y), ref), rel_err(nchw(dx), x.grad)
+                e3 = rel_err(stats[:, 0, :].sum(0), ref.detach().sum((0, 2, 3)))
+                if e1 > 2e-2 or e2 > 2e-2 or e3 > 1.2e-2:
+                    bad.append((cfg, split, e1, e2, e3))
     finally:
         C.set_conv_tile(0, -1)
+        C.set_conv_tile(2, -1)
     assert not bad, bad
 
 

@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--wcfgs", default="-1,0,3,4,5")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="")
+    ap.add_argument("--splits", default="-1", help="split-K overrides for fwd/dgrad (-1 heuristic, 0 off)")
     a = ap.parse_args()
     from pytorch_cifar_amd import _native
 
@@ -74,13 +75,18 @@ def main():
         yr = F.conv2d(xr, wr, stride=s, padding=p)
         err = ((y.permute(0, 3, 1, 2).float() - yr).abs().max() / yr.abs().max()).item()
         shape = f"{Cin}->{Cout} k{k}s{s} @{H}"
-        for cfg in [int(c) for c in a.cfgs.split(",")]:
-            C.set_conv_tile(0, cfg)
-            tf = timeit(lambda: C.conv_fwd(x, wb, None, s, p, 1, True), a.iters)
-            td = timeit(lambda: C.conv_dgrad(dy, wt, H, H, s, p, 1), a.iters) if Cin % 8 == 0 and Cin >= 16 else float("nan")
-            rows.append(dict(shape=shape, pass_="fwd", cfg=cfg, us=tf * 1e6, tflops=flops / tf / 1e12, err=err))
-            rows.append(dict(shape=shape, pass_="dgrad", cfg=cfg, us=td * 1e6, tflops=flops / td / 1e12))
+        n_ig = 0
+        for sp in [int(v) for v in a.splits.split(",")]:
+            C.set_conv_tile(2, sp)
+            for cfg in [int(c) for c in a.cfgs.split(",")]:
+                C.set_conv_tile(0, cfg)
+                tf = timeit(lambda: C.conv_fwd(x, wb, None, s, p, 1, True), a.iters)
+                td = timeit(lambda: C.conv_dgrad(dy, wt, H, H, s, p, 1), a.iters) if Cin % 8 == 0 and Cin >= 16 else float("nan")
+                rows.append(dict(shape=shape, pass_="fwd", cfg=cfg, split=sp, us=tf * 1e6, tflops=flops / tf / 1e12, err=err))
+                rows.append(dict(shape=shape, pass_="dgrad", cfg=cfg, split=sp, us=td * 1e6, tflops=flops / td / 1e12))
+                n_ig += 2
         C.set_conv_tile(0, -1)
+        C.set_conv_tile(2, -1)
         for cfg in [int(c) for c in a.wcfgs.split(",")]:
             C.set_conv_tile(1, cfg)
             tw = timeit(lambda: C.conv_wgrad(x, dy, k, k, s, p, 1, None), a.iters)
@@ -95,7 +101,7 @@ def main():
         tmb = timeit(lambda: torch.autograd.grad(out, (xm, wm), dym, retain_graph=True), a.iters)
         rows.append(dict(shape=shape, pass_="miopen_fwd", cfg=None, us=tmf * 1e6, tflops=flops / tmf / 1e12))
         rows.append(dict(shape=shape, pass_="miopen_bwd(d+w)", cfg=None, us=tmb * 1e6, tflops=2 * flops / tmb / 1e12))
-        for r in rows[-(2 * len(a.cfgs.split(",")) + len(a.wcfgs.split(",")) + 2):]:
+        for r in rows[-(n_ig + len(a.wcfgs.split(",")) + 2):]:
             print(json.dumps(r), flush=True)
     if a.out:
         with open(a.out, "w") as f:
