@@ -31,6 +31,16 @@ void conv_record_tuned(int kind, int N, int H, int W, int Cin, int Cout, int KH,
                        int stride, int pad, int groups, int Ho, int Wo, int cfg, int split);
 int conv_tuned_count();
 void conv_clear_tuned();
+bool wgrad_needs_tune(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                      int groups);
+std::vector<std::pair<int, int>> wgrad_tune_candidates(int N, int H, int W, int Cin, int Cout,
+                                                       int KH, int KW, int stride, int pad,
+                                                       int groups);
+void wgrad_set_trial(int cfg, int split);
+void wgrad_record_tuned(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                        int groups, int cfg, int split);
+int wgrad_tuned_count();
+void wgrad_clear_tuned();
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
 void set_conv_tile(int kind, int idx);
@@ -81,6 +91,8 @@ void act_fwd_launch(const bf16*, size_t, int, bf16*, hipStream_t);
 void act_bwd_launch(const bf16*, const bf16*, size_t, int, bf16*, hipStream_t);
 void add_act_launch(const bf16*, const bf16*, size_t, int, bf16*, hipStream_t);
 void weight_prep_launch(const float*, int, int, int, int, bf16*, bf16*, hipStream_t);
+void weight_prep_multi_launch(const int64_t* desc, const int64_t* chunks, int nchunks,
+                              hipStream_t st);
 // dwconv.hip
 void dw_fwd_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int, int, int,
                    bf16*, hipStream_t);
@@ -305,6 +317,31 @@ Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride,
   } else {
     dw = at::zeros({Cout, KH, KW, Cin / groups}, x.options().dtype(at::kFloat));
   }
+  if (g_autotune && !stream_capturing(cur_stream()) &&
+      pca::wgrad_needs_tune(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
+    // trials accumulate into a scratch gradient (never the real one)
+    auto dwt = at::empty({Cout, KH, KW, Cin / groups}, x.options().dtype(at::kFloat));
+    auto cands = pca::wgrad_tune_candidates(N, H, W, Cin, Cout, KH, KW, stride, pad, groups);
+    float best = 1e30f;
+    std::pair<int, int> pick = cands.front();
+    for (const auto& c : cands) {
+      pca::wgrad_set_trial(c.first, c.second);
+      const int64_t n = pca::conv_wgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+      Tensor wst;
+      if (n > 0) wst = at::empty({n}, x.options().dtype(at::kFloat));
+      const float t = time_launches([&] {
+        pca::conv_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), ptr<float>(dwt),
+                               n > 0 ? ptr<float>(wst) : nullptr, N, H, W, Cin, Cout, KH, KW,
+                               stride, pad, groups, Ho, Wo, cur_stream());
+      }, cur_stream(), 3);
+      if (t < best) {
+        best = t;
+        pick = c;
+      }
+    }
+    pca::wgrad_set_trial(-1, -1);
+    pca::wgrad_record_tuned(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, pick.first, pick.second);
+  }
   // slab workspace of the wide kernel (partial tiles, reduced into dw in a fixed order)
   const int64_t wsn = pca::conv_wgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   Tensor ws;
@@ -324,6 +361,16 @@ std::vector<Tensor> weight_prep(const Tensor& w, int groups, bool want_t) {
   pca::weight_prep_launch(ptr<float>(w), groups, Cout / groups, KH * KW, Cg, ptr<bf16>(wb),
                           want_t ? ptr<bf16>(wt) : nullptr, cur_stream());
   return {wb, wt};
+}
+
+// batched weight_prep over a descriptor table (see misc.hip weight_prep_multi_kernel)
+void weight_prep_multi(const Tensor& desc, const Tensor& chunks) {
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.dim() == 2 &&
+                  desc.size(1) == 8, "desc must be a [n,8] int64 GPU tensor");
+  TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == at::kLong && chunks.dim() == 2 &&
+                  chunks.size(1) == 4, "chunks must be a [m,4] int64 GPU tensor");
+  pca::weight_prep_multi_launch(desc.data_ptr<int64_t>(), chunks.data_ptr<int64_t>(),
+                                (int)chunks.size(0), cur_stream());
 }
 
 // ------------------------------------------------------------------------------- BN
@@ -743,10 +790,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
   m.def("conv_autotune_enabled", []() { return g_autotune; });
-  m.def("conv_tuned_count", &pca::conv_tuned_count);
-  m.def("conv_clear_tuned", &pca::conv_clear_tuned);
+  m.def("conv_trial", [](int kind, int cfg, int split) {
+    if (kind == 0) pca::conv_set_trial(cfg, split);
+    else pca::wgrad_set_trial(cfg, split);
+  }, "force an autotune candidate (kind 0 fwd/dgrad, 1 wgrad); (-1, -1) clears");
+  m.def("wgrad_candidates", &pca::wgrad_tune_candidates);
+  m.def("igemm_candidates", &pca::conv_tune_candidates);
+  m.def("conv_tuned_count", []() { return pca::conv_tuned_count() + pca::wgrad_tuned_count(); });
+  m.def("conv_clear_tuned", []() {
+    pca::conv_clear_tuned();
+    pca::wgrad_clear_tuned();
+  });
   m.def("set_conv_tile", &pca::set_conv_tile, "override tile config (kind 0: fwd/dgrad, 1: wgrad; -1 = heuristic)");
   m.def("weight_prep", &weight_prep);
+  m.def("weight_prep_multi", &weight_prep_multi);
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply);

@@ -34,6 +34,8 @@
 namespace pca {
 
 bool deterministic_conv();   // conv_halo.hip
+int wgrad_split_force();     // conv_halo.hip
+void set_wgrad_split(int splits);
 
 struct ConvGeom {
   int N;                // batch
@@ -909,6 +911,7 @@ static int igemm_rows(const ConvGeom& g) {
 // process-wide overrides (set_conv_tile) used by tools/bench_conv.py sweeps and the tests
 static int g_igemm_override = -1;
 static int g_wgrad_override = -1;
+static int g_weff_cfg = -1;    // wgrad config resolved by wgrad_resolve() for the current geometry
 
 // ---- autotuning (the analogue of the reference's cudnn.benchmark = True, main.py:75) ----
 // The first eager call of each conv geometry times a candidate set of (tile config, split-K)
@@ -1153,7 +1156,8 @@ static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int K
 // kind 0: forward, 1: dgrad. Returns false when the geometry is not autotunable (c64 path,
 // an explicit override is active) or is already tuned.
 static bool tunable(const ConvGeom& g, bool c64) {
-  return !c64 && g_igemm_override < 0 && g_splitk_override < 0 && !deterministic_conv() &&
+  return !c64 && g_igemm_override < 0 && g_splitk_override < 0 && g_trial_cfg < 0 &&
+         !deterministic_conv() &&
          !tuned_choice(g);
 }
 
@@ -1259,6 +1263,7 @@ static int64_t splitk_plan(WgradGeom& g, int target_blocks) {
   int splits = cdiv(target_blocks, tiles);
   const int min_chunk = 512;
   splits = std::max(1, std::min(splits, cdiv(g.P, min_chunk)));
+  if (wgrad_split_force() >= 1) splits = std::min(wgrad_split_force(), std::max(1, cdiv(g.P, 64)));
   int chunk = cdiv(g.P, splits);
   chunk = cdiv(chunk, 64) * 64;
   splits = cdiv(g.P, chunk);
@@ -1316,7 +1321,7 @@ static WgradGeom wgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int 
 
 static int wgrad_select(const WgradGeom& g) {
   const bool wide_ok = g.cin_g % 64 == 0 && g.cout_g % 64 == 0;
-  int cfg = g_wgrad_override >= 32 ? -1 : g_wgrad_override;
+  int cfg = g_weff_cfg >= 32 ? -1 : g_weff_cfg;
   if (cfg >= 16 && !wide_ok) cfg = -1;
   if (cfg < 0) {
     // measured (tools/bench_conv.py): the wide kernel only pays with all 9 taps in a tile and
@@ -1334,12 +1339,14 @@ static int64_t wide_plan(WgradGeom& g) {
   const int slots = wide_occupancy<MB, NB, WM, WN>() * num_cus();
   int splits = std::max(1, slots / tiles);
   splits = std::min(splits, std::max(1, cdiv(g.P, 256)));
+  const int forced = wgrad_split_force();
+  if (forced >= 1) splits = std::min(forced, std::max(1, cdiv(g.P, 32)));
   int chunk = cdiv(cdiv(g.P, splits), 32) * 32;
   splits = cdiv(g.P, chunk);
   g.chunk = chunk;
   g.splits = splits;
   // few partials per output: atomics; many: slab rows + one ordered reduce
-  g.atomic = (!deterministic_conv() && splits <= 8) ? 1 : 0;
+  g.atomic = (!deterministic_conv() && (splits <= 8 || forced >= 1)) ? 1 : 0;
   return g.atomic ? 0 : slab_ws_floats(splits, (int64_t)g.groups * g.cout_g * g.Ktot);
 }
 
@@ -1362,13 +1369,41 @@ void wgrad_halo_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int 
                        int Cin, int Cout, int groups, hipStream_t st);
 void set_halo_cfg(int cfg);
 
-static bool use_halo() { return g_wgrad_override < 0 || g_wgrad_override >= 32; }
+// wgrad autotuning: (cfg, split) per geometry; cfg >= 32 = halo config cfg-32, 16..21 = wide,
+// 0..7 = generic split-K; split -1 = occupancy-derived plan
+static std::map<TuneKey, std::pair<int, int>> g_wtuned;
+static int g_wtrial_cfg = -1, g_wtrial_split = -1;
+
+static TuneKey wgrad_key(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                         int pad, int groups) {
+  return TuneKey{{10, N, H, W, Cin, 0, 0, Cout, KH, KW, stride, pad, groups}};
+}
+
+static void wgrad_resolve(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                          int pad, int groups) {
+  int cfg = g_wgrad_override, split = -1;
+  if (cfg < 0 && g_wtrial_cfg >= 0) {
+    cfg = g_wtrial_cfg;
+    split = g_wtrial_split;
+  } else if (cfg < 0) {
+    auto it = g_wtuned.find(wgrad_key(N, H, W, Cin, Cout, KH, KW, stride, pad, groups));
+    if (it != g_wtuned.end() && !deterministic_conv()) {
+      cfg = it->second.first;
+      split = it->second.second;
+    }
+  }
+  g_weff_cfg = cfg;
+  set_wgrad_split(split);
+}
+
+static bool use_halo() { return g_weff_cfg < 0 || g_weff_cfg >= 32; }
 
 // workspace (floats) conv_wgrad_launch will need for this geometry under the current selection
 int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                              int pad, int groups, int Ho, int Wo) {
+  wgrad_resolve(N, H, W, Cin, Cout, KH, KW, stride, pad, groups);
   if (use_halo()) {
-    set_halo_cfg(g_wgrad_override >= 32 ? g_wgrad_override - 32 : -1);
+    set_halo_cfg(g_weff_cfg >= 32 ? g_weff_cfg - 32 : -1);
     const int64_t h = wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups);
     if (h >= 0) return h;
   }
@@ -1391,8 +1426,9 @@ int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int
 void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
                        int Cin, int Cout, int KH, int KW, int stride, int pad, int groups, int Ho,
                        int Wo, hipStream_t st) {
+  wgrad_resolve(N, H, W, Cin, Cout, KH, KW, stride, pad, groups);
   if (use_halo()) {
-    set_halo_cfg(g_wgrad_override >= 32 ? g_wgrad_override - 32 : -1);
+    set_halo_cfg(g_weff_cfg >= 32 ? g_weff_cfg - 32 : -1);
     if (wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) >= 0) {
       wgrad_halo_launch(x, dy, dw, ws, N, H, W, Cin, Cout, groups, st);
       return;
@@ -1416,5 +1452,44 @@ void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int 
     default: launch_wgrad<128, 128, 2, 2, 3>(x, dy, dw, ws, g, st, target); break;
   }
 }
+
+// ---- wgrad autotune API (bindings.cpp) ----
+bool wgrad_needs_tune(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                      int groups) {
+  if (g_wgrad_override >= 0 || g_wtrial_cfg >= 0 || deterministic_conv()) return false;
+  return g_wtuned.find(wgrad_key(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) == g_wtuned.end();
+}
+
+std::vector<std::pair<int, int>> wgrad_tune_candidates(int N, int H, int W, int Cin, int Cout,
+                                                       int KH, int KW, int stride, int pad,
+                                                       int groups) {
+  std::vector<int> cfgs;
+  const bool halo = wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) >= 0;
+  if (halo) cfgs.insert(cfgs.end(), {32, 33, 34});
+  const int cin_g = Cin / groups, cout_g = Cout / groups;
+  if (cin_g % 64 == 0 && cout_g % 64 == 0) cfgs.insert(cfgs.end(), {16, 17, 18, 19, 20, 21});
+  cfgs.insert(cfgs.end(), {0, 1, 2, 3, 6, 7});
+  const int64_t P = (int64_t)N * ((H + 2 * pad - KH) / stride + 1) * ((W + 2 * pad - KW) / stride + 1);
+  std::vector<std::pair<int, int>> c;
+  for (int cfg : cfgs)
+    for (int sp : {-1, 1, 2, 4, 8, 16, 32}) {
+      if (sp > 1 && P / sp < 256) continue;
+      c.emplace_back(cfg, sp);
+    }
+  return c;
+}
+
+void wgrad_set_trial(int cfg, int split) {
+  g_wtrial_cfg = cfg;
+  g_wtrial_split = split;
+}
+
+void wgrad_record_tuned(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                        int groups, int cfg, int split) {
+  g_wtuned[wgrad_key(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)] = {cfg, split};
+}
+
+int wgrad_tuned_count() { return (int)g_wtuned.size(); }
+void wgrad_clear_tuned() { g_wtuned.clear(); }
 
 }  // namespace pca

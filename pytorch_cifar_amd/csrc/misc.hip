@@ -421,7 +421,63 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, int G, int Cn, i
   }
 }
 
+// Multi-tensor weight preparation: one launch converts every MFMA conv weight of a model
+// (fp32 master [G*Cn][T][Cr], physical channels_last order) into its bf16 forward operand (same
+// layout) and its bf16 transposed dgrad operand [G*Cr][T][Cn]. desc[t] = {w, wb, wt, G, Cn, T,
+// Cr, numel}; chunks[b] = {t, a, b, pass}:
+//   pass 0: elements [a, b) of the forward layout, 8 per thread (16-byte stores);
+//   pass 1: 64x64 (co, ci) transpose tile number a of one (group, tap), staged through LDS so
+//           both the fp32 reads (along ci) and the bf16 writes (along co) are coalesced.
+// All index math is 32-bit and per block / per 8 elements (64-bit div/mod per element made the
+// first version of this kernel 10x slower than its bandwidth).
+__global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* __restrict__ desc,
+                                                                const int64_t* __restrict__ chunks) {
+  __shared__ float tile[64][65];
+  const int64_t* ch = chunks + (size_t)blockIdx.x * 4;
+  const int64_t* d = desc + ch[0] * 8;
+  const float* w = reinterpret_cast<const float*>(d[0]);
+  const int Cn = (int)d[4], T = (int)d[5], Cr = (int)d[6];
+  const int tid = threadIdx.x;
+  if (ch[3] == 0) {
+    bf16* wb = reinterpret_cast<bf16*>(d[1]);
+    const int s0 = (int)ch[1], s1 = (int)ch[2];
+    for (int i = s0 + tid * 8; i < s1; i += 256 * 8) {
+      const float4 v0 = *reinterpret_cast<const float4*>(w + i);
+      const float4 v1 = *reinterpret_cast<const float4*>(w + i + 4);
+      const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      *reinterpret_cast<uint4*>(wb + i) = pack8(f);
+    }
+    return;
+  }
+  bf16* wt = reinterpret_cast<bf16*>(d[2]);
+  const int nco = (Cn + 63) >> 6, nci = (Cr + 63) >> 6;
+  int q = (int)ch[1];
+  const int ci_t = q % nci;
+  q /= nci;
+  const int co_t = q % nco;
+  q /= nco;
+  const int tap = q % T;
+  const int g = q / T;
+  const int co0 = co_t * 64, ci0 = ci_t * 64;
+  for (int k = tid; k < 64 * 64; k += 256) {
+    const int r = k >> 6, c = k & 63;               // r: co, c: ci (contiguous in w)
+    const int co = co0 + r, ci = ci0 + c;
+    tile[r][c] = (co < Cn && ci < Cr) ? w[((g * Cn + co) * T + tap) * Cr + ci] : 0.f;
+  }
+  __syncthreads();
+  for (int k = tid; k < 64 * 64; k += 256) {
+    const int r = k >> 6, c = k & 63;               // r: ci, c: co (contiguous in wt)
+    const int ci = ci0 + r, co = co0 + c;
+    if (ci < Cr && co < Cn) wt[((g * Cr + ci) * T + tap) * Cn + co] = f2bf(tile[c][r]);
+  }
+}
+
 // ================================================================================ host
+void weight_prep_multi_launch(const int64_t* desc, const int64_t* chunks, int nchunks,
+                              hipStream_t st) {
+  if (nchunks > 0)
+    hipLaunchKernelGGL(weight_prep_multi_kernel, dim3(nchunks), dim3(256), 0, st, desc, chunks);
+}
 void nchw_to_nhwc_launch(const float* x, int N, int C, int HW, int Cp, bf16* y, hipStream_t st) {
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_cap((size_t)N * HW * Cp)), dim3(256), 0, st, x,
                      N, C, HW, Cp, y);

@@ -4,7 +4,8 @@ What main_dist.py runs per step (SGD 0.9/5e-4, CE, autocast) with the library ke
 ships for ROCm (MIOpen convolutions/BN, hipBLASLt linear, RCCL DDP), in the best stock
 configuration: channels_last + bf16 autocast, synthetic batches already on the GPU. Used by
 ``bench.py --baseline`` to put our number next to the stock one measured on the same box.
-The network is built from torch.nn layers with the CIFAR ResNet topology of models/resnet.py.
+ResNet-18 is built from torch.nn layers with the CIFAR ResNet topology of models/resnet.py; any
+other zoo model runs our model code with every op routed to stock torch (``reference_kernels``).
 """
 from __future__ import annotations
 
@@ -41,15 +42,26 @@ def stock_resnet18(num_classes=10):
 
 
 def build_stock_step(model_name, per_rank_batch, device, ctx, images, labels):
-    if model_name != "ResNet18":
-        raise ValueError("stock comparator implements ResNet18 only")
     torch.manual_seed(0)
-    net = stock_resnet18().to(device).to(memory_format=torch.channels_last)
+    ref_ctx = None
+    if model_name == "ResNet18":
+        net = stock_resnet18()
+    else:
+        # any other zoo model: our model code run entirely through stock torch ops
+        # (F.conv2d / F.batch_norm / ... = MIOpen / hipBLASLt), i.e. the reference's op sequence
+        from .. import models
+        from ..ops.functional import reference_kernels
+
+        net = models.build_model(model_name)
+        ref_ctx = reference_kernels
+    net = net.to(device).to(memory_format=torch.channels_last)
     model = net
     if ctx.world > 1:
         model = nn.parallel.DistributedDataParallel(net, device_ids=[device.index])
     opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4)
-    torch.backends.cudnn.benchmark = True
+    # MIOpen exhaustive find per shape (cudnn.benchmark) takes minutes on the mobile zoo's many
+    # depthwise shapes; it is used for ResNet-18 (the reference sets it, main.py:75)
+    torch.backends.cudnn.benchmark = model_name == "ResNet18"
     mean = torch.tensor((0.4914, 0.4822, 0.4465), device=device).view(1, 3, 1, 1)
     std = torch.tensor((0.2023, 0.1994, 0.2010), device=device).view(1, 3, 1, 1)
     imgs = torch.from_numpy(images).to(device)
@@ -65,10 +77,17 @@ def build_stock_step(model_name, per_rank_batch, device, ctx, images, labels):
         x = ((x - mean) / std).contiguous(memory_format=torch.channels_last)
         y = labs.index_select(0, idx)
         opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = model(x)
-            loss = F.cross_entropy(out, y)
-        loss.backward()
+        if ref_ctx is not None:
+            with ref_ctx(), torch.autocast("cuda", dtype=torch.bfloat16):
+                out = model(x)
+                loss = F.cross_entropy(out.float(), y)
+            with ref_ctx():
+                loss.backward()
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = model(x)
+                loss = F.cross_entropy(out, y)
+            loss.backward()
         opt.step()
 
     return run, {"comparator": "torch.nn + MIOpen + autocast bf16 + channels_last"}

@@ -13,6 +13,7 @@ so one capture serves the whole run.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -31,6 +32,11 @@ class TrainStep:
         self.opt = optimizer
         self.loader = loader
         self.B = batch_size
+        inner = getattr(net, "module", net)
+        if loader.device.type == "cuda" and os.environ.get("PCA_BATCHED_WPREP", "1") != "0":
+            from ..ops.functional import enable_batched_weight_prep
+
+            enable_batched_weight_prep(inner)
         self.ddp = ddp
         self.device = loader.device
         self.metrics = metrics if metrics is not None else torch.zeros(3, dtype=torch.float64, device=self.device)

@@ -151,6 +151,156 @@ def _slot_for_residual(x):
     return getattr(x, "_pca_slot", None)
 
 
+# ------------------------------------------------------------- concurrent weight gradients
+# dW of a conv depends only on (x, dY); the rest of the backward chain depends on dX only. The
+# weight-gradient kernels therefore run on a second HIP stream, concurrently with the dgrad /
+# BatchNorm-backward chain of the layers below: at a per-GPU batch of 128 (the 8-GPU
+# strong-scaling shard) no single backward kernel fills the 256 CUs, so two independent kernel
+# streams recover the idle CUs. Ordering: the side stream waits for the main stream when a dW
+# is issued; a callback at the end of the backward pass joins it back into the main stream
+# (before the optimizer, and inside hipGraph capture); the data-parallel engine's bucket
+# launches also wait on it (parallel/ddp.py).
+# Measured on MI355X (ResNet-18, hipGraph step): the per-conv cross-stream dependencies cost more
+# than the overlap recovers (bs128 2.28 -> 2.40 ms, bs1024 7.30 -> 7.50 ms), so the side stream
+# is opt-in: PCA_WGRAD_STREAM=1.
+_WGRAD_STREAM = os.environ.get("PCA_WGRAD_STREAM", "0") == "1"
+_side = {}          # device index -> torch.cuda.Stream
+_join_pending = {"on": False}
+
+
+def wgrad_stream(device):
+    """The side stream carrying weight-gradient kernels on ``device`` (None when disabled)."""
+    if not _WGRAD_STREAM:
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _side.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _side[idx] = s
+    return s
+
+
+def _join_side_streams():
+    _join_pending["on"] = False
+    cur = torch.cuda.current_stream()
+    for s in _side.values():
+        if s.device == cur.device:
+            cur.wait_stream(s)
+
+
+def _schedule_join():
+    if not _join_pending["on"]:
+        _join_pending["on"] = True
+        torch.autograd.Variable._execution_engine.queue_callback(_join_side_streams)
+
+
+def join_wgrad_streams():
+    """Make the current stream wait for all outstanding side-stream weight gradients."""
+    if _side:
+        _join_side_streams()
+
+
+# ------------------------------------------------------------------ batched weight prep
+# Each MFMA conv consumes a bf16 copy of its fp32 master weight (plus a transposed copy for
+# dgrad). Converting them per conv costs one small launch per layer per step; a WeightPrepPlan
+# attached to the model converts ALL of them in one multi-tensor launch from a forward
+# pre-hook, into persistent buffers (stable addresses for hipGraph replay). The conversion runs
+# every forward from the current masters, so it can never serve a stale weight.
+_PLAN = {"cur": None}
+_PREP_CHUNK = 4096
+
+
+class _PrepEntry:
+    __slots__ = ("w", "groups", "wb", "wt")
+
+    def __init__(self, w, groups, wb, wt):
+        self.w, self.groups, self.wb, self.wt = w, groups, wb, wt
+
+
+class WeightPrepPlan:
+    def __init__(self):
+        self.entries = []
+        self.by_id = {}
+        self.tables = None
+        self.owner = None
+
+    def lookup(self, w, groups):
+        e = self.by_id.get(id(w))
+        if e is not None and e.w is w and e.groups == groups and e.wb.device == w.device:
+            return e
+        if e is not None:   # stale (deep copy / device move): rebuild the plan
+            self.entries, self.by_id, self.tables = [], {}, None
+        return None
+
+    def register(self, w, groups, w_phys):
+        wb, wt = _C().weight_prep(w_phys, groups, True)
+        e = _PrepEntry(w, groups, wb, wt)
+        self.entries.append(e)
+        self.by_id[id(w)] = e
+        self.tables = None
+        return e
+
+    def _build(self):
+        desc, chunks = [], []
+        for t, e in enumerate(self.entries):
+            wp = G.physical(e.w)
+            Cout, KH, KW, Cg = wp.shape
+            n = wp.numel()
+            desc.append([wp.data_ptr(), e.wb.data_ptr(), e.wt.data_ptr(), e.groups,
+                         Cout // e.groups, KH * KW, Cg, n])
+            chunks += [[t, s0, min(n, s0 + _PREP_CHUNK), 0] for s0 in range(0, n, _PREP_CHUNK)]
+            cn, cr = Cout // e.groups, Cg
+            tiles = e.groups * KH * KW * ((cn + 63) // 64) * ((cr + 63) // 64)
+            chunks += [[t, k, 0, 1] for k in range(tiles)]
+        dev = self.entries[0].wb.device
+        self.tables = (torch.tensor(desc, dtype=torch.int64).to(dev),
+                       torch.tensor(chunks, dtype=torch.int64).to(dev),
+                       tuple(G.physical(e.w).data_ptr() for e in self.entries))
+
+    def run(self):
+        if not self.entries:
+            return
+        if self.tables is None or self.tables[2] != tuple(G.physical(e.w).data_ptr() for e in self.entries):
+            self._build()
+        _C().weight_prep_multi(self.tables[0], self.tables[1])
+
+
+def _plan_pre_hook(module, args):
+    plan = module.__dict__.get("_pca_wplan")
+    # replicas made by torch DataParallel share __dict__ entries: only the owner runs the plan
+    if plan is not None and plan.owner == id(module) and not _FORCE_REFERENCE and \
+            next(iter(module.parameters())).is_cuda:
+        plan.run()
+        _PLAN["cur"] = plan
+
+
+def _plan_post_hook(module, args, out):
+    _PLAN["cur"] = None
+
+
+def enable_batched_weight_prep(model):
+    """Attach a WeightPrepPlan to ``model`` (idempotent). Returns the model."""
+    if "_pca_wplan" not in model.__dict__:
+        plan = WeightPrepPlan()
+        plan.owner = id(model)
+        model.__dict__["_pca_wplan"] = plan
+        model.register_forward_pre_hook(_plan_pre_hook)
+        model.register_forward_hook(_plan_post_hook)
+    return model
+
+
+def _prepped_weight(weight, groups, w_phys, need_dx):
+    """(wb, wt) for an MFMA conv: from the active plan when there is one, else converted now."""
+    plan = _PLAN["cur"]
+    if plan is not None and weight.is_leaf and weight.dim() == 4 and \
+            weight.permute(0, 2, 3, 1).is_contiguous():
+        e = plan.lookup(weight, groups)
+        if e is None:
+            e = plan.register(weight, groups, w_phys)
+        return e.wb, e.wt
+    return _C().weight_prep(w_phys, groups, need_dx)
+
+
 class _ConvMFMA(torch.autograd.Function):
     """Implicit-GEMM MFMA conv (fwd + BN-stat epilogue, dgrad, split-K wgrad)."""
 
@@ -165,7 +315,10 @@ class _ConvMFMA(torch.autograd.Function):
         if cin_pad:
             w_phys = F.pad(w_phys, (0, cin_pad - w_phys.shape[-1]))
         need_dx = ctx.needs_input_grad[0]
-        wb, wt = C.weight_prep(w_phys, groups, need_dx)
+        if cin_pad:
+            wb, wt = C.weight_prep(w_phys, groups, need_dx)
+        else:
+            wb, wt = _prepped_weight(weight, groups, w_phys, need_dx)
         y, stats = C.conv_fwd(x, wb, bias, stride, padding, groups, want_stats)
         ctx.geom = (stride, padding, groups, cin_pad, x.shape[1], x.shape[2])
         ctx.save_for_backward(x, wt if need_dx else None)
@@ -174,10 +327,15 @@ class _ConvMFMA(torch.autograd.Function):
         if stats is None or not want_stats:
             stats = torch.empty(0, device=x.device)
         ctx.mark_non_differentiable(stats)
+        # no zero-filled gradient for the (non-differentiable) statistics output: autograd
+        # would otherwise launch one fill kernel per conv per step
+        ctx.set_materialize_grads(False)
         return y, stats
 
     @staticmethod
     def backward(ctx, dy, _dstats):
+        if dy is None:
+            return (None,) * 10
         C = _C()
         x, wt = ctx.saved_tensors
         stride, padding, groups, cin_pad, H, W = ctx.geom
@@ -197,7 +355,16 @@ class _ConvMFMA(torch.autograd.Function):
         dw_ret = db_ret = None
         if weight.requires_grad:
             buf = None if (cin_pad or not weight.is_leaf) else G.grad_buffer(weight)
-            if buf is not None:
+            side = wgrad_stream(x.device) if buf is not None else None
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, buf)
+                x.record_stream(side)
+                dy.record_stream(side)
+                _schedule_join()
+                G.fire(weight)
+            elif buf is not None:
                 C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, buf)
                 G.fire(weight)
             else:

@@ -33,6 +33,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..engine import grads as G
+from ..ops import functional as F
 from ..engine.arena import BufferArena, ParamArena
 
 
@@ -136,6 +137,10 @@ class DistributedDataParallel(nn.Module):
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
             self.comm_stream.wait_event(ev)
+            # weight gradients may still be in flight on the side stream (ops/functional.py)
+            side = F.wgrad_stream(self.comm_stream.device)
+            if side is not None:
+                self.comm_stream.wait_stream(side)
 
     def _join(self):
         if self.comm_stream is not None:

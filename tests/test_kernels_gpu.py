@@ -122,6 +122,34 @@ def test_conv_every_tile_config(C, case):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("case", [(2, 64, 16, 64, 3, 1, 1, 1), (3, 128, 8, 256, 3, 2, 1, 1),
+                                  (2, 64, 16, 128, 1, 2, 0, 1), (2, 128, 8, 128, 3, 1, 1, 2)])
+def test_wgrad_autotune_candidates(C, case):
+    """Every (config, forced split-K) candidate the wgrad autotuner may pick is numerically right."""
+    N, Cin, H, Cout, k, s, p, G = case
+    torch.manual_seed(2)
+    x = bf(torch.randn(N, Cin, H, H, device="cuda"))
+    w = bf(torch.randn(Cout, Cin // G, k, k, device="cuda") * 0.05).requires_grad_(True)
+    ref = F.conv2d(x, w, stride=s, padding=p, groups=G)
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    x_n = nhwc(x).to(torch.bfloat16)
+    dy_n = nhwc(dy).to(torch.bfloat16)
+    cands = C.wgrad_candidates(N, H, H, Cin, Cout, k, k, s, p, G)
+    assert len(cands) > 6
+    bad = []
+    try:
+        for cfg, split in cands:
+            C.conv_trial(1, cfg, split)
+            dw = C.conv_wgrad(x_n, dy_n, k, k, s, p, G, None)
+            e = rel_err(dw.permute(0, 3, 1, 2), w.grad)
+            if e > 2e-2:
+                bad.append((cfg, split, e))
+    finally:
+        C.conv_trial(1, -1, -1)
+    assert not bad, bad
+
+
 WGRAD_CFGS = list(range(8)) + list(range(16, 22)) + [32, 33, 34]
 
 

@@ -132,3 +132,38 @@ def test_zoo_matches_reference(name):
         return m
 
     compare_model(ctor, batch=16)
+
+
+def test_batched_weight_prep_matches_per_conv():
+    """The one-launch weight conversion (forward pre-hook) produces the same forward/backward as
+    per-conv conversion, and follows in-place weight updates (it re-converts every forward)."""
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.engine.arena import ParamArena
+    from pytorch_cifar_amd.ops.functional import cross_entropy, enable_batched_weight_prep
+
+    torch.manual_seed(0)
+    a = models.ResNet18().cuda()
+    b = copy.deepcopy(a)
+    ParamArena(a.parameters())
+    ParamArena(b.parameters())
+    enable_batched_weight_prep(b)
+    x = torch.randn(16, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (16,), device="cuda")
+    for it in range(2):
+        outs = []
+        for m in (a, b):
+            for p in m.parameters():
+                p.grad.zero_()
+            out = m(x)
+            cross_entropy(out, y).backward()
+            outs.append(out.float())
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), it
+        ga = dict(a.named_parameters())
+        for n, p in b.named_parameters():
+            torch.testing.assert_close(p.grad, ga[n].grad, rtol=1e-2, atol=1e-4)
+        with torch.no_grad():   # an in-place update that does not go through the optimizer
+            for m in (a, b):
+                m.conv1.weight.mul_(0.5)
+                m.layer2[0].conv1.weight.add_(0.01)
+    assert len(b.__dict__["_pca_wplan"].entries) >= 19
