@@ -33,7 +33,10 @@ def parse():
     ap.add_argument("--model", default="ResNet18")
     ap.add_argument("--batch", type=int, default=1024, help="global batch")
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (1/0)")
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    # 4 MiB buckets (not DDP's 25): on xGMI the all-reduce of a bucket only overlaps backward if
+    # the bucket closes early; with 25 MiB, ResNet-18's last bucket holds ~18 MiB that can only
+    # start after the stem's wgrad, fully exposed. 4 MiB keeps the exposed tail to layers 1-2.
+    ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--baseline", action="store_true",
                     help="run the stock PyTorch-ROCm comparator step instead (MIOpen/hipBLASLt, autocast bf16)")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -82,7 +85,8 @@ def main():
         meta.update(step.info())
     if rank == 0:
         out = {
-            "metric": "images/sec (whole node) ResNet-18 bs=1024 at 1/2/4/8 MI355X",
+            "metric": ("images/sec (whole node) ResNet-18 bs=1024 at 1/2/4/8 MI355X" if args.model == "ResNet18"
+                       else f"images/sec (whole node) {args.model} bs={args.batch}"),
             "value": round(img_s, 1),
             "unit": "images/sec",
             "n_gpus": world,

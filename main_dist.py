@@ -59,7 +59,8 @@ parser.add_argument('--synthetic_size', default=None, type=int)
 parser.add_argument('--seed', default=0, type=int)
 parser.add_argument('--graph', default=1, type=int)
 parser.add_argument('--max_steps', default=None, type=int)
-parser.add_argument('--bucket_mb', default=25.0, type=float)
+parser.add_argument('--bucket_mb', default=4.0, type=float,
+                    help='gradient all-reduce bucket size (MiB); small buckets overlap backward on xGMI')
 parser.add_argument('--log_every', default=20, type=int)
 parser.add_argument('--no_broadcast_buffers', action='store_true')
 parser.add_argument('--cpu', action='store_true', help='gloo/CPU ranks (tests)')
