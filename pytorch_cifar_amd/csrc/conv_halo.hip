@@ -249,40 +249,44 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
         const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + j;
         if (m < g.cout_g) {
           const size_t idx = ((size_t)grp * g.cout_g + m) * g.Ktot + col;
-          if (g.atomic) atomicAdd(dst + idx, acc[mi][ni][j]);
-          else dst[idx] = acc[mi][ni][j];
+          if (g.atomic) {
+            if (g.splits == 1) dst[idx] += acc[mi][ni][j];   // sole writer
+            else atomicAdd(dst + idx, acc[mi][ni][j]);
+          } else {
+            dst[idx] = acc[mi][ni][j];
+          }
         }
       }
     }
 }
 
-// Slab reduction in a fixed order: stage 1 sums groups of <= 16 slab rows into part[g];
-// stage 2 adds the parts (in order) into dW.
-__global__ __launch_bounds__(256) void slab_partial_kernel(const float4* __restrict__ slab,
-                                                           float4* __restrict__ part, int splits,
-                                                           int per, int64_t n4) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n4) return;
-  const int s0 = blockIdx.y * per, s1 = min(splits, s0 + per);
+// Slab reduction in a fixed order, one kernel: a block owns 64 float4 columns; its 4 thread
+// lanes per column sum the slab rows s = l, l+4, ... and the 4 lane partials are added in lane
+// order (deterministic) before dW += sum.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float4* __restrict__ slab,
+                                                          float4* __restrict__ dw, int splits,
+                                                          int64_t n4) {
+  __shared__ float4 red[4][64];
+  const int c = threadIdx.x & 63, l = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + c;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = s0; s < s1; ++s) {
-    const float4 v = slab[(int64_t)s * n4 + i];
-    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  if (i < n4) {
+    for (int sidx = l; sidx < splits; sidx += 4) {
+      const float4 v = slab[(int64_t)sidx * n4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
   }
-  part[(int64_t)blockIdx.y * n4 + i] = a;
-}
-
-__global__ __launch_bounds__(256) void slab_final_kernel(const float4* __restrict__ part,
-                                                         float4* __restrict__ dw, int nparts,
-                                                         int64_t n4) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n4) return;
-  float4 a = dw[i];
-  for (int s = 0; s < nparts; ++s) {
-    const float4 v = part[(int64_t)s * n4 + i];
-    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  red[l][c] = a;
+  __syncthreads();
+  if (l == 0 && i < n4) {
+    float4 o = dw[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = red[k][c];
+      o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+    }
+    dw[i] = o;
   }
-  dw[i] = a;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -329,21 +333,15 @@ static int g_wsplit = -1;
 void set_wgrad_split(int splits) { g_wsplit = splits; }
 int wgrad_split_force() { return g_deterministic ? -1 : g_wsplit; }
 
-// dW[i] += sum_s slab[s][i] over `splits` rows of n floats (two-level, fixed order); the
-// workspace must hold splits*n + cdiv(splits,16)*n floats.
+// dW[i] += sum_s slab[s][i] over `splits` rows of n floats (fixed order); the workspace must
+// hold slab_ws_floats(splits, n) floats.
 void slab_reduce_launch(float* ws, float* dw, int splits, int64_t n, hipStream_t st) {
   const int64_t n4 = n / 4;
-  const int per = 16, nparts = cdiv(splits, per);
-  float* part = ws + (int64_t)splits * n;
-  const unsigned gx = (unsigned)cdiv64(n4, 256);
-  hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, nparts), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(part), splits,
-                     per, n4);
-  hipLaunchKernelGGL(slab_final_kernel, dim3(gx), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(part), reinterpret_cast<float4*>(dw), nparts, n4);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv64(n4, 64)), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(dw), splits, n4);
 }
 
-int64_t slab_ws_floats(int splits, int64_t n) { return (int64_t)splits * n + (int64_t)cdiv(splits, 16) * n; }
+int64_t slab_ws_floats(int splits, int64_t n) { return (int64_t)splits * n; }
 
 // Is the halo kernel applicable? 3x3 s1 p1, 64-channel blocks, whole rows (or images) per stage.
 static bool halo_geom(HaloGeom& g, int N, int H, int W, int Cin, int Cout, int groups) {

@@ -581,8 +581,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const bf16* __restrict_
         const int n = n0 + wn * WTN + ni * 16 + (lane & 15);
         if (m < g.cout_g && n < g.Ktot) {
           const size_t idx = ((size_t)grp * g.cout_g + m) * g.Ktot + n;
-          if (g.atomic) atomicAdd(DW + idx, acc[mi][ni][j]);
-          else DW[(size_t)split * g.groups * g.cout_g * g.Ktot + idx] = acc[mi][ni][j];
+          if (g.atomic) {
+            if (g.splits == 1) DW[idx] += acc[mi][ni][j];   // sole writer: plain read-modify-write
+            else atomicAdd(DW + idx, acc[mi][ni][j]);
+          } else {
+            DW[(size_t)split * g.groups * g.cout_g * g.Ktot + idx] = acc[mi][ni][j];
+          }
         }
       }
 }
@@ -745,8 +749,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_wide_kernel(const bf1
         const int n = n0 + wn * WTN + ni * 16 + (lane & 15);
         if (m < g.cout_g && n < g.Ktot) {
           const size_t idx = ((size_t)grp * g.cout_g + m) * g.Ktot + n;
-          if (g.atomic) atomicAdd(slab + idx, acc[mi][ni][j]);
-          else out[idx] = acc[mi][ni][j];
+          if (g.atomic) {
+            if (g.splits == 1) slab[idx] += acc[mi][ni][j];
+            else atomicAdd(slab + idx, acc[mi][ni][j]);
+          } else {
+            out[idx] = acc[mi][ni][j];
+          }
         }
       }
 }

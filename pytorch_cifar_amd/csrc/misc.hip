@@ -315,6 +315,35 @@ __global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) {
   float* b = a.bufs[t];
   bf16* sh = a.shadows ? a.shadows[t] : nullptr;
   const float lr = a.lr[0];
+  if (((s | e) & 3) == 0 && !sh && g && ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                                          reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
+    // float4 path: 16-byte loads/stores of param, grad and momentum (the whole arena)
+    float4* p4 = reinterpret_cast<float4*>(p);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    float4* b4 = reinterpret_cast<float4*>(b);
+    for (int64_t i = s / 4 + threadIdx.x; i < e / 4; i += 256) {
+      const float4 gv = g4[i], pv = p4[i];
+      float pf[4] = {pv.x, pv.y, pv.z, pv.w}, gf[4] = {gv.x, gv.y, gv.z, gv.w}, bf[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.momentum != 0.f && !a.first) {
+        const float4 bv = b4[i];
+        bf[0] = bv.x; bf[1] = bv.y; bf[2] = bv.z; bf[3] = bv.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float d = gf[k] * a.grad_scale;
+        if (a.wd != 0.f) d += a.wd * pf[k];
+        if (a.momentum != 0.f) {
+          const float bv = a.first ? d : a.momentum * bf[k] + (1.f - a.dampening) * d;
+          bf[k] = bv;
+          d = a.nesterov ? d + a.momentum * bv : bv;
+        }
+        pf[k] -= lr * d;
+      }
+      if (a.momentum != 0.f) b4[i] = make_float4(bf[0], bf[1], bf[2], bf[3]);
+      p4[i] = make_float4(pf[0], pf[1], pf[2], pf[3]);
+    }
+    return;
+  }
   for (int64_t i = s + threadIdx.x; i < e; i += 256) {
     float d = g ? g[i] * a.grad_scale : 0.f;
     const float pv = p[i];
