@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <map>
+#include <type_traits>
 #include <vector>
 
 namespace pca {
@@ -207,13 +208,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         const int b_delta = ((kh * g.KW + kw) * g.Cr + cur_sub * BK) * 2;
 #pragma unroll
         for (int i = 0; i < A_PW; ++i) {
-          const bool ok = kok && (uint32_t)(f_h[i] + dh) < (uint32_t)g.Hs &&
-                          (uint32_t)(f_w[i] + dw) < (uint32_t)g.Ws;
+          const bool ok = kok & ((uint32_t)(f_h[i] + dh) < (uint32_t)g.Hs) &
+                          ((uint32_t)(f_w[i] + dw) < (uint32_t)g.Ws);
           dma16(rsA, As + (wid * A_PW + i) * 1024, ok ? (uint32_t)(f_off[i] + a_delta) : kOOB);
         }
 #pragma unroll
         for (int i = 0; i < B_PW; ++i) {
-          const bool ok = kok && b_off[i] >= 0;
+          const bool ok = kok & (b_off[i] >= 0);
           dma16(rsB, Bs + (wid * B_PW + i) * 1024, ok ? (uint32_t)(b_off[i] + b_delta) : kOOB);
         }
         // advance the cursor
@@ -289,27 +290,33 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);   // past-the-end stages load zeros
       const char* As = smem + (rel % STAGES) * STAGE;
       const char* Bs = As + A_BYTES;
-      __builtin_amdgcn_s_setprio(1);
+      // all fragments of the K-step are read up front into distinct registers (the compiler
+      // otherwise sinks each A read next to its MFMAs and waits lgkmcnt(0) per fragment);
+      // the waits then retire them in issue order while the MFMAs run
+      bf16x8 af[BK / 32][TM], bfv[BK / 32][TN];
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
-        bf16x8 af[TM], bfv[TN];
         const int gsel = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int mi = 0; mi < TM; ++mi) {
-          const int r = wm * WTM + mi * 16 + (lane & 15);
-          af[mi] = *reinterpret_cast<const bf16x8*>(As + r * RB + ((gsel ^ (r & 7)) << 4));
-        }
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) {
           const int r = wn * WTN + ni * 16 + (lane & 15);
-          bfv[ni] = *reinterpret_cast<const bf16x8*>(Bs + r * RB + ((gsel ^ (r & 7)) << 4));
+          bfv[kk][ni] = *reinterpret_cast<const bf16x8*>(Bs + r * RB + ((gsel ^ (r & 7)) << 4));
         }
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          const int r = wm * WTM + mi * 16 + (lane & 15);
+          af[kk][mi] = *reinterpret_cast<const bf16x8*>(As + r * RB + ((gsel ^ (r & 7)) << 4));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk)
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
           for (int ni = 0; ni < TN; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfv[ni], acc[mi][ni], 0, 0, 0);
-      }
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][mi], bfv[kk][ni], acc[mi][ni], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
     wait_vmcnt<0>();
@@ -436,6 +443,350 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         s += red[(w * BN + tid) * 2 + 0];
         q += red[(w * BN + tid) * 2 + 1];
       }
+      const int c = n0 + tid;
+      if (c < g.Cn) {
+        float* srow = stats + (size_t)blockIdx.x * 2 * g.Co;
+        srow[grp * g.Cn + c] = s;
+        srow[g.Co + grp * g.Cn + c] = q;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// phased 256-row implicit GEMM (large-M forward and stride-1 dgrad), after the structure of
+// cdna_hip_programming.md §5 "The 256² 8-phase template": 8 waves (2 M x 4 N, 512 threads),
+// BK = 64, two LDS K-tile buffers, 4 phases per K-tile. Each phase = {counted vmcnt (never 0 in
+// the loop), one raw barrier, LDS-DMA of one quarter ("part") of the NEXT K-tile, this phase's
+// fragment reads, the MFMAs of one quadrant of the wave's 128 x BN/4 output}. Parts are staged in
+// the order they are first read (A rows of M-quadrant 0, B rows of N-quadrant 0, B N-quadrant 1,
+// A M-quadrant 1), so every part is read >= 2 phases after it was issued and loads stay in
+// flight across barriers; the structure the 2-stage kernel above lacks (it waits vmcnt(0) +
+// barrier once per K-step, which caps it near ~0.9 PF/s, §5 'The step-3 structure').
+// Fast path only: Cr % 64 == 0 (every K-step inside one tap), forward or stride-1 dgrad.
+// ---------------------------------------------------------------------------------------
+template <int BN, int WAVES, int MODE, bool STATS>
+__global__ __launch_bounds__(WAVES * 64) void conv_igemm_ph_kernel(const bf16* __restrict__ A,
+                                                            const bf16* __restrict__ B,
+                                                            bf16* __restrict__ Y,
+                                                            float* __restrict__ stats,
+                                                            const float* __restrict__ bias,
+                                                            const bf16* __restrict__ addend,
+                                                            const ConvGeom g) {
+  static_assert(MODE == 0 || MODE == 1, "forward or stride-1 dgrad");
+  constexpr int BM = 256, BK = 64, RB = 128;
+  constexpr int NT = WAVES * 64;
+  constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB, BUF = A_BYTES + B_BYTES;
+  constexpr int WAVES_N = WAVES / 2;  // waves are 2 (M) x WAVES_N (N); each owns 128 x WTN
+  constexpr int WTN = BN / WAVES_N;
+  constexpr int TN = WTN / 16;        // N-fragments per wave
+  constexpr int QN = TN / 2;          // N-fragments per N-quadrant
+  constexpr int GA = 16 / WAVES;      // DMA instructions per wave for an A part (128 rows)
+  constexpr int GB = BN / 16 / WAVES; // ... for a B part (BN/2 rows)
+  static_assert(BN == 128 || BN == 256, "BN");
+  static_assert(WAVES == 4 || WAVES == 8, "waves");
+  static_assert(GB >= 1 && QN >= 1, "tile");
+  static_assert(BM * BN * 2 <= 2 * BUF, "C tile must fit the LDS ring");
+  constexpr bool DGRAD = MODE != 0;
+
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WAVES_N, wn = wid % WAVES_N;
+  const int grp = blockIdx.z;
+  const int n0 = blockIdx.y * BN;
+  const int Mrows = g.M;
+  const int mtiles = cdiv(Mrows, BM);
+  const int kfull = g.KH * g.KW * g.Cr;
+  const int ksub = g.Cr / BK;
+  const int KT = g.KH * g.KW * ksub;
+
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A, g.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(B, g.b_bytes);
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;   // swizzle on the DMA source (rows are 8-aligned)
+
+  // A DMA slots: q (M-quadrant) x i (instruction): 8-row group j = 2*wid + i of the quadrant
+  // covers rows (j >> 3) * 128 + q * 64 + (j & 7) * 8 + [0, 8)
+  auto a_row0 = [&](int q, int i) {
+    const int j = GA * wid + i;
+    return (j >> 3) * 128 + q * 64 + (j & 7) * 8;
+  };
+  // B DMA slots: q (N-quadrant) x i: group j = GB*wid + i, wn' = j / (BN/64), k = j % (BN/64)
+  auto b_row0 = [&](int q, int i) {
+    const int j = GB * wid + i;
+    return (j / TN) * WTN + q * (WTN / 2) + (j % TN) * 8;
+  };
+
+  int b_off[2][GB];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int br = n0 + b_row0(q, i) + lrow;
+      b_off[q][i] = br < g.Cn ? ((grp * g.Cn + br) * kfull + lchunk * 8) * 2 : -1;
+    }
+
+  float st_s[TN], st_q[TN];
+#pragma unroll
+  for (int ni = 0; ni < TN; ++ni) st_s[ni] = st_q[ni] = 0.f;
+
+  for (int tile = blockIdx.x; tile < mtiles; tile += gridDim.x) {
+    const int m0 = tile * BM;
+    int f_h[2][GA], f_w[2][GA], f_off[2][GA];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const int r = m0 + a_row0(q, i) + lrow;
+        const uint32_t rr = r < Mrows ? r : 0;
+        const uint32_t n = fdiv(rr, g.fd_hw);
+        const uint32_t rem = rr - n * (g.Ho * g.Wo);
+        const uint32_t h = fdiv(rem, g.fd_w);
+        const uint32_t w = rem - h * g.Wo;
+        int bh, bw;
+        if constexpr (!DGRAD) {
+          bh = (int)h * g.stride - g.pad;
+          bw = (int)w * g.stride - g.pad;
+        } else {
+          bh = (int)h + g.pad;
+          bw = (int)w + g.pad;
+        }
+        f_off[q][i] = ((((int)n * g.Hs + bh) * g.Ws + bw) * g.Cs + grp * g.Cr + lchunk * 8) * 2;
+        if (r >= Mrows) bh = -(1 << 20);
+        f_h[q][i] = bh;
+        f_w[q][i] = bw;
+      }
+
+    // staging cursor: K-tile kt = (tap (th, tw), sub)
+    int s_kt = 0, s_sub = 0, s_th = 0, s_tw = 0;
+    int a_delta = 0, b_delta = 0, s_dh = 0, s_dw = 0;
+    bool s_ok = false;
+    auto cursor = [&]() {   // deltas of the K-tile at the cursor
+      s_ok = s_kt < KT;
+      if constexpr (!DGRAD) {
+        s_dh = s_th;
+        s_dw = s_tw;
+      } else {
+        s_dh = -s_th;
+        s_dw = -s_tw;
+      }
+      a_delta = ((s_dh * g.Ws + s_dw) * g.Cs + s_sub * BK) * 2;
+      b_delta = ((s_th * g.KW + s_tw) * g.Cr + s_sub * BK) * 2;
+    };
+    auto advance = [&]() {
+      ++s_kt;
+      if (++s_sub == ksub) {
+        s_sub = 0;
+        if (++s_tw == g.KW) {
+          s_tw = 0;
+          ++s_th;
+        }
+      }
+      cursor();
+    };
+    // part p of the cursor's K-tile into buffer `buf`: 0 = A quadrant 0, 1 = B quadrant 0,
+    // 2 = B quadrant 1, 3 = A quadrant 1
+    // (compile-time part / quadrant indices: std::integral_constant arguments, so every
+    // accumulator index is a constant after inlining and acc stays in registers)
+    auto stage = [&](auto pc, int buf) {
+      constexpr int p = decltype(pc)::value;
+      char* As = smem + buf * BUF;
+      char* Bs = As + A_BYTES;
+      if constexpr (p == 0 || p == 3) {
+        constexpr int q = p == 0 ? 0 : 1;
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+          // bitwise, not short-circuit: && becomes exec-mask branches around each DMA
+          const bool ok = s_ok & ((uint32_t)(f_h[q][i] + s_dh) < (uint32_t)g.Hs) &
+                          ((uint32_t)(f_w[q][i] + s_dw) < (uint32_t)g.Ws);
+          dma16(rsA, As + a_row0(q, i) * RB, ok ? (uint32_t)(f_off[q][i] + a_delta) : kOOB);
+        }
+      } else {
+        constexpr int q = p - 1;
+#pragma unroll
+        for (int i = 0; i < GB; ++i) {
+          const bool ok = s_ok & (b_off[q][i] >= 0);
+          dma16(rsB, Bs + b_row0(q, i) * RB, ok ? (uint32_t)(b_off[q][i] + b_delta) : kOOB);
+        }
+      }
+    };
+
+    f32x4 acc[8][TN];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // prologue: K-tile 0 -> buffer 0, parts in read order
+    cursor();
+    stage(std::integral_constant<int, 0>{}, 0);
+    stage(std::integral_constant<int, 1>{}, 0);
+    stage(std::integral_constant<int, 2>{}, 0);
+    stage(std::integral_constant<int, 3>{}, 0);
+    advance();
+
+    bf16x8 fa[2][4], fb[2][QN];
+    // fragment rows are (multiple of 16) + (lane & 15), so their swizzle (row & 7) is lane & 7:
+    // one per-lane base per operand and kk, everything else is an immediate offset
+    const int a_lane = (wm * 128 + (lane & 15)) * RB;
+    const int b_lane = (wn * WTN + (lane & 15)) * RB;
+    const int swz0 = ((0 + (lane >> 4)) ^ (lane & 7)) << 4;
+    const int swz1 = ((4 + (lane >> 4)) ^ (lane & 7)) << 4;
+    auto read_a = [&](const char* As, auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const char* p0 = As + a_lane + swz0 + q * 64 * RB;
+      const char* p1 = As + a_lane + swz1 + q * 64 * RB;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        fa[0][mi] = *reinterpret_cast<const bf16x8*>(p0 + mi * 16 * RB);
+        fa[1][mi] = *reinterpret_cast<const bf16x8*>(p1 + mi * 16 * RB);
+      }
+    };
+    auto read_b = [&](const char* Bs, auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const char* p0 = Bs + b_lane + swz0 + q * (WTN / 2) * RB;
+      const char* p1 = Bs + b_lane + swz1 + q * (WTN / 2) * RB;
+#pragma unroll
+      for (int ni = 0; ni < QN; ++ni) {
+        fb[0][ni] = *reinterpret_cast<const bf16x8*>(p0 + ni * 16 * RB);
+        fb[1][ni] = *reinterpret_cast<const bf16x8*>(p1 + ni * 16 * RB);
+      }
+    };
+    auto mma = [&](auto qmc, auto qnc) {
+      constexpr int qm = decltype(qmc)::value, qn = decltype(qnc)::value;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < QN; ++ni)
+            acc[qm * 4 + mi][qn * QN + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fa[kk][mi], fb[kk][ni], acc[qm * 4 + mi][qn * QN + ni], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    for (int kt = 0; kt < KT; ++kt) {
+      const int cur = kt & 1, nxt = cur ^ 1;
+      const char* As = smem + cur * BUF;
+      const char* Bs = As + A_BYTES;
+      // phase 0: needs parts 0, 1 of kt (parts 2, 3 may stay in flight)
+      wait_vmcnt<GB + GA>();
+      raw_barrier();
+      stage(I0{}, nxt);
+      read_a(As, I0{});
+      read_b(Bs, I0{});
+      mma(I0{}, I0{});
+      // phase 1: needs part 2 of kt (part 3 of kt, part 0 of kt+1 in flight)
+      wait_vmcnt<2 * GA>();
+      raw_barrier();
+      stage(I1{}, nxt);
+      read_b(Bs, I1{});
+      mma(I0{}, I1{});
+      // phase 2: needs part 3 of kt (parts 0, 1 of kt+1 in flight)
+      wait_vmcnt<GA + GB>();
+      raw_barrier();
+      stage(I2{}, nxt);
+      read_a(As, I1{});
+      mma(I1{}, I1{});
+      // phase 3: A quadrant 1 stays in registers, B quadrant 0 is re-read (landed since phase 0;
+      // its buffer is not restaged before the next K-tile's phase 1, after two barriers)
+      stage(I3{}, nxt);
+      advance();
+      read_b(Bs, I0{});
+      mma(I1{}, I0{});
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+
+    // ---- epilogue: bias, BN partials, bf16 tile through LDS (XOR-swizzled 16-B chunks) ----
+    if (bias) {
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int c = n0 + wn * WTN + ni * 16 + (lane & 15);
+        const float bv = c < g.Cn ? bias[grp * g.Cn + c] : 0.f;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = m0 + wm * 128 + mi * 16 + (lane >> 4) * 4 + j;
+            if (r < Mrows) acc[mi][ni][j] += bv;
+          }
+      }
+    }
+    if constexpr (STATS) {
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float v = acc[mi][ni][j];   // rows past M are exact zeros (zero-filled A)
+            st_s[ni] += v;
+            st_q[ni] += v * v;
+          }
+    }
+    constexpr int CRB = BN * 2;   // bytes per staged C row
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = wm * 128 + mi * 16 + (lane >> 4) * 4 + j;
+          const int c = wn * WTN + ni * 16 + (lane & 15);
+          *reinterpret_cast<bf16*>(smem + r * CRB + ((((c >> 3) ^ (r & 7))) << 4) + (c & 7) * 2) =
+              f2bf(acc[mi][ni][j]);
+        }
+    __syncthreads();
+    constexpr int CG = BN / 8;
+#pragma unroll
+    for (int it = 0; it < (BM * CG) / NT; ++it) {
+      const int idx = tid + it * NT;
+      const int r = idx / CG, c8 = idx % CG;
+      const int gm = m0 + r, gc = n0 + c8 * 8;
+      if (gm < Mrows && gc < g.Cn) {
+        uint4 v = *reinterpret_cast<const uint4*>(smem + r * CRB + ((c8 ^ (r & 7)) << 4));
+        const size_t o = (size_t)gm * g.Co + (size_t)grp * g.Cn + gc;
+        if (addend) {
+          float a[8], b[8];
+          unpack8(v, a);
+          unpack8(*reinterpret_cast<const uint4*>(addend + o), b);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) a[q] += b[q];
+          v = pack8(a);
+        }
+        *reinterpret_cast<uint4*>(Y + o) = v;
+      }
+    }
+    __syncthreads();   // the C tile aliases the ring the next tile's prologue refills
+  }
+
+  if constexpr (STATS) {
+    float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN][2]
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      float s = st_s[ni], q = st_q[ni];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        const int c = wn * WTN + ni * 16 + lane;
+        red[(wm * BN + c) * 2 + 0] = s;
+        red[(wm * BN + c) * 2 + 1] = q;
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const float s = red[tid * 2 + 0] + red[(BN + tid) * 2 + 0];
+      const float q = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
       const int c = n0 + tid;
       if (c < g.Cn) {
         float* srow = stats + (size_t)blockIdx.x * 2 * g.Co;
@@ -1076,10 +1427,86 @@ static int igemm_select(const ConvGeom& g) {
   X(17, 64, 64, 2, 2, 3)             \
   X(18, 64, 64, 1, 4, 4)
 
+// ---- phased 256-row kernel: cfg 20 (BN 256, 8 waves), 21 (BN 128, 8 waves),
+//      22 (BN 256, 4 waves: 128x128 per wave, 1 wave/SIMD), 23 (BN 128, 4 waves) ----
+static bool ph_eligible(const ConvGeom& g, int mode) {
+  return g.Cr % 64 == 0 && (mode == 0 || (mode == 1 && g.stride == 1));
+}
+
+template <int BN, int WAVES, int MODE>
+static int ph_occupancy() {
+  static int occ = 0;
+  if (occ == 0)
+    occ = std::min(
+        blocks_per_cu((const void*)conv_igemm_ph_kernel<BN, WAVES, MODE, true>, WAVES * 64, "igemm_ph"),
+        blocks_per_cu((const void*)conv_igemm_ph_kernel<BN, WAVES, MODE, false>, WAVES * 64, "igemm_ph"));
+  return occ;
+}
+
+template <int BN, int WAVES, int MODE>
+static int ph_grid_x(const ConvGeom& g) {
+  return persistent_grid_x(cdiv(g.M, 256), cdiv(g.Cn, BN) * g.groups, ph_occupancy<BN, WAVES, MODE>());
+}
+
+template <int BN, int WAVES, int MODE>
+static void launch_ph(const bf16* A, const bf16* B, bf16* Y, float* stats, const float* bias,
+                      const ConvGeom& g, hipStream_t st, const bf16* addend) {
+  dim3 grid(ph_grid_x<BN, WAVES, MODE>(g), cdiv(g.Cn, BN), g.groups);
+  if (stats)
+    hipLaunchKernelGGL((conv_igemm_ph_kernel<BN, WAVES, MODE, true>), grid, dim3(WAVES * 64), 0, st,
+                       A, B, Y, stats, bias, addend, g);
+  else
+    hipLaunchKernelGGL((conv_igemm_ph_kernel<BN, WAVES, MODE, false>), grid, dim3(WAVES * 64), 0, st,
+                       A, B, Y, stats, bias, addend, g);
+}
+
+// cfg of the phased kernel to use for this launch, or -1 (generic tile configs)
+template <int MODE>
+static int ph_cfg(const ConvGeom& g) {
+  if constexpr (MODE == 2) {
+    return -1;
+  } else {
+    const int c = igemm_select(g);
+    return (c >= 20 && c <= 23) && ph_eligible(g, MODE) ? c : -1;
+  }
+}
+
+template <int MODE>
+static bool ph_launch(int pc, const bf16* A, const bf16* B, bf16* Y, float* stats,
+                      const float* bias, const ConvGeom& g, hipStream_t st, const bf16* addend) {
+  if constexpr (MODE == 2) {
+    return false;
+  } else {
+    switch (pc) {
+      case 20: launch_ph<256, 8, MODE>(A, B, Y, stats, bias, g, st, addend); return true;
+      case 21: launch_ph<128, 8, MODE>(A, B, Y, stats, bias, g, st, addend); return true;
+      case 22: launch_ph<256, 4, MODE>(A, B, Y, stats, bias, g, st, addend); return true;
+      case 23: launch_ph<128, 4, MODE>(A, B, Y, stats, bias, g, st, addend); return true;
+      default: return false;
+    }
+  }
+}
+
+template <int MODE>
+static int ph_grid(int pc, const ConvGeom& g) {
+  if constexpr (MODE == 2) {
+    return 0;
+  } else {
+    switch (pc) {
+      case 20: return ph_grid_x<256, 8, MODE>(g);
+      case 21: return ph_grid_x<128, 8, MODE>(g);
+      case 22: return ph_grid_x<256, 4, MODE>(g);
+      case 23: return ph_grid_x<128, 4, MODE>(g);
+      default: return 0;
+    }
+  }
+}
+
 template <int MODE>
 static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, const float* bias,
                            const ConvGeom& g, hipStream_t st, const bf16* addend = nullptr,
                            float* ws = nullptr) {
+  if (ph_launch<MODE>(ph_cfg<MODE>(g), A, B, Y, stats, bias, g, st, addend)) return;
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
     case C: launch_igemm<BM, BN, WM, WN, ST, MODE>(A, B, Y, stats, bias, g, st, addend, ws); break;
@@ -1091,6 +1518,7 @@ static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, 
 
 template <int MODE>
 static int64_t igemm_ws_floats(const ConvGeom& g) {
+  if (ph_cfg<MODE>(g) >= 0) return 0;   // no split-K in the phased kernel
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
     case C: return igemm_ws_floats_t<BM, BN, WM, WN, ST, MODE>(g);
@@ -1102,6 +1530,7 @@ static int64_t igemm_ws_floats(const ConvGeom& g) {
 
 template <int MODE>
 static int igemm_grid_x(const ConvGeom& g) {
+  if (const int pc = ph_cfg<MODE>(g); pc >= 0) return ph_grid<MODE>(pc, g);
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
     case C: return igemm_grid_x_t<BM, BN, WM, WN, ST, MODE>(g);
@@ -1192,11 +1621,20 @@ std::vector<std::pair<int, int>> conv_tune_candidates(int kind, int N, int H, in
   const int KT = cdiv(taps * g.Cr, 64);
   const bool can_split = g.Co % 8 == 0 && g.Co <= kMaxSplitCo;
   std::vector<std::pair<int, int>> c;
-  const int cfgs[] = {3, 0, 4, 1, 16, 17, 18};
+  // every compiled tile config: BN in {32, 64, 128}, BM in {64, 128, 256, 512}, 4 or 8 waves,
+  // 2-4 stages (the 8-wave / 256-row tiles win on large-M shapes, the 64-row ones at small M)
+  static const int cfgs[] = {3, 0, 4, 1, 16, 17, 18, 5, 6, 7, 9, 10, 11, 12, 13, 14, 15, 2, 8};
+  static const int bn_of[] = {128, 64, 32, 128, 64, 64, 64, 128, 32, 128, 64, 64, 128, 64, 128, 64, 128, 64, 64};
+  if (ph_eligible(g, g.mode) && g.M >= 256 * 64) {   // phased 256-row kernel: large M only
+    // cfg 20 (BN 256, 8 waves) spills at 2 waves/SIMD (256 registers) and cfg 22 (BN 256, 4
+    // waves) past 512: not candidates
+    // (cfg 23, the 4-wave form, measured 30-40 % slower everywhere: one wave per SIMD cannot
+    // cover the DMA / LDS latency; not a candidate)
+    if (g.Cn >= 128) c.emplace_back(21, 1);
+  }
   for (int cfg : cfgs) {
-    if (cfg == 3 || cfg == 0 || cfg == 16) {
-      if (g.Cn <= 64) continue;          // 128-wide N tiles on <= 64 channels waste half
-    }
+    if (bn_of[cfg] >= 128 && g.Cn <= 64) continue;   // 128-wide N tiles on <= 64 channels
+    if (bn_of[cfg] <= 32 && g.Cn > 64) continue;     // 32-wide N tiles on wide layers
     for (int sp : {1, 2, 4, 8}) {
       if (sp > 1 && (!can_split || KT / sp < 2)) continue;
       c.emplace_back(cfg, sp);

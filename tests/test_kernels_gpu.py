@@ -89,7 +89,8 @@ N_IGEMM_CFGS = 19
 
 @pytest.mark.parametrize("case", [(3, 64, 16, 64, 3, 1, 1, 1), (2, 128, 8, 256, 3, 2, 1, 1),
                                   (2, 32, 8, 64, 3, 1, 1, 1), (3, 64, 7, 128, 3, 1, 1, 2),
-                                  (2, 64, 8, 128, 1, 2, 0, 1)])
+                                  (2, 64, 8, 128, 1, 2, 0, 1), (5, 128, 16, 320, 3, 1, 1, 1),
+                                  (9, 256, 8, 256, 3, 1, 1, 1)])
 def test_conv_every_tile_config(C, case):
     """Every compiled fwd/dgrad tile configuration (4- and 8-wave, fast scalar-tap path for
     Cin % 64 == 0 and the generic gather otherwise, stride-2 parity dgrad, odd M tails)."""
@@ -106,7 +107,7 @@ def test_conv_every_tile_config(C, case):
     dy_n = nhwc(dy).to(torch.bfloat16)
     bad = []
     try:
-        for cfg in range(N_IGEMM_CFGS):
+        for cfg in list(range(N_IGEMM_CFGS)) + [20, 21, 22, 23]:   # 20-23: phased 256-row kernel
             for split in (0, 3):   # 0: no split-K; 3: K loop split 3 ways + reduce kernel
                 C.set_conv_tile(0, cfg)
                 C.set_conv_tile(2, split)
