@@ -9,6 +9,8 @@
 // float4 loads. wgrad is a deterministic per-(pixel-chunk, tap) slab reduction.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace pca {
 
 struct DwGeom {
@@ -185,6 +187,200 @@ __global__ void dw_wgrad_final_kernel(const float* __restrict__ partial, int R, 
   dw[(size_t)co * T + tap] = s;
 }
 
+// ---------------------------------------------------------------------------------------
+// 3x3 depthwise fast paths (multiplier 1, C % 8 == 0, C <= 2048) — the MobileNet /
+// MobileNetV2 / ShuffleNetV2 / EfficientNet-k3 shapes. The generic kernels above re-load every
+// weight and every tap from L1/L2 per output vector, with 64-bit index math per element, and the
+// generic wgrad runs one block per tap (dY re-read 9x): 2.5-7x off their bandwidth roofline on
+// MobileNetV2 (profiles/). Here a thread owns 8 channels of one output column strip (RPT rows):
+//   * the 3 input rows of the 3x3 window roll down the strip as raw bf16 vectors, so each output
+//     row loads 3 new 16-byte vectors (stride 1) or 6 (stride 2) instead of 9;
+//   * fwd / stride-1 dgrad keep the 9 x 8 fp32 weights in registers (the stride-1 dgrad is the
+//     same correlation with mirrored taps and pad K-1-p);
+//   * wgrad accumulates all 9 taps x 8 channels in registers across every strip the thread
+//     walks (dY read once), then the threads sharing a channel group are reduced through LDS,
+//     one tap at a time, into one deterministic partial row per block.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void fma8(float* acc, const uint4& xv, const float* w) {
+  float f[8];
+  unpack8(xv, f);
+#pragma unroll
+  for (int v = 0; v < 8; ++v) acc[v] += f[v] * w[v];
+}
+
+// the 3 input vectors (kw = 0..2) of row ih for output column ow (zeros outside the image)
+template <int S>
+__device__ __forceinline__ void dw3_load_row(const bf16* xn, const DwGeom& g, int ih, int ow,
+                                             uint4* r) {
+  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+  const bool rok = (unsigned)ih < (unsigned)g.H;
+  const int iw0 = ow * S - g.p;
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) {
+    const int iw = iw0 + kw;
+    r[kw] = (rok && (unsigned)iw < (unsigned)g.W)
+                ? *reinterpret_cast<const uint4*>(xn + ((size_t)ih * g.W + iw) * g.C)
+                : zero;
+  }
+}
+
+template <int S>
+__device__ __forceinline__ void dw3_roll(uint4 (&win)[3][3]) {
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) {
+    if constexpr (S == 1) {
+      win[0][kw] = win[1][kw];
+      win[1][kw] = win[2][kw];
+    } else {
+      win[0][kw] = win[2][kw];
+    }
+  }
+}
+
+template <int S, bool FLIP>
+__global__ __launch_bounds__(256) void dw3_fwd_kernel(const bf16* __restrict__ x,
+                                                      const float* __restrict__ wT, DwGeom g,
+                                                      int rpt, bf16* __restrict__ y) {
+  const int G = g.C >> 3;
+  const int nstrip = (g.Ho + rpt - 1) / rpt;
+  const int total = g.N * nstrip * g.Wo * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G;
+    int q = i / G;
+    const int ow = q % g.Wo;
+    q /= g.Wo;
+    const int strip = q % nstrip;
+    const int n = q / nstrip;
+    const int c = gi * 8;
+    float w[9][8];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int src = FLIP ? 8 - t : t;
+      const float4 w0 = *reinterpret_cast<const float4*>(wT + src * g.Co + c);
+      const float4 w1 = *reinterpret_cast<const float4*>(wT + src * g.Co + c + 4);
+      w[t][0] = w0.x; w[t][1] = w0.y; w[t][2] = w0.z; w[t][3] = w0.w;
+      w[t][4] = w1.x; w[t][5] = w1.y; w[t][6] = w1.z; w[t][7] = w1.w;
+    }
+    const bf16* xn = x + (size_t)n * g.H * g.W * g.C + c;
+    const int oh0 = strip * rpt, oh1 = min(g.Ho, oh0 + rpt);
+    uint4 win[3][3];
+    dw3_load_row<S>(xn, g, oh0 * S - g.p, ow, win[0]);
+    if constexpr (S == 1) dw3_load_row<S>(xn, g, oh0 * S - g.p + 1, ow, win[1]);
+    bf16* yr = y + (((size_t)n * g.Ho + oh0) * g.Wo + ow) * g.Co + c;
+    for (int oh = oh0; oh < oh1; ++oh) {
+      const int ih0 = oh * S - g.p;
+      if constexpr (S == 2) dw3_load_row<S>(xn, g, ih0 + 1, ow, win[1]);
+      dw3_load_row<S>(xn, g, ih0 + 2, ow, win[2]);
+      float acc[8];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) acc[v] = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) fma8(acc, win[kh][kw], w[kh * 3 + kw]);
+      *reinterpret_cast<uint4*>(yr) = pack8(acc);
+      yr += (size_t)g.Wo * g.Co;
+      dw3_roll<S>(win);
+    }
+  }
+}
+
+// partial[block][tap][Co]: thread t owns channel group t % G and walks the column strips
+// item = blockIdx.x * W + t / G (+ gridDim.x * W ...), W = 256 / G workers per block
+template <int S>
+__global__ __launch_bounds__(256) void dw3_wgrad_kernel(const bf16* __restrict__ x,
+                                                        const bf16* __restrict__ dy, DwGeom g,
+                                                        int rpt, float* __restrict__ partial) {
+  __shared__ float red[256 * 8];
+  const int G = g.Co >> 3;
+  const int W = 256 / G;
+  const int t = threadIdx.x;
+  const int gi = t % G, wk = t / G;
+  const int c = gi * 8;
+  const int nstrip = (g.Ho + rpt - 1) / rpt;
+  const int items = g.N * nstrip * g.Wo;
+  float acc[9][8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int v = 0; v < 8; ++v) acc[k][v] = 0.f;
+  if (wk < W) {
+    for (int item = blockIdx.x * W + wk; item < items; item += gridDim.x * W) {
+      const int ow = item % g.Wo;
+      const int q = item / g.Wo;
+      const int strip = q % nstrip, n = q / nstrip;
+      const bf16* xn = x + (size_t)n * g.H * g.W * g.C + c;
+      const int oh0 = strip * rpt, oh1 = min(g.Ho, oh0 + rpt);
+      uint4 win[3][3];
+      dw3_load_row<S>(xn, g, oh0 * S - g.p, ow, win[0]);
+      if constexpr (S == 1) dw3_load_row<S>(xn, g, oh0 * S - g.p + 1, ow, win[1]);
+      const bf16* dr = dy + (((size_t)n * g.Ho + oh0) * g.Wo + ow) * g.Co + c;
+      for (int oh = oh0; oh < oh1; ++oh) {
+        const int ih0 = oh * S - g.p;
+        if constexpr (S == 2) dw3_load_row<S>(xn, g, ih0 + 1, ow, win[1]);
+        dw3_load_row<S>(xn, g, ih0 + 2, ow, win[2]);
+        float d[8];
+        unpack8(*reinterpret_cast<const uint4*>(dr), d);
+        dr += (size_t)g.Wo * g.Co;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            float f[8];
+            unpack8(win[kh][kw], f);
+#pragma unroll
+            for (int v = 0; v < 8; ++v) acc[kh * 3 + kw][v] += f[v] * d[v];
+          }
+        dw3_roll<S>(win);
+      }
+    }
+  }
+  float* prow = partial + (size_t)blockIdx.x * 9 * g.Co;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) red[t * 8 + v] = acc[k][v];
+    __syncthreads();
+    if (t < G) {
+      float s[8];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) s[v] = red[t * 8 + v];
+      for (int j = 1; j < W; ++j)
+#pragma unroll
+        for (int v = 0; v < 8; ++v) s[v] += red[(j * G + t) * 8 + v];
+      float4* o = reinterpret_cast<float4*>(prow + (size_t)k * g.Co + c);
+      o[0] = make_float4(s[0], s[1], s[2], s[3]);
+      o[1] = make_float4(s[4], s[5], s[6], s[7]);
+    }
+    __syncthreads();
+  }
+}
+
+// dw[co][tap] = sum_r partial[r][tap][co]: 32 columns x 8 row lanes per block, lanes added in
+// a fixed order (deterministic)
+__global__ __launch_bounds__(256) void dw_wgrad_final4_kernel(const float* __restrict__ partial,
+                                                              int R, int T, int Co,
+                                                              float* __restrict__ dw) {
+  __shared__ float red[8][32];
+  const int cl = threadIdx.x & 31, l = threadIdx.x >> 5;
+  const int idx = blockIdx.x * 32 + cl;
+  const int n = T * Co;
+  float s = 0.f;
+  if (idx < n) {
+#pragma unroll 4
+    for (int r = l; r < R; r += 8) s += partial[(size_t)r * n + idx];
+  }
+  red[l][cl] = s;
+  __syncthreads();
+  if (l == 0 && idx < n) {
+    float o = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o += red[k][cl];
+    const int tap = idx / Co, co = idx - tap * Co;
+    dw[(size_t)co * T + tap] = o;
+  }
+}
+
 // ================================================================================ host
 static DwGeom dwg(int N, int H, int W, int C, int Ho, int Wo, int Co, int KH, int KW, int s, int p) {
   DwGeom g{N, H, W, C, Ho, Wo, Co, KH, KW, s, p, Co / C};
@@ -195,9 +391,34 @@ static int gcap(size_t work) {
   return (int)(b < 8192 ? (b ? b : 1) : 8192);
 }
 
+static bool dw3_ok(const DwGeom& g) {
+  static const bool off = [] {
+    const char* e = getenv("PCA_DW3");
+    return e && e[0] == '0';
+  }();
+  return !off && g.mult == 1 && g.C % 8 == 0 && g.C <= 2048 && g.KH == 3 && g.KW == 3 &&
+         g.p == 1 && (g.s == 1 || g.s == 2);
+}
+
+static int dw3_rpt(int Ho) { return Ho < 8 ? Ho : 8; }
+
+static void dw3_fwd(const bf16* x, const float* wT, const DwGeom& g, bool flip, bf16* y,
+                    hipStream_t st) {
+  const int rpt = dw3_rpt(g.Ho);
+  const size_t work = (size_t)g.N * cdiv(g.Ho, rpt) * g.Wo * (g.C / 8);
+  const dim3 grid(gcap(work)), block(256);
+  if (g.s == 1) {
+    if (flip) hipLaunchKernelGGL((dw3_fwd_kernel<1, true>), grid, block, 0, st, x, wT, g, rpt, y);
+    else hipLaunchKernelGGL((dw3_fwd_kernel<1, false>), grid, block, 0, st, x, wT, g, rpt, y);
+  } else {
+    hipLaunchKernelGGL((dw3_fwd_kernel<2, false>), grid, block, 0, st, x, wT, g, rpt, y);
+  }
+}
+
 void dw_fwd_launch(const bf16* x, const float* wT, int N, int H, int W, int C, int Ho, int Wo,
                    int Co, int KH, int KW, int s, int p, bf16* y, hipStream_t st) {
   DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
+  if (dw3_ok(g)) return dw3_fwd(x, wT, g, false, y, st);
   if (g.mult == 1 && C % 8 == 0)
     hipLaunchKernelGGL(dw_fwd_kernel<8>, dim3(gcap((size_t)N * Ho * Wo * Co / 8)), dim3(256), 0, st,
                        x, wT, g, y);
@@ -209,6 +430,11 @@ void dw_fwd_launch(const bf16* x, const float* wT, int N, int H, int W, int C, i
 void dw_dgrad_launch(const bf16* dy, const float* wT, int N, int H, int W, int C, int Ho, int Wo,
                      int Co, int KH, int KW, int s, int p, bf16* dx, hipStream_t st) {
   DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
+  if (dw3_ok(g) && s == 1) {
+    // stride-1 dgrad = forward correlation of dY with the mirrored taps (pad K-1-p)
+    const DwGeom gd = dwg(N, Ho, Wo, Co, H, W, C, KH, KW, 1, KH - 1 - p);
+    return dw3_fwd(dy, wT, gd, true, dx, st);
+  }
   if (g.mult == 1 && C % 8 == 0)
     hipLaunchKernelGGL(dw_dgrad_kernel<8>, dim3(gcap((size_t)N * H * W * C / 8)), dim3(256), 0, st,
                        dy, wT, g, dx);
@@ -220,7 +446,7 @@ void dw_dgrad_launch(const bf16* dy, const float* wT, int N, int H, int W, int C
 int dw_wgrad_partials(int N, int Ho, int Wo) {
   const int P = N * Ho * Wo;
   int chunks = cdiv(P, 256);
-  return chunks > 256 ? 256 : chunks;
+  return chunks > 1024 ? 1024 : chunks;
 }
 
 void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, int Ho, int Wo,
@@ -230,13 +456,24 @@ void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, 
   const int P = N * Ho * Wo;
   const int rows = cdiv(P, chunks);
   const int T = KH * KW;
+  if (dw3_ok(g) && Co / 8 <= 256) {
+    // chunks = partial rows = blocks of the strip-walking kernel
+    const int rpt = dw3_rpt(Ho);
+    if (s == 1)
+      hipLaunchKernelGGL(dw3_wgrad_kernel<1>, dim3(chunks), dim3(256), 0, st, x, dy, g, rpt, partial);
+    else
+      hipLaunchKernelGGL(dw3_wgrad_kernel<2>, dim3(chunks), dim3(256), 0, st, x, dy, g, rpt, partial);
+    hipLaunchKernelGGL(dw_wgrad_final4_kernel, dim3(cdiv(T * Co, 32)), dim3(256), 0, st, partial,
+                       chunks, T, Co, dw);
+    return;
+  }
   if (g.mult == 1 && Co % 8 == 0)
     hipLaunchKernelGGL(dw_wgrad_kernel<8>, dim3(chunks, T), dim3(256), 0, st, x, dy, g, rows,
                        partial);
   else
     hipLaunchKernelGGL(dw_wgrad_kernel<1>, dim3(chunks, T), dim3(256), 0, st, x, dy, g, rows,
                        partial);
-  hipLaunchKernelGGL(dw_wgrad_final_kernel, dim3(cdiv(T * Co, 256)), dim3(256), 0, st, partial,
+  hipLaunchKernelGGL(dw_wgrad_final4_kernel, dim3(cdiv(T * Co, 32)), dim3(256), 0, st, partial,
                      chunks, T, Co, dw);
   (void)partial2;
 }

@@ -296,10 +296,15 @@ def test_pools_and_gap(C):
     assert rel_err(pooled, x.detach().mean((2, 3))) < 1e-2
 
 
-@pytest.mark.parametrize("Cin,mult,k,s", [(32, 1, 3, 1), (144, 1, 3, 2), (240, 1, 5, 1), (44, 2, 7, 2), (58, 1, 3, 2)])
-def test_depthwise(C, Cin, mult, k, s):
+@pytest.mark.parametrize("Cin,mult,k,s,H", [(32, 1, 3, 1, 16), (144, 1, 3, 2, 16), (240, 1, 5, 1, 16),
+                                            (44, 2, 7, 2, 16), (58, 1, 3, 2, 16), (96, 1, 3, 1, 16),
+                                            (1152, 1, 3, 1, 4), (192, 1, 3, 2, 8), (72, 1, 3, 2, 7),
+                                            (24, 1, 3, 1, 9)])
+def test_depthwise(C, Cin, mult, k, s, H):
+    """k3 / multiplier 1 / C % 8 == 0 takes the rolling-window fast paths (dw3_*), the rest the
+    generic kernels; both against torch's fp32 grouped conv."""
     torch.manual_seed(5)
-    N, H = 2, 16
+    N = 2
     p = (k - 1) // 2
     Co = Cin * mult
     x = bf(torch.randn(N, Cin, H, H, device="cuda")).requires_grad_(True)
