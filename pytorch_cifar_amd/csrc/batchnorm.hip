@@ -275,8 +275,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
       }
       int r = r0 + ry;
       if constexpr (VEC == 8 && NS == 2) {
-        // masked-ReLU / no-act fast path: two rows in flight per thread
-        if (mask || act == ACT_NONE) {
+        // masked-ReLU / no-act / swish fast path: two rows in flight per thread
+        const bool swish = act == ACT_SWISH;
+        if (mask || act == ACT_NONE || swish) {
+          float sc[8], sh[8];
+#pragma unroll
+          for (int v = 0; v < 8; ++v) {
+            sc[v] = swish ? aux[2 * C + c0 + v] : 0.f;
+            sh[v] = swish ? aux[3 * C + c0 + v] : 0.f;
+          }
           for (; r + rp.RPP < r1; r += 2 * rp.RPP) {
             const size_t e = (size_t)r * C + c0, e2 = e + (size_t)rp.RPP * C;
             float dz[8], dz2[8], yy[8], yy2[8];
@@ -287,8 +294,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
             const uint32_t m = mask ? mask[e >> 3] : 0xffu, m2 = mask ? mask[e2 >> 3] : 0xffu;
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
-              const float a = ((m >> v) & 1u) ? dz[v] : 0.f;
-              const float b = ((m2 >> v) & 1u) ? dz2[v] : 0.f;
+              float a = ((m >> v) & 1u) ? dz[v] : 0.f;
+              float b = ((m2 >> v) & 1u) ? dz2[v] : 0.f;
+              if (swish) {   // swish'(z), z recomputed from y (the BN output before the act)
+                a *= act_grad(yy[v] * sc[v] + sh[v], ACT_SWISH);
+                b *= act_grad(yy2[v] * sc[v] + sh[v], ACT_SWISH);
+              }
               acc[0][v] += a + b;
               acc[1][v] += (a * (yy[v] - mean[v]) + b * (yy2[v] - mean[v])) * istd[v];
             }
@@ -483,18 +494,24 @@ __global__ __launch_bounds__(256) void bn_apply_rows_kernel(
   }
 }
 
-template <bool RES, bool DUAL, bool MASK>
+// KIND: 0 = no activation, 1 = ReLU through the 1-bit mask, 2 = swish (z recomputed from y)
+template <bool RES, bool DUAL, int KIND>
 __global__ __launch_bounds__(256) void bn_bwd_apply_rows_kernel(
     const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
     const float* __restrict__ coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
-    const bf16* __restrict__ y2, bf16* __restrict__ dy2) {
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux) {
+  constexpr bool MASK = KIND == 1;
   const int TPR = C >> 3, RPB = 256 / TPR;
   const int g = threadIdx.x % TPR, ro = threadIdx.x / TPR;
   if (ro >= RPB) return;
   const int c0 = g * 8;
-  float ca[8], cb[8], cd[8], ca2[8], cb2[8], cd2[8];
+  float ca[8], cb[8], cd[8], ca2[8], cb2[8], cd2[8], zs[8], zb[8];
 #pragma unroll
   for (int v = 0; v < 8; ++v) {
+    if constexpr (KIND == 2) {
+      zs[v] = aux[2 * C + c0 + v];
+      zb[v] = aux[3 * C + c0 + v];
+    }
     ca[v] = coef[c0 + v];
     cb[v] = coef[C + c0 + v];
     cd[v] = coef[2 * C + c0 + v];
@@ -521,6 +538,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows_kernel(
       for (int v = 0; v < 8; ++v) {
         dz[v] = ((m >> v) & 1u) ? dz[v] : 0.f;
         dz2[v] = ((m2 >> v) & 1u) ? dz2[v] : 0.f;
+      }
+    }
+    if constexpr (KIND == 2) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        dz[v] *= act_grad(yy[v] * zs[v] + zb[v], ACT_SWISH);
+        dz2[v] *= act_grad(yy2[v] * zs[v] + zb[v], ACT_SWISH);
       }
     }
     float o[8], o2[8];
@@ -611,12 +635,15 @@ void bn_finalize_launch(const float* stat, int R, int C, double count, const flo
 void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const bf16* res,
                      const bf16* y2, const float* aux2, int act, bf16* out, uint8_t* mask,
                      hipStream_t st) {
-  if (rows_enabled() && C % 8 == 0 && C <= 2048 && (act == ACT_RELU || act == ACT_NONE) && !(res && y2)) {
+  if (rows_enabled() && C % 8 == 0 && C <= 2048 &&
+      (act == ACT_RELU || act == ACT_NONE || (act == ACT_SWISH && !res && !y2)) && !(res && y2)) {
     const int M = (int)(total / C);
     const dim3 gr(rows_grid(M, C)), bl(256);
 #define PCA_APPLY(R, D, A) \
     hipLaunchKernelGGL((bn_apply_rows_kernel<R, D, A>), gr, bl, 0, st, y, aux, C, M, res, y2, aux2, out, mask)
-    if (act == ACT_RELU) {
+    if (act == ACT_SWISH) {
+      PCA_APPLY(false, false, ACT_SWISH);
+    } else if (act == ACT_RELU) {
       if (res) PCA_APPLY(true, false, ACT_RELU);
       else if (y2) PCA_APPLY(false, true, ACT_RELU);
       else PCA_APPLY(false, false, ACT_RELU);
@@ -680,21 +707,24 @@ void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask,
                          const float* aux, const float* coef, int act, int C, size_t total,
                          bf16* dy, bf16* dres, const bf16* y2, bf16* dy2, hipStream_t st) {
   const bool masked = act == ACT_RELU && mask != nullptr;
-  if (rows_enabled() && C % 8 == 0 && C <= 2048 && (masked || act == ACT_NONE)) {
+  const bool swish = act == ACT_SWISH && !dres && !y2;
+  if (rows_enabled() && C % 8 == 0 && C <= 2048 && (masked || act == ACT_NONE || swish)) {
     const int M = (int)(total / C);
     const dim3 gr(rows_grid(M, C)), bl(256);
 #define PCA_BWD(R, D, K) \
-    hipLaunchKernelGGL((bn_bwd_apply_rows_kernel<R, D, K>), gr, bl, 0, st, dout, mask, y, coef, C, M, dy, dres, y2, dy2)
+    hipLaunchKernelGGL((bn_bwd_apply_rows_kernel<R, D, K>), gr, bl, 0, st, dout, mask, y, coef, C, M, dy, dres, y2, dy2, aux)
     if (masked) {
-      if (dres && y2) PCA_BWD(true, true, true);
-      else if (dres) PCA_BWD(true, false, true);
-      else if (y2) PCA_BWD(false, true, true);
-      else PCA_BWD(false, false, true);
+      if (dres && y2) PCA_BWD(true, true, 1);
+      else if (dres) PCA_BWD(true, false, 1);
+      else if (y2) PCA_BWD(false, true, 1);
+      else PCA_BWD(false, false, 1);
+    } else if (swish) {
+      PCA_BWD(false, false, 2);
     } else {
-      if (dres && y2) PCA_BWD(true, true, false);
-      else if (dres) PCA_BWD(true, false, false);
-      else if (y2) PCA_BWD(false, true, false);
-      else PCA_BWD(false, false, false);
+      if (dres && y2) PCA_BWD(true, true, 0);
+      else if (dres) PCA_BWD(true, false, 0);
+      else if (y2) PCA_BWD(false, true, 0);
+      else PCA_BWD(false, false, 0);
     }
 #undef PCA_BWD
     return;
