@@ -45,7 +45,11 @@ int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
                        int groups, int Ho, int Wo);
 void set_conv_tile(int kind, int idx);
 void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int, int, int, int,
-                       int, int, int, int, hipStream_t, const bf16* addend, float* ws);
+                       int, int, int, int, hipStream_t, const bf16* addend, float* ws,
+                       const bf16* bn_y = nullptr, const uint8_t* bn_mask = nullptr,
+                       const float* bn_aux = nullptr, float* bn_part = nullptr);
+int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                       int groups, int Ho, int Wo);
 void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
                        int Cin, int Cout, int KH, int KW, int stride, int pad, int groups, int Ho,
                        int Wo, hipStream_t st);
@@ -254,8 +258,13 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
   return {y, stats};
 }
 
-Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, int pad,
-                  int groups, const optional<Tensor>& addend) {
+// dgrad; with (bn_y, bn_mask, bn_aux) also the fused backward reduce of the BatchNorm+ReLU that
+// produced the conv input: returns {dx, partial [rows][2][Cin]} (partial empty when the selected
+// kernel cannot fuse it, e.g. the phased 256-row kernel; the caller then reduces separately)
+std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, int W, int stride,
+                                    int pad, int groups, const optional<Tensor>& addend,
+                                    const optional<Tensor>& bn_y, const optional<Tensor>& bn_mask,
+                                    const optional<Tensor>& bn_aux) {
   check_bf16(dy, "dy");
   check_bf16(wt, "wt");
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
@@ -270,6 +279,17 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, 
     TORCH_CHECK(addend->numel() == (int64_t)N * H * W * Cin && addend->is_contiguous(),
                 "addend must match dx (NHWC)");
     add = ptr<bf16>(*addend);
+  }
+  const bool want_bn = bn_y.has_value() && bn_y->defined();
+  if (want_bn) {
+    check_bf16(*bn_y, "bn_y");
+    TORCH_CHECK(bn_y->numel() == (int64_t)N * H * W * Cin, "bn_y must match dx (NHWC)");
+    TORCH_CHECK(bn_mask.has_value() && bn_mask->defined() && bn_mask->is_contiguous() &&
+                    bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == bn_y->numel(),
+                "bn_mask: one bit per element");
+    TORCH_CHECK(bn_aux.has_value() && bn_aux->defined(), "bn_aux required");
+    check_f32(*bn_aux, "bn_aux");
+    TORCH_CHECK(bn_aux->numel() >= 2 * Cin, "bn_aux [mean|istd|...][C]");
   }
   if (g_autotune && !stream_capturing(cur_stream()) &&
       pca::conv_needs_tune(1, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, false)) {
@@ -289,10 +309,26 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, 
                                                 Ho, Wo);
   Tensor ws;
   if (wsn > 0) ws = at::empty({wsn}, dy.options().dtype(at::kFloat));
+  Tensor part;
+  const int rows = want_bn ? pca::conv_dgrad_bn_rows(N, H, W, Cin, Cout, KH, KW, stride, pad,
+                                                     groups, Ho, Wo)
+                           : 0;
+  if (rows > 0) part = at::empty({rows, 2, Cin}, dy.options().dtype(at::kFloat));
   pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dx), N, H, W, Cin, Cout, KH, KW,
                          stride, pad, groups, Ho, Wo, cur_stream(), add,
-                         wsn > 0 ? ptr<float>(ws) : nullptr);
-  return dx;
+                         wsn > 0 ? ptr<float>(ws) : nullptr,
+                         rows > 0 ? ptr<bf16>(*bn_y) : nullptr,
+                         rows > 0 ? bn_mask->data_ptr<uint8_t>() : nullptr,
+                         rows > 0 ? ptr<float>(*bn_aux) : nullptr,
+                         rows > 0 ? ptr<float>(part) : nullptr);
+  if (rows == 0) part = at::empty({0}, dy.options().dtype(at::kFloat));
+  return {dx, part};
+}
+
+Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, int pad,
+                  int groups, const optional<Tensor>& addend) {
+  return conv_dgrad_impl(dy, wt, H, W, stride, pad, groups, addend, c10::nullopt, c10::nullopt,
+                         c10::nullopt)[0];
 }
 
 // dw: fp32 [Cout, KH, KW, Cin/G] (zeroed here)
@@ -448,7 +484,8 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
                                 bool need_dres, const optional<Tensor>& dgamma_acc,
                                 const optional<Tensor>& dbeta_acc,
                                 const optional<Tensor>& dgamma2_acc,
-                                const optional<Tensor>& dbeta2_acc) {
+                                const optional<Tensor>& dbeta2_acc,
+                                const optional<Tensor>& partial_in) {
   check_bf16(dout, "dout");
   check_bf16(y, "y");
   const int C = y.size(-1);
@@ -461,14 +498,25 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
                 "relu backward needs the output or its sign mask");
   const uint8_t* mk = has_mask ? mask->data_ptr<uint8_t>() : nullptr;
   auto st = cur_stream();
-  const int P = pca::bn_row_blocks(M, C);
   auto fopt = y.options().dtype(at::kFloat);
-  auto partial = at::empty({P, NS, C}, fopt);
-  pca::bn_bwd_reduce_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
-                            optr<bf16>(y2), optr<float>(aux2), act, M, C, ptr<float>(partial), P,
-                            st);
+  Tensor partial;
+  int R;
+  if (partial_in.has_value() && partial_in->defined() && partial_in->numel() > 0) {
+    // (sum dz, sum dz*xhat) already reduced by the producing conv's dgrad epilogue
+    check_f32(*partial_in, "partial_in");
+    TORCH_CHECK(!dual && partial_in->dim() == 3 && partial_in->size(1) == 2 &&
+                    partial_in->size(2) == C, "partial_in must be [R][2][C] (single BN)");
+    partial = *partial_in;
+    R = partial.size(0);
+  } else {
+    const int P = pca::bn_row_blocks(M, C);
+    partial = at::empty({P, NS, C}, fopt);
+    pca::bn_bwd_reduce_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
+                              optr<bf16>(y2), optr<float>(aux2), act, M, C, ptr<float>(partial), P,
+                              st);
+    R = P;
+  }
   const float* stat = ptr<float>(partial);
-  int R = P;
   Tensor folded;
   if (R > 1024) {
     folded = at::empty({64, NS, C}, fopt);
@@ -787,6 +835,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend") = py::none());
+  m.def("conv_dgrad_bn", &conv_dgrad_impl, py::arg("dy"), py::arg("wt"), py::arg("H"),
+        py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend"),
+        py::arg("bn_y"), py::arg("bn_mask"), py::arg("bn_aux"),
+        "dgrad + fused backward reduce of the producing BN+ReLU -> (dx, partial[rows][2][C])");
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
   m.def("conv_autotune_enabled", []() { return g_autotune; });
@@ -807,7 +859,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply);
-  m.def("bn_backward", &bn_backward);
+  m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("mask"), py::arg("y"),
+        py::arg("aux"), py::arg("gamma"), py::arg("y2"), py::arg("aux2"), py::arg("gamma2"),
+        py::arg("act"), py::arg("training"), py::arg("need_dres"), py::arg("dgamma_acc"),
+        py::arg("dbeta_acc"), py::arg("dgamma2_acc"), py::arg("dbeta2_acc"),
+        py::arg("partial_in") = py::none());
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("nhwc_to_nchw", &nhwc_to_nchw);
   m.def("augment", &augment);

@@ -23,6 +23,12 @@ struct C64Geom {
   int N, H;        // images, rows (W == 32)
   int tiles;       // N * H / 8
   uint32_t a_bytes;
+  // dgrad: fused backward reduce of the BN(+ReLU) that produced the conv input (see
+  // conv_mfma.hip ConvGeom::bn_*); bn_part = nullptr disables it
+  const bf16* bn_y;
+  const uint8_t* bn_mask;
+  const float* bn_aux;
+  float* bn_part;   // [gridDim.x][2][64]
 };
 
 namespace c64 {
@@ -105,6 +111,15 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
   const int kq = lane >> 4;                      // 8-channel chunk within a 32-channel half
 
   float st_s[4] = {0.f, 0.f, 0.f, 0.f}, st_q[4] = {0.f, 0.f, 0.f, 0.f};
+  // fused BN-backward reduce (dgrad): this thread's store-loop channel group is tid & 7
+  const bool bnf = DGRAD && g.bn_part != nullptr;
+  float bs1[8], bs2[8], bmean[8], bistd[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bs1[q] = bs2[q] = 0.f;
+    bmean[q] = bnf ? g.bn_aux[(tid & 7) * 8 + q] : 0.f;
+    bistd[q] = bnf ? g.bn_aux[64 + (tid & 7) * 8 + q] : 0.f;
+  }
 
   constexpr int STORES = (TILE * 8) / 256;      // global stores per thread per tile
   wait_vmcnt<0>();                                // weights + first halo
@@ -199,6 +214,18 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
         for (int e = 0; e < 8; ++e) a[e] += b[e];
         v = pack8(a);
       }
+      if (bnf) {
+        float f[8], yy[8];
+        unpack8(v, f);
+        unpack8(*reinterpret_cast<const uint4*>(g.bn_y + o), yy);
+        const uint32_t m = g.bn_mask[o >> 3];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
+          bs1[e] += dz;
+          bs2[e] += dz * (yy[e] - bmean[e]) * bistd[e];
+        }
+      }
       *reinterpret_cast<uint4*>(Y + o) = v;
     }
   }
@@ -234,6 +261,30 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
     }
   } else {
     wait_vmcnt<0>();
+    if (bnf) {
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);  // [256][16]
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        red[tid * 16 + q] = bs1[q];
+        red[tid * 16 + 8 + q] = bs2[q];
+      }
+      __syncthreads();
+      if (tid < 8) {
+        float a[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) a[q] = 0.f;
+        for (int j = tid; j < 256; j += 8)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) a[q] += red[j * 16 + q];
+        float* r0 = g.bn_part + (size_t)blockIdx.x * 128 + tid * 8;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          r0[q] = a[q];
+          r0[64 + q] = a[8 + q];
+        }
+      }
+    }
   }
 }
 
@@ -264,12 +315,17 @@ bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW,
 int conv_c64_stat_rows(int N, int H) { return c64_grid(N * H / 8); }
 
 void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const bf16* addend,
-                     int N, int H, bool dgrad, hipStream_t st) {
+                     int N, int H, bool dgrad, hipStream_t st, const bf16* bn_y,
+                     const uint8_t* bn_mask, const float* bn_aux, float* bn_part) {
   C64Geom g;
   g.N = N;
   g.H = H;
   g.tiles = N * H / 8;
   g.a_bytes = (uint32_t)((size_t)N * H * 32 * 64 * 2);
+  g.bn_y = bn_y;
+  g.bn_mask = bn_mask;
+  g.bn_aux = bn_aux;
+  g.bn_part = dgrad ? bn_part : nullptr;
   const dim3 grid(c64_grid(g.tiles)), block(256);
   if (dgrad)
     hipLaunchKernelGGL((conv3x3_c64_kernel<true, false>), grid, block, 0, st, a, w, y, nullptr,

@@ -53,7 +53,57 @@ struct ConvGeom {
   int ksplit;           // split-K factor (1 = off): grid.z = ksplit * groups * classes
   float* ws;            // split-K fp32 partials [ksplit][N*Ho*Wo][Co]
   int mode;             // 0 fwd, 1 dgrad, 2 parity dgrad (autotune cache key)
+  // dgrad only: fused backward reduce of the BatchNorm(+ReLU) that produced this conv's input
+  // (bn_part != nullptr): per-channel sums of dz = dX * relu'(mask) and dz * xhat into slab rows
+  const bf16* bn_y;     // that BN's input y
+  const uint8_t* bn_mask;
+  const float* bn_aux;  // [mean | istd | ...][Co]
+  float* bn_part;       // [rows][2][Co]
 };
+
+// dz = dX * relu'(y), accumulated as (sum dz, sum dz * xhat) for 8 channels
+__device__ __forceinline__ void bn_fuse_acc(const uint4& v, const bf16* y, uint8_t m,
+                                            const float* mean, const float* istd, float* s1,
+                                            float* s2) {
+  float f[8], yy[8];
+  unpack8(v, f);
+  unpack8(*reinterpret_cast<const uint4*>(y), yy);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
+    s1[q] += dz;
+    s2[q] += dz * (yy[q] - mean[q]) * istd[q];
+  }
+}
+
+// block reduction of the per-thread (s1, s2) of channel group c8 = tid % CG (NT % CG == 0) into
+// slab row `row`; channel base ch0 of group 0 (red: NT * 16 floats of LDS)
+template <int NT>
+__device__ __forceinline__ void bn_fuse_flush(float* red, const float* s1, const float* s2,
+                                              int CG, int ch0, int cvalid, int Co, float* part,
+                                              int row) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    red[tid * 16 + q] = s1[q];
+    red[tid * 16 + 8 + q] = s2[q];
+  }
+  __syncthreads();
+  if (tid < CG && tid * 8 < cvalid) {
+    float a[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a[q] = 0.f;
+    for (int j = tid; j < NT; j += CG)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a[q] += red[j * 16 + q];
+    float* r0 = part + (size_t)row * 2 * Co + ch0 + tid * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      r0[q] = a[q];
+      r0[Co + q] = a[8 + q];
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------------------
 // forward / dgrad implicit GEMM
@@ -147,6 +197,25 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
   float st_s[TN], st_q[TN];
 #pragma unroll
   for (int ni = 0; ni < TN; ++ni) st_s[ni] = st_q[ni] = 0.f;
+
+  // fused BN-backward reduce (dgrad): this thread's store-loop channel group is fixed
+  constexpr int CG_ = BN / 8;
+  static_assert(NT % CG_ == 0, "store loop channel group must be per-thread constant");
+  const bool bnf = DGRAD && !SPLITK && g.bn_part != nullptr;
+  float bs1[8], bs2[8], bmean[8], bistd[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bs1[q] = bs2[q] = bmean[q] = bistd[q] = 0.f;
+  if (bnf) {
+    const int gc = n0 + (tid % CG_) * 8;
+    if (gc < g.Cn) {
+      const int ch = grp * g.Cn + gc;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        bmean[q] = g.bn_aux[ch + q];
+        bistd[q] = g.bn_aux[g.Co + ch + q];
+      }
+    }
+  }
 
   // Persistent over M tiles (grid.x <= mtiles): amortises the per-block set-up and bounds the
   // BN statistics slab at grid.x rows.
@@ -414,12 +483,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
           for (int q = 0; q < 8; ++q) a[q] += b[q];
           v = pack8(a);
         }
+        if (bnf) bn_fuse_acc(v, g.bn_y + o, g.bn_mask[o >> 3], bmean, bistd, bs1, bs2);
         *reinterpret_cast<uint4*>(Y + o) = v;
       }
     }
     __syncthreads();   // the C tile aliases the ring the next tile's prologue refills
   }
 
+  if constexpr (DGRAD && !SPLITK) {
+    if (bnf) {   // slab row per (M-walker, parity class); channels of this block's N tile
+      const int row = PARITY ? (int)blockIdx.x * 4 + cls : (int)blockIdx.x;
+      bn_fuse_flush<NT>(reinterpret_cast<float*>(smem), bs1, bs2, CG_, grp * g.Cn + n0,
+                        g.Cn - n0, g.Co, g.bn_part, row);
+    }
+  }
   if constexpr (STATS && !SPLITK) {
     float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
 #pragma unroll
@@ -1136,7 +1213,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                            const float* __restrict__ bias,
                                                            const bf16* __restrict__ addend,
                                                            bf16* __restrict__ Y,
-                                                           float* __restrict__ stats) {
+                                                           float* __restrict__ stats,
+                                                           const bf16* __restrict__ bn_y,
+                                                           const uint8_t* __restrict__ bn_mask,
+                                                           const float* __restrict__ bn_aux,
+                                                           float* __restrict__ bn_part) {
   __shared__ float red[2 * 2048];
   const int CG = Co >> 3;             // 8-channel groups per row (Co <= 2048: CG <= 256)
   const int RP = 256 / CG;            // rows per pass
@@ -1151,6 +1232,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
   const size_t plane = (size_t)M * Co;
+  float bs1[8], bs2[8], bmean[8], bistd[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bs1[q] = bs2[q] = 0.f;
+    bmean[q] = bn_part && active ? bn_aux[cg * 8 + q] : 0.f;
+    bistd[q] = bn_part && active ? bn_aux[Co + cg * 8 + q] : 0.f;
+  }
   if (active) {
     for (int r = r0 + rr; r < r1; r += RP) {
       const size_t o = (size_t)r * Co + cg * 8;
@@ -1176,8 +1264,30 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 #pragma unroll
         for (int q = 0; q < 8; ++q) a[q] += d[q];
       }
-      *reinterpret_cast<uint4*>(Y + o) = pack8(a);
+      const uint4 pv = pack8(a);
+      if (bn_part) bn_fuse_acc(pv, bn_y + o, bn_mask[o >> 3], bmean, bistd, bs1, bs2);
+      *reinterpret_cast<uint4*>(Y + o) = pv;
     }
+  }
+  if (bn_part) {   // fused BN-backward reduce: one slab row per block (rows = gridDim.x)
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[(rr * Co + cg * 8 + q) * 2 + 0] = active ? bs1[q] : 0.f;
+      red[(rr * Co + cg * 8 + q) * 2 + 1] = active ? bs2[q] : 0.f;
+    }
+    __syncthreads();
+    float* prow = bn_part + (size_t)blockIdx.x * 2 * Co;
+    for (int c = tid; c < Co; c += 256) {
+      float s0 = 0.f, q0 = 0.f;
+      for (int k = 0; k < RP; ++k) {
+        s0 += red[(k * Co + c) * 2 + 0];
+        q0 += red[(k * Co + c) * 2 + 1];
+      }
+      prow[c] = s0;
+      prow[Co + c] = q0;
+    }
+    return;
   }
   if constexpr (STATS) {
     if (active) {
@@ -1223,6 +1333,10 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   g.ksplit = 1;
   g.ws = nullptr;
   g.mode = 0;
+  g.bn_y = nullptr;
+  g.bn_mask = nullptr;
+  g.bn_aux = nullptr;
+  g.bn_part = nullptr;
   return g;
 }
 
@@ -1369,10 +1483,10 @@ static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, co
     const int gx = splitk_reduce_grid(M, g.Co, &rpb);
     if (stats)
       hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
-                         rpb, bias, addend, Y, stats);
+                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part);
     else
       hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
-                         rpb, bias, addend, Y, stats);
+                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part);
     return;
   }
   const ConvGeom& g = g0;
@@ -1546,7 +1660,9 @@ bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW,
                          int pad, int groups);
 int conv_c64_stat_rows(int N, int H);
 void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const bf16* addend,
-                     int N, int H, bool dgrad, hipStream_t st);
+                     int N, int H, bool dgrad, hipStream_t st, const bf16* bn_y = nullptr,
+                     const uint8_t* bn_mask = nullptr, const float* bn_aux = nullptr,
+                     float* bn_part = nullptr);
 
 // split-K workspace (floats) the forward / dgrad launch of this geometry will need (0 = none)
 int64_t conv_fwd_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
@@ -1587,6 +1703,36 @@ static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int K
     g.fd_w = make_fastdiv(W / 2);
   }
   return g;
+}
+
+// slab rows the fused BN-backward reduce of this dgrad launch writes (its grid / reduce grid),
+// or 0 when the selected kernel cannot fuse it (the phased 256-row kernel)
+int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                       int groups, int Ho, int Wo) {
+  // the layer-1 c64 kernel runs one workgroup per CU: the y / mask reads of the fused reduce sit
+  // un-overlapped in its epilogue (measured +116 us per call at bs1024 against ~50 us saved), so
+  // its BN keeps the separate reduce pass (the kernel still supports it: PCA_C64_BN_FUSE=1)
+  static const bool c64_fuse = [] {
+    const char* e = getenv("PCA_C64_BN_FUSE");
+    return e && e[0] == '1';
+  }();
+  if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return c64_fuse ? conv_c64_stat_rows(N, H) : 0;
+  const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  if (g.Co % 8 != 0) return 0;
+  if (g.mode == 2) {
+    if (igemm_ws_floats<2>(g) > 0) {
+      int rpb;
+      return splitk_reduce_grid(g.N * g.Ho * g.Wo, g.Co, &rpb);
+    }
+    return igemm_grid_x<2>(g) * 4;
+  }
+  if (ph_cfg<1>(g) >= 0) return 0;
+  if (igemm_ws_floats<1>(g) > 0) {
+    int rpb;
+    return splitk_reduce_grid(g.N * g.Ho * g.Wo, g.Co, &rpb);
+  }
+  return igemm_grid_x<1>(g);
 }
 
 // ---- autotune API (bindings.cpp) ----
@@ -1684,12 +1830,17 @@ void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, f
 // dx = conv^T(dy, W); wt is W transposed to [Cin][KH][KW][Cout/G].
 void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, int W, int Cin,
                        int Cout, int KH, int KW, int stride, int pad, int groups, int Ho, int Wo,
-                       hipStream_t st, const bf16* addend, float* ws) {
+                       hipStream_t st, const bf16* addend, float* ws, const bf16* bn_y,
+                       const uint8_t* bn_mask, const float* bn_aux, float* bn_part) {
   if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
-    conv_c64_launch(dy, wt, dx, nullptr, addend, N, H, true, st);
+    conv_c64_launch(dy, wt, dx, nullptr, addend, N, H, true, st, bn_y, bn_mask, bn_aux, bn_part);
     return;
   }
-  const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  g.bn_y = bn_y;
+  g.bn_mask = bn_mask;
+  g.bn_aux = bn_aux;
+  g.bn_part = bn_part;
   if (g.mode == 2) {
     igemm_dispatch<2>(dy, wt, dx, nullptr, nullptr, g, st, addend, ws);
   } else {

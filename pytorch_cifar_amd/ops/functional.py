@@ -301,14 +301,50 @@ def _prepped_weight(weight, groups, w_phys, need_dx):
     return _C().weight_prep(w_phys, groups, need_dx)
 
 
+# ------------------------------------------------- BN-backward reduce in the dgrad epilogue
+# The BatchNorm+ReLU backward needs per-channel sums of dz and dz*xhat over the whole batch before
+# it can produce dy. When that BN's output feeds an MFMA conv, the conv's dgrad epilogue holds
+# exactly dz's source (the gradient it stores) in registers: it also reads the BN input y and the
+# 1-bit ReLU mask and emits the two sums as slab rows, so the BN backward skips its separate
+# reduce pass (one full read of dout + y + mask) and launch. The sums are used only if the BN's
+# incoming gradient IS that dgrad's output (same storage): any other gradient contribution makes
+# autograd produce a new tensor and the BN falls back to its own reduce.
+_FUSE_BN_BWD = os.environ.get("PCA_FUSE_BN_BWD", "1") != "0"
+
+
+def set_fuse_bn_backward(on: bool) -> None:
+    """Enable/disable the BN-backward reduce fusion into the consumer conv's dgrad epilogue."""
+    global _FUSE_BN_BWD
+    _FUSE_BN_BWD = bool(on)
+
+
+class _BNSrc:
+    __slots__ = ("y", "mask", "aux", "part", "dx")
+
+    def __init__(self, y, mask, aux):
+        self.y, self.mask, self.aux = y, mask, aux
+        self.part = None
+        self.dx = None
+
+
+def _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add):
+    if src is None:
+        return C.conv_dgrad(dy, wt, H, W, stride, padding, groups, add)
+    dx, part = C.conv_dgrad_bn(dy, wt, H, W, stride, padding, groups, add, src.y, src.mask, src.aux)
+    if part.numel():
+        src.part, src.dx = part, dx   # the reference to dx keeps autograd from adding into it
+    return dx
+
+
 class _ConvMFMA(torch.autograd.Function):
     """Implicit-GEMM MFMA conv (fwd + BN-stat epilogue, dgrad, split-K wgrad)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, groups, want_stats, cin_pad, slot=None,
-                owner=False):
+                owner=False, bnsrc=None):
         C = _C()
         ctx.slot, ctx.owner = slot, owner
+        ctx.bnsrc = bnsrc
         w_phys = G.physical(weight)
         if not w_phys.is_contiguous():
             w_phys = w_phys.contiguous()
@@ -335,7 +371,7 @@ class _ConvMFMA(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return (None,) * 10
+            return (None,) * 11
         C = _C()
         x, wt = ctx.saved_tensors
         stride, padding, groups, cin_pad, H, W = ctx.geom
@@ -344,12 +380,16 @@ class _ConvMFMA(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             slot = ctx.slot
+            src = ctx.bnsrc
+            ctx.bnsrc = None
             if slot is not None and ctx.owner:
                 add = slot.take()            # the other branch's dX, summed in the epilogue
-                dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups, add)
+                dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add)
+            elif slot is None:
+                dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, None)
             else:
                 dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
-                if slot is not None and slot.offer(dx):
+                if slot.offer(dx):
                     dx = None                # delivered through the owner's epilogue
         KH, KW = weight.shape[2], weight.shape[3]
         dw_ret = db_ret = None
@@ -381,7 +421,7 @@ class _ConvMFMA(torch.autograd.Function):
                 G.accumulate(bias, db)
             else:
                 db_ret = db
-        return dx, dw_ret, db_ret, None, None, None, None, None, None, None
+        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None
 
 
 class _ConvDirect(torch.autograd.Function):
@@ -485,8 +525,9 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
         return to_nchw(y), None
     if Cg % 8 == 0 and cout_g % 8 == 0:
         slot, owner = _slot_for_conv(x)
+        bnsrc = getattr(x, "_pca_bnsrc", None) if x.requires_grad else None
         y, stats = _ConvMFMA.apply(to_nhwc(x), weight, bias, stride, padding, groups, want_stats, 0,
-                                   slot, owner)
+                                   slot, owner, bnsrc)
         return to_nchw(y), (stats if want_stats else None)
     if groups == 1 and cout_g % 8 == 0 and Cin < 8 * 2 and Cout >= 16:
         # stem conv on 3-channel images: pad channels to 8 and run on MFMA
@@ -522,10 +563,11 @@ def add_bias(y_nhwc, bias):
 
 # -------------------------------------------------------------------------- batch norm
 class _BNCfg:
-    __slots__ = ("bn", "bn2", "act", "training", "count")
+    __slots__ = ("bn", "bn2", "act", "training", "count", "src")
 
     def __init__(self, bn, bn2, act, training, count):
         self.bn, self.bn2, self.act, self.training, self.count = bn, bn2, act, training, count
+        self.src = None
 
 
 def _bn_aux(C, bn, y, stats, training, count):
@@ -565,6 +607,12 @@ class _BatchNormAct(torch.autograd.Function):
         has_mask = mask is not None and mask.numel() > 0
         ctx.save_for_backward(y, out if (relu and not has_mask) else None, mask if has_mask else None,
                               aux, y2, aux2)
+        ctx.bnsrc = None
+        # (grad mode is off inside Function.forward: the caller decided it in cfg.src)
+        if cfg.src is not None and relu and has_mask and y2 is None:
+            ctx.bnsrc = cfg.src = _BNSrc(y, mask, aux)
+        else:
+            cfg.src = None
         return out
 
     @staticmethod
@@ -584,12 +632,20 @@ class _BatchNormAct(torch.autograd.Function):
         g2 = b2 = None
         if bn2 is not None:
             g2, b2 = acc(bn2.weight), acc(bn2.bias)
+        part = None
+        src = ctx.bnsrc
+        if src is not None:
+            if src.part is not None and src.dx is not None and dout.data_ptr() == src.dx.data_ptr() \
+                    and dout.shape == src.dx.shape:
+                part = src.part           # reduced by the consumer conv's dgrad epilogue
+            src.part = src.dx = None
+            ctx.bnsrc = None
         dy, dres, dy2, dg, db, dg2, db2 = C.bn_backward(
             dout, out, mask, y, aux,
             bn.weight.detach() if bn.weight is not None else None,
             y2, aux2,
             bn2.weight.detach() if (bn2 is not None and bn2.weight is not None) else None,
-            ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2)
+            ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2, part)
         ret = {}
 
         def deliver(p, buf, val, slot):
@@ -662,11 +718,16 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
         st2 = residual_bn[2] if len(residual_bn) > 2 else None
         y2 = to_nhwc(xb)
     cfg = _BNCfg(bn, bn2, act, training, N * H * W)
+    if _FUSE_BN_BWD and torch.is_grad_enabled() and training:
+        cfg.src = True                # request: forward replaces it with the _BNSrc record
     out = _BatchNormAct.apply(y, bn.weight, bn.bias, res, y2,
                               bn2.weight if bn2 is not None else None,
                               bn2.bias if bn2 is not None else None, stats, st2, cfg,
                               _slot_for_residual(residual))
-    return to_nchw(out)
+    v = to_nchw(out)
+    if cfg.src is not None:
+        v._pca_bnsrc = cfg.src        # the consumer conv fuses this BN's backward reduce
+    return v
 
 
 # ------------------------------------------------------------------------ activations

@@ -167,3 +167,31 @@ def test_batched_weight_prep_matches_per_conv():
                 m.conv1.weight.mul_(0.5)
                 m.layer2[0].conv1.weight.add_(0.01)
     assert len(b.__dict__["_pca_wplan"].entries) >= 19
+
+
+def test_bn_backward_reduce_fusion_matches_separate_pass():
+    """BN+ReLU backward with its (sum dz, sum dz*xhat) reduced in the consumer conv's dgrad
+    epilogue (igemm, split-K reduce and layer-1 c64 kernels) equals the separate-pass reduce."""
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.ops import functional as PF
+
+    torch.manual_seed(0)
+    base = models.ResNet18().cuda()
+    x = torch.randn(64, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (64,), device="cuda")
+    grads = []
+    try:
+        for fuse in (False, True):
+            PF.set_fuse_bn_backward(fuse)
+            m = copy.deepcopy(base)
+            PF.cross_entropy(m(x), y).backward()
+            torch.cuda.synchronize()
+            grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    finally:
+        PF.set_fuse_bn_backward(True)
+    bad = []
+    for n, g0 in grads[0].items():
+        e = rel(grads[1][n], g0)
+        if e > 2e-2:
+            bad.append((n, round(e, 4)))
+    assert not bad, bad
