@@ -133,6 +133,26 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
     if (t + (int)gridDim.x < g.tiles) issue(t + gridDim.x, buf ^ 1);
     const char* S = smem + buf * HBYTES;
 
+    // epilogue operands of this tile (residual-gradient addend; BN input y + ReLU mask of the
+    // fused backward reduce) are loaded now, so their latency hides under the 18 MFMA steps
+    // instead of sitting in the epilogue of a one-workgroup-per-CU kernel
+    uint4 pre_a[STORES], pre_y[STORES];
+    uint32_t pre_m[STORES];
+    {
+      const int pn = t / tiles_per_img, ph0 = (t - pn * tiles_per_img) * ROWS;
+      const size_t ppix0 = ((size_t)pn * g.H + ph0) * W;
+#pragma unroll
+      for (int q = 0; q < STORES; ++q) {
+        const int idx = tid + q * 256;
+        const size_t o = (ppix0 + (idx >> 3)) * 64 + (idx & 7) * 8;
+        if (addend) pre_a[q] = *reinterpret_cast<const uint4*>(addend + o);
+        if (bnf) {
+          pre_y[q] = *reinterpret_cast<const uint4*>(g.bn_y + o);
+          pre_m[q] = g.bn_mask[o >> 3];
+        }
+      }
+    }
+
     f32x4 acc[4][4];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -209,7 +229,7 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
       if (addend) {
         float a[8], b[8];
         unpack8(v, a);
-        unpack8(*reinterpret_cast<const uint4*>(addend + o), b);
+        unpack8(pre_a[q], b);
 #pragma unroll
         for (int e = 0; e < 8; ++e) a[e] += b[e];
         v = pack8(a);
@@ -217,8 +237,8 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
       if (bnf) {
         float f[8], yy[8];
         unpack8(v, f);
-        unpack8(*reinterpret_cast<const uint4*>(g.bn_y + o), yy);
-        const uint32_t m = g.bn_mask[o >> 3];
+        unpack8(pre_y[q], yy);
+        const uint32_t m = pre_m[q];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float dz = ((m >> e) & 1u) ? f[e] : 0.f;

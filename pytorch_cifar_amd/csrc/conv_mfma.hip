@@ -1709,12 +1709,12 @@ static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int K
 // or 0 when the selected kernel cannot fuse it (the phased 256-row kernel)
 int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo) {
-  // the layer-1 c64 kernel runs one workgroup per CU: the y / mask reads of the fused reduce sit
-  // un-overlapped in its epilogue (measured +116 us per call at bs1024 against ~50 us saved), so
-  // its BN keeps the separate reduce pass (the kernel still supports it: PCA_C64_BN_FUSE=1)
+  // the layer-1 c64 kernel prefetches the fused reduce's y / mask (and the residual addend) at
+  // tile start so they hide under its MFMA loop (read in its one-workgroup-per-CU epilogue they
+  // cost +116 us per call at bs1024); PCA_C64_BN_FUSE=0 keeps the separate reduce for layer 1
   static const bool c64_fuse = [] {
     const char* e = getenv("PCA_C64_BN_FUSE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
     return c64_fuse ? conv_c64_stat_rows(N, H) : 0;
