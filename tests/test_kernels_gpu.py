@@ -322,10 +322,19 @@ def test_depthwise(C, Cin, mult, k, s, H):
     assert rel_err(dw.reshape(Co, 1, k, k), w.grad) < 2e-2
 
 
-def test_se_scale(C):
+@pytest.mark.parametrize("Cc,H", [(48, 4), (1152, 2), (96, 32), (20, 4)])
+def test_se_scale(C, Cc, H):
+    """Squeeze-excite scale fwd/bwd and the global average pool (fwd/bwd) it uses: vectorized
+    8-channel kernels for C % 8 == 0, scalar ones otherwise."""
     torch.manual_seed(6)
-    x = bf(torch.randn(3, 48, 4, 4, device="cuda")).requires_grad_(True)
-    s = torch.randn(3, 48, device="cuda").requires_grad_(True)
+    x = bf(torch.randn(3, Cc, H, H, device="cuda")).requires_grad_(True)
+    s = torch.randn(3, Cc, device="cuda").requires_grad_(True)
+    xn0 = nhwc(x.detach()).bfloat16()
+    pooled = C.gap_fwd(xn0)
+    assert rel_err(pooled, x.detach().mean((2, 3))) < 1e-2
+    gy = torch.randn(3, Cc, device="cuda")
+    gx = C.gap_bwd(gy, H, H)
+    assert rel_err(nchw(gx).float(), (gy / (H * H))[:, :, None, None].expand(3, Cc, H, H)) < 1e-2
     ref = x * torch.sigmoid(s)[:, :, None, None]
     dy = bf(torch.randn_like(ref))
     ref.backward(dy)
