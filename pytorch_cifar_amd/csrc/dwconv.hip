@@ -9,6 +9,7 @@
 // float4 loads. wgrad is a deterministic per-(pixel-chunk, tap) slab reduction.
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace pca {
@@ -188,60 +189,81 @@ __global__ void dw_wgrad_final_kernel(const float* __restrict__ partial, int R, 
 }
 
 // ---------------------------------------------------------------------------------------
-// 3x3 depthwise fast paths (multiplier 1, C % 8 == 0, C <= 2048) — the MobileNet /
-// MobileNetV2 / ShuffleNetV2 / EfficientNet-k3 shapes. The generic kernels above re-load every
-// weight and every tap from L1/L2 per output vector, with 64-bit index math per element, and the
-// generic wgrad runs one block per tap (dY re-read 9x): 2.5-7x off their bandwidth roofline on
-// MobileNetV2 (profiles/). Here a thread owns 8 channels of one output column strip (RPT rows):
-//   * the 3 input rows of the 3x3 window roll down the strip as raw bf16 vectors, so each output
-//     row loads 3 new 16-byte vectors (stride 1) or 6 (stride 2) instead of 9;
-//   * fwd / stride-1 dgrad keep the 9 x 8 fp32 weights in registers (the stride-1 dgrad is the
+// k3 / k5 depthwise fast paths (multiplier 1, stride 1 or 2, "same" padding K/2) — the
+// MobileNet / MobileNetV2 / ShuffleNetV2 / EfficientNet-B0 (k3 and k5, efficientnet.py:70-76)
+// shapes. The generic kernels above re-load every weight and every tap from L1/L2 per output
+// vector, with 64-bit index math per element, and the generic wgrad runs one block per tap
+// (dY re-read K*K times): 2.5-15x off their bandwidth roofline (profiles/). Here a thread owns
+// V channels of one output column strip (RPT rows):
+//   * the K input rows of the KxK window roll down the strip as raw bf16 vectors, so each output
+//     row loads K new vectors (stride 1) or 2K (stride 2) instead of K*K;
+//   * fwd / stride-1 dgrad keep the K*K x V fp32 weights in registers (the stride-1 dgrad is the
 //     same correlation with mirrored taps and pad K-1-p);
-//   * wgrad accumulates all 9 taps x 8 channels in registers across every strip the thread
+//   * wgrad accumulates all K*K taps x V channels in registers across every strip the thread
 //     walks (dY read once), then the threads sharing a channel group are reduced through LDS,
 //     one tap at a time, into one deterministic partial row per block.
+// V = 8 (16-byte vectors) at K = 3; V = 4 (8-byte vectors) at K = 5, so that the 25 x V weights
+// (or accumulators) plus the 25-vector window stay in registers (~170 VGPRs).
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void fma8(float* acc, const uint4& xv, const float* w) {
-  float f[8];
-  unpack8(xv, f);
-#pragma unroll
-  for (int v = 0; v < 8; ++v) acc[v] += f[v] * w[v];
+template <int V> struct DwVec;
+template <> struct DwVec<8> { using T = uint4; };
+template <> struct DwVec<4> { using T = uint2; };
+
+template <int V>
+__device__ __forceinline__ typename DwVec<V>::T dw_zero() {
+  if constexpr (V == 8) return make_uint4(0u, 0u, 0u, 0u);
+  else return make_uint2(0u, 0u);
 }
 
-// the 3 input vectors (kw = 0..2) of row ih for output column ow (zeros outside the image)
-template <int S>
-__device__ __forceinline__ void dw3_load_row(const bf16* xn, const DwGeom& g, int ih, int ow,
-                                             uint4* r) {
-  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+template <int V>
+__device__ __forceinline__ void dw_unpack(const typename DwVec<V>::T& u, float* f) {
+  if constexpr (V == 8) {
+    unpack8(u, f);
+  } else {
+    f[0] = __uint_as_float(u.x << 16);
+    f[1] = __uint_as_float(u.x & 0xffff0000u);
+    f[2] = __uint_as_float(u.y << 16);
+    f[3] = __uint_as_float(u.y & 0xffff0000u);
+  }
+}
+
+template <int V>
+__device__ __forceinline__ typename DwVec<V>::T dw_pack(const float* f) {
+  if constexpr (V == 8) return pack8(f);
+  else return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
+}
+
+// the K vectors (kw = 0..K-1) of input row ih starting at column iw0 (zeros outside the image)
+template <int K, int V>
+__device__ __forceinline__ void dwk_load_row(const bf16* xn, const DwGeom& g, int ih, int iw0,
+                                             typename DwVec<V>::T* r) {
+  using T = typename DwVec<V>::T;
   const bool rok = (unsigned)ih < (unsigned)g.H;
-  const int iw0 = ow * S - g.p;
 #pragma unroll
-  for (int kw = 0; kw < 3; ++kw) {
+  for (int kw = 0; kw < K; ++kw) {
     const int iw = iw0 + kw;
     r[kw] = (rok && (unsigned)iw < (unsigned)g.W)
-                ? *reinterpret_cast<const uint4*>(xn + ((size_t)ih * g.W + iw) * g.C)
-                : zero;
+                ? *reinterpret_cast<const T*>(xn + ((size_t)ih * g.W + iw) * g.C)
+                : dw_zero<V>();
   }
 }
 
-template <int S>
-__device__ __forceinline__ void dw3_roll(uint4 (&win)[3][3]) {
+// advance the window by S input rows: rows S..K-1 move up, rows K-S..K-1 are reloaded
+template <int K, int S, typename T>
+__device__ __forceinline__ void dwk_roll(T (&win)[K][K]) {
 #pragma unroll
-  for (int kw = 0; kw < 3; ++kw) {
-    if constexpr (S == 1) {
-      win[0][kw] = win[1][kw];
-      win[1][kw] = win[2][kw];
-    } else {
-      win[0][kw] = win[2][kw];
-    }
-  }
+  for (int k = 0; k + S < K; ++k)
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw) win[k][kw] = win[k + S][kw];
 }
 
-template <int S, bool FLIP>
-__global__ __launch_bounds__(256) void dw3_fwd_kernel(const bf16* __restrict__ x,
+template <int K, int S, int V, bool FLIP>
+__global__ __launch_bounds__(256) void dwk_fwd_kernel(const bf16* __restrict__ x,
                                                       const float* __restrict__ wT, DwGeom g,
                                                       int rpt, bf16* __restrict__ y) {
-  const int G = g.C >> 3;
+  using T = typename DwVec<V>::T;
+  constexpr int KK = K * K;
+  const int G = g.C / V;
   const int nstrip = (g.Ho + rpt - 1) / rpt;
   const int total = g.N * nstrip * g.Wo * G;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
@@ -251,106 +273,121 @@ __global__ __launch_bounds__(256) void dw3_fwd_kernel(const bf16* __restrict__ x
     q /= g.Wo;
     const int strip = q % nstrip;
     const int n = q / nstrip;
-    const int c = gi * 8;
-    float w[9][8];
+    const int c = gi * V;
+    float w[KK][V];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int src = FLIP ? 8 - t : t;
-      const float4 w0 = *reinterpret_cast<const float4*>(wT + src * g.Co + c);
-      const float4 w1 = *reinterpret_cast<const float4*>(wT + src * g.Co + c + 4);
-      w[t][0] = w0.x; w[t][1] = w0.y; w[t][2] = w0.z; w[t][3] = w0.w;
-      w[t][4] = w1.x; w[t][5] = w1.y; w[t][6] = w1.z; w[t][7] = w1.w;
+    for (int t = 0; t < KK; ++t) {
+      const int src = FLIP ? KK - 1 - t : t;
+#pragma unroll
+      for (int v4 = 0; v4 < V; v4 += 4) {
+        const float4 wv = *reinterpret_cast<const float4*>(wT + src * g.Co + c + v4);
+        w[t][v4] = wv.x; w[t][v4 + 1] = wv.y; w[t][v4 + 2] = wv.z; w[t][v4 + 3] = wv.w;
+      }
     }
     const bf16* xn = x + (size_t)n * g.H * g.W * g.C + c;
     const int oh0 = strip * rpt, oh1 = min(g.Ho, oh0 + rpt);
-    uint4 win[3][3];
-    dw3_load_row<S>(xn, g, oh0 * S - g.p, ow, win[0]);
-    if constexpr (S == 1) dw3_load_row<S>(xn, g, oh0 * S - g.p + 1, ow, win[1]);
+    const int iw0 = ow * S - g.p;
+    T win[K][K];
+#pragma unroll
+    for (int k = 0; k < K - S; ++k) dwk_load_row<K, V>(xn, g, oh0 * S - g.p + k, iw0, win[k]);
     bf16* yr = y + (((size_t)n * g.Ho + oh0) * g.Wo + ow) * g.Co + c;
     for (int oh = oh0; oh < oh1; ++oh) {
       const int ih0 = oh * S - g.p;
-      if constexpr (S == 2) dw3_load_row<S>(xn, g, ih0 + 1, ow, win[1]);
-      dw3_load_row<S>(xn, g, ih0 + 2, ow, win[2]);
-      float acc[8];
 #pragma unroll
-      for (int v = 0; v < 8; ++v) acc[v] = 0.f;
+      for (int k = K - S; k < K; ++k) dwk_load_row<K, V>(xn, g, ih0 + k, iw0, win[k]);
+      float acc[V];
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
+      for (int v = 0; v < V; ++v) acc[v] = 0.f;
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) fma8(acc, win[kh][kw], w[kh * 3 + kw]);
-      *reinterpret_cast<uint4*>(yr) = pack8(acc);
+      for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) {
+          float f[V];
+          dw_unpack<V>(win[kh][kw], f);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[v] += f[v] * w[kh * K + kw][v];
+        }
+      *reinterpret_cast<T*>(yr) = dw_pack<V>(acc);
       yr += (size_t)g.Wo * g.Co;
-      dw3_roll<S>(win);
+      dwk_roll<K, S>(win);
     }
   }
 }
 
-// partial[block][tap][Co]: thread t owns channel group t % G and walks the column strips
-// item = blockIdx.x * W + t / G (+ gridDim.x * W ...), W = 256 / G workers per block
-template <int S>
-__global__ __launch_bounds__(256) void dw3_wgrad_kernel(const bf16* __restrict__ x,
+// partial[block.x][tap][Co]: block (x, y) owns channel groups [y*GB, y*GB + GB) (GB <= 256);
+// thread t owns group y*GB + t % GB and walks the column strips item = x*W + t/GB (+ gridDim.x*W
+// ...), W = 256 / GB workers per group
+template <int K, int S, int V>
+__global__ __launch_bounds__(256) void dwk_wgrad_kernel(const bf16* __restrict__ x,
                                                         const bf16* __restrict__ dy, DwGeom g,
-                                                        int rpt, float* __restrict__ partial) {
-  __shared__ float red[256 * 8];
-  const int G = g.Co >> 3;
-  const int W = 256 / G;
+                                                        int rpt, int GB,
+                                                        float* __restrict__ partial) {
+  using T = typename DwVec<V>::T;
+  constexpr int KK = K * K;
+  __shared__ float red[256 * V];
+  const int G = g.Co / V;
+  const int gb0 = blockIdx.y * GB;
+  const int Gl = min(GB, G - gb0);
+  const int W = 256 / GB;
   const int t = threadIdx.x;
-  const int gi = t % G, wk = t / G;
-  const int c = gi * 8;
+  const int gl = t % GB, wk = t / GB;
+  const int c = (gb0 + gl) * V;
   const int nstrip = (g.Ho + rpt - 1) / rpt;
   const int items = g.N * nstrip * g.Wo;
-  float acc[9][8];
+  float acc[KK][V];
 #pragma unroll
-  for (int k = 0; k < 9; ++k)
+  for (int k = 0; k < KK; ++k)
 #pragma unroll
-    for (int v = 0; v < 8; ++v) acc[k][v] = 0.f;
-  if (wk < W) {
+    for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
+  if (wk < W && gl < Gl) {
     for (int item = blockIdx.x * W + wk; item < items; item += gridDim.x * W) {
       const int ow = item % g.Wo;
       const int q = item / g.Wo;
       const int strip = q % nstrip, n = q / nstrip;
       const bf16* xn = x + (size_t)n * g.H * g.W * g.C + c;
       const int oh0 = strip * rpt, oh1 = min(g.Ho, oh0 + rpt);
-      uint4 win[3][3];
-      dw3_load_row<S>(xn, g, oh0 * S - g.p, ow, win[0]);
-      if constexpr (S == 1) dw3_load_row<S>(xn, g, oh0 * S - g.p + 1, ow, win[1]);
+      const int iw0 = ow * S - g.p;
+      T win[K][K];
+#pragma unroll
+      for (int k = 0; k < K - S; ++k) dwk_load_row<K, V>(xn, g, oh0 * S - g.p + k, iw0, win[k]);
       const bf16* dr = dy + (((size_t)n * g.Ho + oh0) * g.Wo + ow) * g.Co + c;
       for (int oh = oh0; oh < oh1; ++oh) {
         const int ih0 = oh * S - g.p;
-        if constexpr (S == 2) dw3_load_row<S>(xn, g, ih0 + 1, ow, win[1]);
-        dw3_load_row<S>(xn, g, ih0 + 2, ow, win[2]);
-        float d[8];
-        unpack8(*reinterpret_cast<const uint4*>(dr), d);
+#pragma unroll
+        for (int k = K - S; k < K; ++k) dwk_load_row<K, V>(xn, g, ih0 + k, iw0, win[k]);
+        float d[V];
+        dw_unpack<V>(*reinterpret_cast<const T*>(dr), d);
         dr += (size_t)g.Wo * g.Co;
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
+        for (int kh = 0; kh < K; ++kh)
 #pragma unroll
-          for (int kw = 0; kw < 3; ++kw) {
-            float f[8];
-            unpack8(win[kh][kw], f);
+          for (int kw = 0; kw < K; ++kw) {
+            float f[V];
+            dw_unpack<V>(win[kh][kw], f);
 #pragma unroll
-            for (int v = 0; v < 8; ++v) acc[kh * 3 + kw][v] += f[v] * d[v];
+            for (int v = 0; v < V; ++v) acc[kh * K + kw][v] += f[v] * d[v];
           }
-        dw3_roll<S>(win);
+        dwk_roll<K, S>(win);
       }
     }
   }
-  float* prow = partial + (size_t)blockIdx.x * 9 * g.Co;
+  float* prow = partial + (size_t)blockIdx.x * KK * g.Co;
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
+  for (int k = 0; k < KK; ++k) {
 #pragma unroll
-    for (int v = 0; v < 8; ++v) red[t * 8 + v] = acc[k][v];
+    for (int v = 0; v < V; ++v) red[t * V + v] = acc[k][v];
     __syncthreads();
-    if (t < G) {
-      float s[8];
+    if (t < Gl) {
+      float s[V];
 #pragma unroll
-      for (int v = 0; v < 8; ++v) s[v] = red[t * 8 + v];
+      for (int v = 0; v < V; ++v) s[v] = red[t * V + v];
       for (int j = 1; j < W; ++j)
 #pragma unroll
-        for (int v = 0; v < 8; ++v) s[v] += red[(j * G + t) * 8 + v];
-      float4* o = reinterpret_cast<float4*>(prow + (size_t)k * g.Co + c);
-      o[0] = make_float4(s[0], s[1], s[2], s[3]);
-      o[1] = make_float4(s[4], s[5], s[6], s[7]);
+        for (int v = 0; v < V; ++v) s[v] += red[(j * GB + t) * V + v];
+      float4* o = reinterpret_cast<float4*>(prow + (size_t)k * g.Co + (gb0 + t) * V);
+#pragma unroll
+      for (int v4 = 0; v4 < V / 4; ++v4)
+        o[v4] = make_float4(s[4 * v4], s[4 * v4 + 1], s[4 * v4 + 2], s[4 * v4 + 3]);
     }
     __syncthreads();
   }
@@ -391,34 +428,58 @@ static int gcap(size_t work) {
   return (int)(b < 8192 ? (b ? b : 1) : 8192);
 }
 
-static bool dw3_ok(const DwGeom& g) {
+// K of the fast path (3 or 5) this geometry takes, 0 = generic kernels
+static int dwk_kind(const DwGeom& g) {
   static const bool off = [] {
     const char* e = getenv("PCA_DW3");
     return e && e[0] == '0';
   }();
-  return !off && g.mult == 1 && g.C % 8 == 0 && g.C <= 2048 && g.KH == 3 && g.KW == 3 &&
-         g.p == 1 && (g.s == 1 || g.s == 2);
+  if (off || g.mult != 1 || g.KH != g.KW || (g.s != 1 && g.s != 2)) return 0;
+  if (g.KH == 3 && g.p == 1 && g.C % 8 == 0) return 3;
+  if (g.KH == 5 && g.p == 2 && g.C % 4 == 0) return 5;
+  return 0;
 }
 
-static int dw3_rpt(int Ho) { return Ho < 8 ? Ho : 8; }
+static int dwk_rpt(int Ho) { return Ho < 8 ? Ho : 8; }
 
-static void dw3_fwd(const bf16* x, const float* wT, const DwGeom& g, bool flip, bf16* y,
-                    hipStream_t st) {
-  const int rpt = dw3_rpt(g.Ho);
-  const size_t work = (size_t)g.N * cdiv(g.Ho, rpt) * g.Wo * (g.C / 8);
+template <int K, int V>
+static void dwk_fwd_t(const bf16* x, const float* wT, const DwGeom& g, bool flip, bf16* y,
+                      hipStream_t st) {
+  const int rpt = dwk_rpt(g.Ho);
+  const size_t work = (size_t)g.N * cdiv(g.Ho, rpt) * g.Wo * (g.C / V);
   const dim3 grid(gcap(work)), block(256);
   if (g.s == 1) {
-    if (flip) hipLaunchKernelGGL((dw3_fwd_kernel<1, true>), grid, block, 0, st, x, wT, g, rpt, y);
-    else hipLaunchKernelGGL((dw3_fwd_kernel<1, false>), grid, block, 0, st, x, wT, g, rpt, y);
+    if (flip) hipLaunchKernelGGL((dwk_fwd_kernel<K, 1, V, true>), grid, block, 0, st, x, wT, g, rpt, y);
+    else hipLaunchKernelGGL((dwk_fwd_kernel<K, 1, V, false>), grid, block, 0, st, x, wT, g, rpt, y);
   } else {
-    hipLaunchKernelGGL((dw3_fwd_kernel<2, false>), grid, block, 0, st, x, wT, g, rpt, y);
+    hipLaunchKernelGGL((dwk_fwd_kernel<K, 2, V, false>), grid, block, 0, st, x, wT, g, rpt, y);
   }
+}
+
+static void dwk_fwd(int kind, const bf16* x, const float* wT, const DwGeom& g, bool flip, bf16* y,
+                    hipStream_t st) {
+  if (kind == 3) dwk_fwd_t<3, 8>(x, wT, g, flip, y, st);
+  else dwk_fwd_t<5, 4>(x, wT, g, flip, y, st);
+}
+
+template <int K, int V>
+static void dwk_wgrad_t(const bf16* x, const bf16* dy, const DwGeom& g, int chunks,
+                        float* partial, hipStream_t st) {
+  const int G = g.Co / V;
+  const int ny = cdiv(G, 256);
+  const int GB = cdiv(G, ny);
+  const int rpt = dwk_rpt(g.Ho);
+  const dim3 grid(chunks, ny), block(256);
+  if (g.s == 1)
+    hipLaunchKernelGGL((dwk_wgrad_kernel<K, 1, V>), grid, block, 0, st, x, dy, g, rpt, GB, partial);
+  else
+    hipLaunchKernelGGL((dwk_wgrad_kernel<K, 2, V>), grid, block, 0, st, x, dy, g, rpt, GB, partial);
 }
 
 void dw_fwd_launch(const bf16* x, const float* wT, int N, int H, int W, int C, int Ho, int Wo,
                    int Co, int KH, int KW, int s, int p, bf16* y, hipStream_t st) {
   DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
-  if (dw3_ok(g)) return dw3_fwd(x, wT, g, false, y, st);
+  if (const int kind = dwk_kind(g)) return dwk_fwd(kind, x, wT, g, false, y, st);
   if (g.mult == 1 && C % 8 == 0)
     hipLaunchKernelGGL(dw_fwd_kernel<8>, dim3(gcap((size_t)N * Ho * Wo * Co / 8)), dim3(256), 0, st,
                        x, wT, g, y);
@@ -430,10 +491,11 @@ void dw_fwd_launch(const bf16* x, const float* wT, int N, int H, int W, int C, i
 void dw_dgrad_launch(const bf16* dy, const float* wT, int N, int H, int W, int C, int Ho, int Wo,
                      int Co, int KH, int KW, int s, int p, bf16* dx, hipStream_t st) {
   DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
-  if (dw3_ok(g) && s == 1) {
+  const int kind = dwk_kind(g);
+  if (kind && s == 1) {
     // stride-1 dgrad = forward correlation of dY with the mirrored taps (pad K-1-p)
     const DwGeom gd = dwg(N, Ho, Wo, Co, H, W, C, KH, KW, 1, KH - 1 - p);
-    return dw3_fwd(dy, wT, gd, true, dx, st);
+    return dwk_fwd(kind, dy, wT, gd, true, dx, st);
   }
   if (g.mult == 1 && C % 8 == 0)
     hipLaunchKernelGGL(dw_dgrad_kernel<8>, dim3(gcap((size_t)N * H * W * C / 8)), dim3(256), 0, st,
@@ -443,9 +505,12 @@ void dw_dgrad_launch(const bf16* dy, const float* wT, int N, int H, int W, int C
                        wT, g, dx);
 }
 
+// partial rows = grid.x of the wgrad kernels: one per 256 output pixels, but at least 256 (one
+// block per CU) so the small late-stage maps (EfficientNet 2x2 / 4x4: P = 4-16K) still fill the
+// chip, and at most 1024 (the final reduce reads rows x taps x Co floats)
 int dw_wgrad_partials(int N, int Ho, int Wo) {
   const int P = N * Ho * Wo;
-  int chunks = cdiv(P, 256);
+  int chunks = std::max(cdiv(P, 256), std::min(256, P));
   return chunks > 1024 ? 1024 : chunks;
 }
 
@@ -456,13 +521,10 @@ void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, 
   const int P = N * Ho * Wo;
   const int rows = cdiv(P, chunks);
   const int T = KH * KW;
-  if (dw3_ok(g) && Co / 8 <= 256) {
-    // chunks = partial rows = blocks of the strip-walking kernel
-    const int rpt = dw3_rpt(Ho);
-    if (s == 1)
-      hipLaunchKernelGGL(dw3_wgrad_kernel<1>, dim3(chunks), dim3(256), 0, st, x, dy, g, rpt, partial);
-    else
-      hipLaunchKernelGGL(dw3_wgrad_kernel<2>, dim3(chunks), dim3(256), 0, st, x, dy, g, rpt, partial);
+  if (const int kind = dwk_kind(g)) {
+    // chunks = partial rows = blocks (grid.x) of the strip-walking kernel
+    if (kind == 3) dwk_wgrad_t<3, 8>(x, dy, g, chunks, partial, st);
+    else dwk_wgrad_t<5, 4>(x, dy, g, chunks, partial, st);
     hipLaunchKernelGGL(dw_wgrad_final4_kernel, dim3(cdiv(T * Co, 32)), dim3(256), 0, st, partial,
                        chunks, T, Co, dw);
     return;

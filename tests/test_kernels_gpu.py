@@ -299,10 +299,13 @@ def test_pools_and_gap(C):
 @pytest.mark.parametrize("Cin,mult,k,s,H", [(32, 1, 3, 1, 16), (144, 1, 3, 2, 16), (240, 1, 5, 1, 16),
                                             (44, 2, 7, 2, 16), (58, 1, 3, 2, 16), (96, 1, 3, 1, 16),
                                             (1152, 1, 3, 1, 4), (192, 1, 3, 2, 8), (72, 1, 3, 2, 7),
-                                            (24, 1, 3, 1, 9)])
+                                            (24, 1, 3, 1, 9), (144, 1, 5, 2, 16), (36, 1, 5, 1, 8),
+                                            (1152, 1, 5, 1, 2), (672, 1, 5, 2, 4), (2304, 1, 3, 1, 4),
+                                            (20, 1, 5, 1, 6)])
 def test_depthwise(C, Cin, mult, k, s, H):
-    """k3 / multiplier 1 / C % 8 == 0 takes the rolling-window fast paths (dw3_*), the rest the
-    generic kernels; both against torch's fp32 grouped conv."""
+    """Multiplier 1 with k3 (C % 8 == 0) or k5 (C % 4 == 0) takes the rolling-window fast paths
+    (dwk_*, incl. > 256 channel groups split over grid.y in wgrad), the rest the generic
+    kernels; both against torch's fp32 grouped conv."""
     torch.manual_seed(5)
     N = 2
     p = (k - 1) // 2

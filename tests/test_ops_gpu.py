@@ -120,8 +120,24 @@ GPU_ZOO = ["LeNet", "VGG11", "PreActResNet18", "GoogLeNet", "densenet_cifar", "R
            "ShuffleNetV2_1", "ResNet50"]
 
 
+@pytest.fixture
+def reproducible_convs():
+    """Static tile heuristic + deterministic reductions: the timing-based autotuner may pick a
+    different (equally valid, separately tested) tile/split per run, which moves bf16 rounding
+    around; near-cancelling gradients (SE biases) then pass or fail by chance."""
+    from pytorch_cifar_amd import _native
+
+    C = _native.lib()
+    at, det = C.conv_autotune_enabled(), C.deterministic()
+    C.conv_autotune(False)
+    C.set_deterministic(True)
+    yield
+    C.conv_autotune(at)
+    C.set_deterministic(det)
+
+
 @pytest.mark.parametrize("name", GPU_ZOO)
-def test_zoo_matches_reference(name):
+def test_zoo_matches_reference(name, reproducible_convs):
     """Every model family through the native kernels: as close to fp32 as stock bf16."""
     from pytorch_cifar_amd import models
 
