@@ -104,7 +104,7 @@ void dw_dgrad_launch(const bf16*, const float*, int, int, int, int, int, int, in
                      int, bf16*, hipStream_t);
 int dw_wgrad_partials(int, int, int);
 void dw_wgrad_launch(const bf16*, const bf16*, int, int, int, int, int, int, int, int, int, int,
-                     int, float*, int, float*, float*, hipStream_t);
+                     int, float*, int, int, float*, hipStream_t);
 // conv_direct.hip
 void direct_fwd_launch(const bf16*, const float*, const float*, int, int, int, int, int, int, int,
                        int, int, int, int, int, bf16*, hipStream_t);
@@ -756,7 +756,10 @@ Tensor dw_dgrad(const Tensor& dy, const Tensor& wT, int H, int W, int C, int KH,
 }
 
 // returns dw fp32 [Cout, KH*KW]
-Tensor dw_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride, int pad) {
+// dW [Co, KH*KW] fp32; with `accum` given (fp32, Co*KH*KW contiguous, e.g. the parameter's view
+// of the gradient arena) the result is added into it by the final reduce and `accum` returned
+Tensor dw_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride, int pad,
+                const optional<Tensor>& accum) {
   check_bf16(x, "x");
   check_bf16(dy, "dy");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -765,9 +768,18 @@ Tensor dw_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride, i
   const int chunks = pca::dw_wgrad_partials(N, Ho, Wo);
   auto fopt = x.options().dtype(at::kFloat);
   auto partial = at::empty({chunks, KH * KW, Co}, fopt);
-  auto dw = at::empty({Co, KH * KW}, fopt);
+  Tensor dw;
+  if (accum.has_value() && accum->defined()) {
+    dw = *accum;
+    TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.is_contiguous() && dw.numel() == (int64_t)Co * KH * KW &&
+                    dw.device() == x.device(),
+                "dw_wgrad: accum must be a contiguous fp32 [Co*KH*KW] tensor on the input's device");
+  } else {
+    dw = at::empty({Co, KH * KW}, fopt);
+  }
   pca::dw_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad,
-                       ptr<float>(partial), chunks, nullptr, ptr<float>(dw), cur_stream());
+                       ptr<float>(partial), chunks, accum.has_value() && accum->defined() ? 1 : 0,
+                       ptr<float>(dw), cur_stream());
   return dw;
 }
 
@@ -883,7 +895,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_act", &add_act);
   m.def("dw_fwd", &dw_fwd);
   m.def("dw_dgrad", &dw_dgrad);
-  m.def("dw_wgrad", &dw_wgrad);
+  m.def("dw_wgrad", &dw_wgrad, py::arg("x"), py::arg("dy"), py::arg("KH"), py::arg("KW"),
+        py::arg("stride"), py::arg("pad"), py::arg("accum") = py::none());
   m.def("direct_fwd", &direct_fwd);
   m.def("direct_dgrad", &direct_dgrad);
   m.def("direct_wgrad", &direct_wgrad);

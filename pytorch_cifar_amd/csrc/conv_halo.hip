@@ -328,7 +328,9 @@ void set_deterministic_conv(bool on) { g_deterministic = on; }
 bool deterministic_conv() { return g_deterministic; }
 
 // Forced split-K plan for the wgrad kernels (autotuner trials / tuned choices): splits >= 1
-// replaces the occupancy-derived split count and forces fp32 atomics (non-deterministic mode).
+// replaces the occupancy-derived split count and forces fp32 atomics (non-deterministic mode);
+// splits <= -2 fixes the count at -splits with deterministic slab rows (autotune candidates that
+// trade parallelism against slab traffic, which does not shrink with the batch).
 static int g_wsplit = -1;
 void set_wgrad_split(int splits) { g_wsplit = splits; }
 int wgrad_split_force() { return g_deterministic ? -1 : g_wsplit; }
@@ -376,11 +378,13 @@ static int64_t halo_plan(HaloGeom& g) {
   splits = std::min(splits, std::max(1, cdiv(g.P, 256)));
   const int forced = wgrad_split_force();
   if (forced >= 1) splits = std::min(forced, std::max(1, cdiv(g.P, 32)));
+  if (forced <= -2) splits = std::min(-forced, std::max(1, cdiv(g.P, 32)));   // slab, fixed count
   int chunk = cdiv(cdiv(g.P, splits), 32) * 32;
   splits = cdiv(g.P, chunk);
   g.chunk = chunk;
   g.splits = splits;
-  g.atomic = (!g_deterministic && (splits <= 4 || forced >= 1)) ? 1 : 0;
+  g.atomic = (splits == 1 || (!g_deterministic && forced >= 1) ||
+              (!g_deterministic && forced == -1 && splits <= 4)) ? 1 : 0;
   static const bool verbose = getenv("PCA_CONV_VERBOSE") != nullptr;
   if (verbose)
     fprintf(stderr, "[pca] halo wgrad W=%d MB=%d waves=%d: occ=%d cus=%d tiles=%d splits=%d chunk=%d atomic=%d\n",

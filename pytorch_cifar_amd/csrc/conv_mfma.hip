@@ -1938,12 +1938,13 @@ static int64_t wide_plan(WgradGeom& g) {
   splits = std::min(splits, std::max(1, cdiv(g.P, 256)));
   const int forced = wgrad_split_force();
   if (forced >= 1) splits = std::min(forced, std::max(1, cdiv(g.P, 32)));
+  if (forced <= -2) splits = std::min(-forced, std::max(1, cdiv(g.P, 32)));   // slab, fixed count
   int chunk = cdiv(cdiv(g.P, splits), 32) * 32;
   splits = cdiv(g.P, chunk);
   g.chunk = chunk;
   g.splits = splits;
   // few partials per output: atomics; many: slab rows + one ordered reduce
-  g.atomic = (!deterministic_conv() && (splits <= 8 || forced >= 1)) ? 1 : 0;
+  g.atomic = (!deterministic_conv() && (forced >= 1 || (forced == -1 && splits <= 8))) ? 1 : 0;
   return g.atomic ? 0 : slab_ws_floats(splits, (int64_t)g.groups * g.cout_g * g.Ktot);
 }
 
@@ -2069,8 +2070,9 @@ std::vector<std::pair<int, int>> wgrad_tune_candidates(int N, int H, int W, int 
   const int64_t P = (int64_t)N * ((H + 2 * pad - KH) / stride + 1) * ((W + 2 * pad - KW) / stride + 1);
   std::vector<std::pair<int, int>> c;
   for (int cfg : cfgs)
-    for (int sp : {-1, 1, 2, 4, 8, 16, 32}) {
+    for (int sp : {-1, 1, 2, 4, 8, 16, 32, -2, -4, -8}) {
       if (sp > 1 && P / sp < 256) continue;
+      if (sp <= -2 && (cfg < 16 || P / -sp < 256)) continue;   // slab counts: halo / wide only
       c.emplace_back(cfg, sp);
     }
   return c;

@@ -393,11 +393,57 @@ __global__ __launch_bounds__(256) void dwk_wgrad_kernel(const bf16* __restrict__
   }
 }
 
+// stride-2 dgrad (multiplier 1, C % 8 == 0): dx[ih, iw] only meets the taps kh = (ih + p) & 1
+// (+2 ...) — the output rows oh = (ih + p - kh) / 2 are exact — so each thread walks just those
+// (<= ceil(K/2)^2) taps of its 8 channels with 32-bit indexing, instead of testing all K*K taps
+// for divisibility with 64-bit math as the generic kernel does.
+template <int K>
+__global__ __launch_bounds__(256) void dwk_dgrad_s2_kernel(const bf16* __restrict__ dy,
+                                                           const float* __restrict__ wT, DwGeom g,
+                                                           bf16* __restrict__ dx) {
+  const int G = g.C >> 3;
+  const int total = g.N * g.H * g.W * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G;
+    int q = i / G;
+    const int iw = q % g.W;
+    q /= g.W;
+    const int ih = q % g.H;
+    const int n = q / g.H;
+    const int c = gi * 8;
+    float acc[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) acc[v] = 0.f;
+    const int kh0 = (ih + g.p) & 1, kw0 = (iw + g.p) & 1;
+    const bf16* dyn = dy + (size_t)n * g.Ho * g.Wo * g.Co + c;
+#pragma unroll
+    for (int th = 0; th < (K + 1) / 2; ++th) {
+      const int kh = kh0 + 2 * th;
+      const int oh = (ih + g.p - kh) >> 1;
+      if (kh >= K || (unsigned)oh >= (unsigned)g.Ho) continue;
+#pragma unroll
+      for (int tw = 0; tw < (K + 1) / 2; ++tw) {
+        const int kw = kw0 + 2 * tw;
+        const int ow = (iw + g.p - kw) >> 1;
+        if (kw >= K || (unsigned)ow >= (unsigned)g.Wo) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(dyn + (oh * g.Wo + ow) * g.Co), f);
+        const float* wr = wT + (kh * K + kw) * g.Co + c;
+        const float4 w0 = *reinterpret_cast<const float4*>(wr);
+        const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
+        acc[0] += f[0] * w0.x; acc[1] += f[1] * w0.y; acc[2] += f[2] * w0.z; acc[3] += f[3] * w0.w;
+        acc[4] += f[4] * w1.x; acc[5] += f[5] * w1.y; acc[6] += f[6] * w1.z; acc[7] += f[7] * w1.w;
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + (size_t)i * 8) = pack8(acc);
+  }
+}
+
 // dw[co][tap] = sum_r partial[r][tap][co]: 32 columns x 8 row lanes per block, lanes added in
 // a fixed order (deterministic)
 __global__ __launch_bounds__(256) void dw_wgrad_final4_kernel(const float* __restrict__ partial,
                                                               int R, int T, int Co,
-                                                              float* __restrict__ dw) {
+                                                              float* __restrict__ dw, int accum) {
   __shared__ float red[8][32];
   const int cl = threadIdx.x & 31, l = threadIdx.x >> 5;
   const int idx = blockIdx.x * 32 + cl;
@@ -414,7 +460,8 @@ __global__ __launch_bounds__(256) void dw_wgrad_final4_kernel(const float* __res
 #pragma unroll
     for (int k = 0; k < 8; ++k) o += red[k][cl];
     const int tap = idx / Co, co = idx - tap * Co;
-    dw[(size_t)co * T + tap] = o;
+    float* d = dw + (size_t)co * T + tap;
+    *d = accum ? *d + o : o;   // accum: straight into the gradient arena (no separate add)
   }
 }
 
@@ -497,6 +544,12 @@ void dw_dgrad_launch(const bf16* dy, const float* wT, int N, int H, int W, int C
     const DwGeom gd = dwg(N, Ho, Wo, Co, H, W, C, KH, KW, 1, KH - 1 - p);
     return dwk_fwd(kind, dy, wT, gd, true, dx, st);
   }
+  if (kind && C % 8 == 0) {   // stride 2: parity-exact taps
+    const dim3 grid(gcap((size_t)N * H * W * C / 8)), block(256);
+    if (kind == 3) hipLaunchKernelGGL(dwk_dgrad_s2_kernel<3>, grid, block, 0, st, dy, wT, g, dx);
+    else hipLaunchKernelGGL(dwk_dgrad_s2_kernel<5>, grid, block, 0, st, dy, wT, g, dx);
+    return;
+  }
   if (g.mult == 1 && C % 8 == 0)
     hipLaunchKernelGGL(dw_dgrad_kernel<8>, dim3(gcap((size_t)N * H * W * C / 8)), dim3(256), 0, st,
                        dy, wT, g, dx);
@@ -516,7 +569,7 @@ int dw_wgrad_partials(int N, int Ho, int Wo) {
 
 void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, int Ho, int Wo,
                      int Co, int KH, int KW, int s, int p, float* partial, int chunks,
-                     float* partial2, float* dw, hipStream_t st) {
+                     int accum, float* dw, hipStream_t st) {
   DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
   const int P = N * Ho * Wo;
   const int rows = cdiv(P, chunks);
@@ -526,7 +579,7 @@ void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, 
     if (kind == 3) dwk_wgrad_t<3, 8>(x, dy, g, chunks, partial, st);
     else dwk_wgrad_t<5, 4>(x, dy, g, chunks, partial, st);
     hipLaunchKernelGGL(dw_wgrad_final4_kernel, dim3(cdiv(T * Co, 32)), dim3(256), 0, st, partial,
-                       chunks, T, Co, dw);
+                       chunks, T, Co, dw, accum);
     return;
   }
   if (g.mult == 1 && Co % 8 == 0)
@@ -536,8 +589,7 @@ void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, 
     hipLaunchKernelGGL(dw_wgrad_kernel<1>, dim3(chunks, T), dim3(256), 0, st, x, dy, g, rows,
                        partial);
   hipLaunchKernelGGL(dw_wgrad_final4_kernel, dim3(cdiv(T * Co, 32)), dim3(256), 0, st, partial,
-                     chunks, T, Co, dw);
-  (void)partial2;
+                     chunks, T, Co, dw, accum);
 }
 
 }  // namespace pca

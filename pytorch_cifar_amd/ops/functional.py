@@ -492,11 +492,18 @@ class _ConvDepthwise(torch.autograd.Function):
         w = ctx.weight
         dw_ret = None
         if w.requires_grad:
-            dw = C.dw_wgrad(x, dy, KH, KW, stride, padding)  # [Co, KH*KW]
-            if w.is_leaf:
-                G.accumulate(w, dw.view(w.shape[0], KH, KW, 1))
+            buf = G.grad_buffer(w) if w.is_leaf else None
+            if buf is not None and buf.is_contiguous():
+                # channels_last [Co,1,KH,KW] == physical [Co][KH][KW]: the final reduce adds into
+                # the arena view directly
+                C.dw_wgrad(x, dy, KH, KW, stride, padding, buf.view(-1))
+                G.fire(w)
             else:
-                dw_ret = dw.view(w.shape)
+                dw = C.dw_wgrad(x, dy, KH, KW, stride, padding)  # [Co, KH*KW]
+                if w.is_leaf:
+                    G.accumulate(w, dw.view(w.shape[0], KH, KW, 1))
+                else:
+                    dw_ret = dw.view(w.shape)
         return dx, dw_ret, None, None
 
 
