@@ -226,6 +226,94 @@ __global__ void maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* _
   }
 }
 
+// 8-channel vectorized max pool (C % 8 == 0): one thread per 8 channels of one output (fwd) or
+// input (bwd) pixel, 16-byte data and 8-byte argmax accesses, 32-bit indexing. The scalar
+// kernels above (one 2-byte element per thread, 64-bit div/mod) ran GoogLeNet's 3x3/s1
+// inception pools at ~15 % of HBM bandwidth (9 of its 23 ms/step at bs256).
+__global__ __launch_bounds__(256) void maxpool_fwd8_kernel(const bf16* __restrict__ x, PoolGeom g,
+                                                           bf16* __restrict__ y,
+                                                           uint8_t* __restrict__ arg) {
+  const int G = g.C >> 3;
+  const int total = g.N * g.Ho * g.Wo * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G;
+    int q = i / G;
+    const int ow = q % g.Wo;
+    q /= g.Wo;
+    const int oh = q % g.Ho;
+    const int n = q / g.Ho;
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      best[v] = -INFINITY;
+      bi[v] = 0;
+    }
+    const bf16* xn = x + (size_t)n * g.H * g.W * g.C + gi * 8;
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int ih = oh * g.s - g.p + kh;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int iw = ow * g.s - g.p + kw;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(xn + (ih * g.W + iw) * g.C), f);
+        const uint32_t t = kh * g.k + kw;
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+          if (f[v] > best[v] || f[v] != f[v]) {
+            best[v] = f[v];
+            bi[v] = t;
+          }
+      }
+    }
+    *reinterpret_cast<uint4*>(y + (size_t)i * 8) = pack8(best);
+    *reinterpret_cast<uint2*>(arg + (size_t)i * 8) =
+        make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
+                   bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd8_kernel(const bf16* __restrict__ dy,
+                                                           const uint8_t* __restrict__ arg,
+                                                           PoolGeom g, bf16* __restrict__ dx) {
+  const int G = g.C >> 3;
+  const int total = g.N * g.H * g.W * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G;
+    int q = i / G;
+    const int iw = q % g.W;
+    q /= g.W;
+    const int ih = q % g.H;
+    const int n = q / g.H;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const size_t nb = (size_t)n * g.Ho * g.Wo;
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int t = ih + g.p - kh;
+      if (t < 0) continue;
+      const int oh = t / g.s;
+      if (oh * g.s != t || oh >= g.Ho) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int u = iw + g.p - kw;
+        if (u < 0) continue;
+        const int ow = u / g.s;
+        if (ow * g.s != u || ow >= g.Wo) continue;
+        const size_t o = ((nb + oh * g.Wo + ow) * g.C) + gi * 8;
+        const uint2 a = *reinterpret_cast<const uint2*>(arg + o);
+        const uint32_t tap = kh * g.k + kw;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(dy + o), f);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          const uint32_t av = ((v < 4 ? a.x : a.y) >> ((v & 3) * 8)) & 0xffu;
+          if (av == tap) s[v] += f[v];
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + (size_t)i * 8) = pack8(s);
+  }
+}
+
 // ----------------------------------------------------------------------- cross-entropy
 // logits[N][K] fp32, targets int64. One 256-thread block, deterministic reductions.
 // Writes loss (mean), dlogits = (softmax - onehot) / N, and accumulates
@@ -662,13 +750,26 @@ void avgpool_bwd_launch(const bf16* dy, int N, int H, int W, int C, int Ho, int 
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_cap((size_t)N * H * W * C)), dim3(256), 0, st, dy,
                      pg(N, H, W, C, Ho, Wo, k, s, p), dx);
 }
+static bool pool8_ok(int N, int H, int W, int C) {
+  return C % 8 == 0 && (size_t)N * H * W * (C / 8) < (size_t)INT32_MAX;
+}
 void maxpool_fwd_launch(const bf16* x, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                         int p, bf16* y, uint8_t* arg, hipStream_t st) {
+  if (k * k <= 256 && pool8_ok(N, H, W, C) && pool8_ok(N, Ho, Wo, C)) {
+    hipLaunchKernelGGL(maxpool_fwd8_kernel, dim3(grid_cap((size_t)N * Ho * Wo * C / 8)), dim3(256), 0,
+                       st, x, pg(N, H, W, C, Ho, Wo, k, s, p), y, arg);
+    return;
+  }
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_cap((size_t)N * Ho * Wo * C)), dim3(256), 0, st,
                      x, pg(N, H, W, C, Ho, Wo, k, s, p), y, arg);
 }
 void maxpool_bwd_launch(const bf16* dy, const uint8_t* arg, int N, int H, int W, int C, int Ho,
                         int Wo, int k, int s, int p, bf16* dx, hipStream_t st) {
+  if (k * k <= 256 && pool8_ok(N, H, W, C) && pool8_ok(N, Ho, Wo, C)) {
+    hipLaunchKernelGGL(maxpool_bwd8_kernel, dim3(grid_cap((size_t)N * H * W * C / 8)), dim3(256), 0,
+                       st, dy, arg, pg(N, H, W, C, Ho, Wo, k, s, p), dx);
+    return;
+  }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_cap((size_t)N * H * W * C)), dim3(256), 0, st, dy,
                      arg, pg(N, H, W, C, Ho, Wo, k, s, p), dx);
 }

@@ -127,7 +127,7 @@ def build_bench_step(model_name, per_rank_batch, device, ctx, graph=True, baseli
     from .optim import SGD
 
     torch.manual_seed(0)
-    model = getattr(models, model_name)().to(device)
+    model = models.build_model(model_name).to(device)
     arena = ParamArena(model.parameters())
     opt = SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4).attach_arena(arena)
     ddp = None

@@ -541,8 +541,47 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
         cp = _round8(Cin)
         y, stats = _ConvMFMA.apply(to_nhwc(x, pad_to=cp), weight, bias, stride, padding, groups, want_stats, cp)
         return to_nchw(y), (stats if want_stats else None)
+    if _GROUP_PAD:
+        return _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats)
     y = _ConvDirect.apply(to_nhwc(x), weight, bias, stride, padding, groups)
     return to_nchw(y), None
+
+
+# Convs whose per-group widths are not multiples of 8 (ShuffleNet's 25/50/100-channel
+# groups, shufflenet.py:26-33; DPN's groups=32 with 3..24 channels, dpn.py:15; ResNeXt29_32x4d's
+# 4, resnext.py:19; LeNet 3->6->16, densenet_cifar's growth 12, PNASNet-A's 44) run on the MFMA
+# implicit GEMM with every group
+# zero-padded to a multiple of 8 channels on both sides: pad (input, weight) and slice (output,
+# BN statistics) are plain differentiable tensor ops, so autograd carries the gradients back
+# through them. Even where the padded group leaves most of a 64-wide MFMA tile empty (DPN's
+# 3-channel groups) this beats the scalar direct kernels by 10-30x (tools/zoo_bench.py).
+_GROUP_PAD = os.environ.get("PCA_GROUP_PAD", "1") != "0"
+
+
+def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
+    Cout, Cg, KH, KW = weight.shape
+    cout_g = Cout // groups
+    cp, op = _round8(Cg), _round8(cout_g)
+    xn = to_nhwc(x)
+    N, H, W, _ = xn.shape
+    if cp != Cg:
+        xn = F.pad(xn.view(N, H, W, groups, Cg), (0, cp - Cg)).reshape(N, H, W, groups * cp)
+    # weight [Cout, Cg, KH, KW] -> [G*op, cp, KH, KW], channels_last (the MFMA B layout)
+    wp = weight.view(groups, cout_g, Cg, KH, KW)
+    wp = F.pad(wp, (0, 0, 0, 0, 0, cp - Cg, 0, op - cout_g)).reshape(groups * op, cp, KH, KW)
+    wp = wp.contiguous(memory_format=torch.channels_last)
+    bp = None
+    if bias is not None:
+        bp = F.pad(bias.view(groups, cout_g), (0, op - cout_g)).reshape(groups * op)
+    y, stats = _ConvMFMA.apply(xn, wp, bp, stride, padding, groups, want_stats, 0)
+    if op != cout_g:
+        Ho, Wo = y.shape[1], y.shape[2]
+        # (.contiguous: with groups == 1 the reshape of the slice is a strided view, not a copy)
+        y = y.view(N, Ho, Wo, groups, op)[..., :cout_g].reshape(N, Ho, Wo, Cout).contiguous()
+        if want_stats and stats is not None and stats.numel():
+            R = stats.shape[0]
+            stats = stats.view(R, 2, groups, op)[..., :cout_g].reshape(R, 2, Cout).contiguous()
+    return to_nchw(y), (stats if want_stats and stats is not None and stats.numel() else None)
 
 
 class _AddBias(torch.autograd.Function):

@@ -272,9 +272,11 @@ def test_cross_entropy(C):
     assert metrics[1].item() == correct and metrics[2].item() == 300
 
 
-def test_pools_and_gap(C):
+@pytest.mark.parametrize("Cc", [16, 12])
+def test_pools_and_gap(C, Cc):
+    """Max/avg pools and global average pool; C % 8 == 0 takes the vectorized max-pool kernels."""
     torch.manual_seed(4)
-    x = bf(torch.randn(2, 16, 8, 8, device="cuda")).requires_grad_(True)
+    x = bf(torch.randn(2, Cc, 8, 8, device="cuda")).requires_grad_(True)
     xn = nhwc(x.detach()).bfloat16()
     for k, s, p in [(2, 2, 0), (3, 1, 1), (3, 2, 1)]:
         ref = F.max_pool2d(x, k, s, p)

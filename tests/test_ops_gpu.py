@@ -117,7 +117,7 @@ def test_resnet18_trains():
 GPU_ZOO = ["LeNet", "VGG11", "PreActResNet18", "GoogLeNet", "densenet_cifar", "ResNeXt29_2x64d",
            "MobileNet", "MobileNetV2", "DPN26", "SENet18", "EfficientNetB0", "RegNetX_200MF",
            "RegNetY_400MF", "SimpleDLA", "DLA", "PNASNetA", "PNASNetB", "ShuffleNetG2",
-           "ShuffleNetV2_1", "ResNet50"]
+           "ShuffleNetV2_1", "ResNet50", "ResNeXt29_32x4d"]
 
 
 @pytest.fixture
@@ -211,3 +211,32 @@ def test_bn_backward_reduce_fusion_matches_separate_pass():
         if e > 2e-2:
             bad.append((n, round(e, 4)))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("Cin,Cout,G,k,s", [(200, 50, 2, 1, 1), (50, 176, 2, 1, 1), (96, 96, 32, 3, 2),
+                                           (128, 128, 32, 3, 1), (12, 44, 1, 3, 1), (3, 6, 1, 5, 1)])
+def test_group_padded_conv_matches_fp32(Cin, Cout, G, k, s):
+    """Odd per-group widths run on the MFMA GEMM with groups zero-padded to multiples of 8:
+    output, BN statistics, dX, dW against fp32 F.conv2d."""
+    import torch.nn.functional as F
+    from pytorch_cifar_amd.ops import functional as OF
+
+    torch.manual_seed(7)
+    p = k // 2
+    x = torch.randn(4, Cin, 12, 12, device="cuda").bfloat16().float().requires_grad_(True)
+    w = (torch.randn(Cout, Cin // G, k, k, device="cuda") * 0.2).requires_grad_(True)
+    wn = w.detach().clone().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    ref = F.conv2d(x, w, None, s, p, 1, G)
+    y, stats = OF.conv2d(x.detach().requires_grad_(True), wn, None, s, p, G, True)
+    assert rel(y, ref) < 1e-2
+    st = stats.sum(0)
+    assert rel(st[0], ref.detach().sum((0, 2, 3))) < 2e-2
+    assert rel(st[1], (ref.detach() ** 2).sum((0, 2, 3))) < 2e-2
+    dy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(dy)
+    # activations reach a conv as bf16 NHWC storage (fp32 NCHW input is the image-conversion path)
+    xn = x.detach().bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y, _ = OF.conv2d(xn, wn, None, s, p, G, False)
+    y.backward(dy.to(y.dtype))
+    assert rel(xn.grad, x.grad) < 2e-2
+    assert rel(wn.grad, w.grad) < 2e-2
