@@ -202,23 +202,28 @@ __global__ void dw_wgrad_final_kernel(const float* __restrict__ partial, int R, 
 //   * wgrad accumulates all K*K taps x V channels in registers across every strip the thread
 //     walks (dY read once), then the threads sharing a channel group are reduced through LDS,
 //     one tap at a time, into one deterministic partial row per block.
-// V = 8 (16-byte vectors) at K = 3; V = 4 (8-byte vectors) at K = 5, so that the 25 x V weights
-// (or accumulators) plus the 25-vector window stay in registers (~170 VGPRs).
+// V = 8 (16-byte vectors) at K = 3; V = 4 (8-byte vectors) at K = 5 and V = 2 (4-byte) at K = 7,
+// so that the K*K x V weights (or accumulators) plus the K*K-vector window stay in registers.
 // ---------------------------------------------------------------------------------------
 template <int V> struct DwVec;
 template <> struct DwVec<8> { using T = uint4; };
 template <> struct DwVec<4> { using T = uint2; };
+template <> struct DwVec<2> { using T = uint32_t; };
 
 template <int V>
 __device__ __forceinline__ typename DwVec<V>::T dw_zero() {
   if constexpr (V == 8) return make_uint4(0u, 0u, 0u, 0u);
-  else return make_uint2(0u, 0u);
+  else if constexpr (V == 4) return make_uint2(0u, 0u);
+  else return 0u;
 }
 
 template <int V>
 __device__ __forceinline__ void dw_unpack(const typename DwVec<V>::T& u, float* f) {
   if constexpr (V == 8) {
     unpack8(u, f);
+  } else if constexpr (V == 2) {
+    f[0] = __uint_as_float(u << 16);
+    f[1] = __uint_as_float(u & 0xffff0000u);
   } else {
     f[0] = __uint_as_float(u.x << 16);
     f[1] = __uint_as_float(u.x & 0xffff0000u);
@@ -230,7 +235,8 @@ __device__ __forceinline__ void dw_unpack(const typename DwVec<V>::T& u, float* 
 template <int V>
 __device__ __forceinline__ typename DwVec<V>::T dw_pack(const float* f) {
   if constexpr (V == 8) return pack8(f);
-  else return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
+  else if constexpr (V == 4) return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
+  else return pack2(f[0], f[1]);
 }
 
 // the K vectors (kw = 0..K-1) of input row ih starting at column iw0 (zeros outside the image)
@@ -278,10 +284,15 @@ __global__ __launch_bounds__(256) void dwk_fwd_kernel(const bf16* __restrict__ x
 #pragma unroll
     for (int t = 0; t < KK; ++t) {
       const int src = FLIP ? KK - 1 - t : t;
+      if constexpr (V == 2) {
+        const float2 wv = *reinterpret_cast<const float2*>(wT + src * g.Co + c);
+        w[t][0] = wv.x; w[t][1] = wv.y;
+      } else {
 #pragma unroll
-      for (int v4 = 0; v4 < V; v4 += 4) {
-        const float4 wv = *reinterpret_cast<const float4*>(wT + src * g.Co + c + v4);
-        w[t][v4] = wv.x; w[t][v4 + 1] = wv.y; w[t][v4 + 2] = wv.z; w[t][v4 + 3] = wv.w;
+        for (int v4 = 0; v4 < V; v4 += 4) {
+          const float4 wv = *reinterpret_cast<const float4*>(wT + src * g.Co + c + v4);
+          w[t][v4] = wv.x; w[t][v4 + 1] = wv.y; w[t][v4 + 2] = wv.z; w[t][v4 + 3] = wv.w;
+        }
       }
     }
     const bf16* xn = x + (size_t)n * g.H * g.W * g.C + c;
@@ -384,10 +395,15 @@ __global__ __launch_bounds__(256) void dwk_wgrad_kernel(const bf16* __restrict__
       for (int j = 1; j < W; ++j)
 #pragma unroll
         for (int v = 0; v < V; ++v) s[v] += red[(j * GB + t) * V + v];
-      float4* o = reinterpret_cast<float4*>(prow + (size_t)k * g.Co + (gb0 + t) * V);
+      float* o = prow + (size_t)k * g.Co + (gb0 + t) * V;
+      if constexpr (V == 2) {
+        *reinterpret_cast<float2*>(o) = make_float2(s[0], s[1]);
+      } else {
 #pragma unroll
-      for (int v4 = 0; v4 < V / 4; ++v4)
-        o[v4] = make_float4(s[4 * v4], s[4 * v4 + 1], s[4 * v4 + 2], s[4 * v4 + 3]);
+        for (int v4 = 0; v4 < V / 4; ++v4)
+          reinterpret_cast<float4*>(o)[v4] =
+              make_float4(s[4 * v4], s[4 * v4 + 1], s[4 * v4 + 2], s[4 * v4 + 3]);
+      }
     }
     __syncthreads();
   }
@@ -484,6 +500,7 @@ static int dwk_kind(const DwGeom& g) {
   if (off || g.mult != 1 || g.KH != g.KW || (g.s != 1 && g.s != 2)) return 0;
   if (g.KH == 3 && g.p == 1 && g.C % 8 == 0) return 3;
   if (g.KH == 5 && g.p == 2 && g.C % 4 == 0) return 5;
+  if (g.KH == 7 && g.p == 3 && g.C % 2 == 0) return 7;   // PNASNet SepConv k7 (pnasnet.py:14-17)
   return 0;
 }
 
@@ -506,7 +523,8 @@ static void dwk_fwd_t(const bf16* x, const float* wT, const DwGeom& g, bool flip
 static void dwk_fwd(int kind, const bf16* x, const float* wT, const DwGeom& g, bool flip, bf16* y,
                     hipStream_t st) {
   if (kind == 3) dwk_fwd_t<3, 8>(x, wT, g, flip, y, st);
-  else dwk_fwd_t<5, 4>(x, wT, g, flip, y, st);
+  else if (kind == 5) dwk_fwd_t<5, 4>(x, wT, g, flip, y, st);
+  else dwk_fwd_t<7, 2>(x, wT, g, flip, y, st);
 }
 
 template <int K, int V>
@@ -547,7 +565,8 @@ void dw_dgrad_launch(const bf16* dy, const float* wT, int N, int H, int W, int C
   if (kind && C % 8 == 0) {   // stride 2: parity-exact taps
     const dim3 grid(gcap((size_t)N * H * W * C / 8)), block(256);
     if (kind == 3) hipLaunchKernelGGL(dwk_dgrad_s2_kernel<3>, grid, block, 0, st, dy, wT, g, dx);
-    else hipLaunchKernelGGL(dwk_dgrad_s2_kernel<5>, grid, block, 0, st, dy, wT, g, dx);
+    else if (kind == 5) hipLaunchKernelGGL(dwk_dgrad_s2_kernel<5>, grid, block, 0, st, dy, wT, g, dx);
+    else hipLaunchKernelGGL(dwk_dgrad_s2_kernel<7>, grid, block, 0, st, dy, wT, g, dx);
     return;
   }
   if (g.mult == 1 && C % 8 == 0)
@@ -577,7 +596,8 @@ void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, 
   if (const int kind = dwk_kind(g)) {
     // chunks = partial rows = blocks (grid.x) of the strip-walking kernel
     if (kind == 3) dwk_wgrad_t<3, 8>(x, dy, g, chunks, partial, st);
-    else dwk_wgrad_t<5, 4>(x, dy, g, chunks, partial, st);
+    else if (kind == 5) dwk_wgrad_t<5, 4>(x, dy, g, chunks, partial, st);
+    else dwk_wgrad_t<7, 2>(x, dy, g, chunks, partial, st);
     hipLaunchKernelGGL(dw_wgrad_final4_kernel, dim3(cdiv(T * Co, 32)), dim3(256), 0, st, partial,
                        chunks, T, Co, dw, accum);
     return;
