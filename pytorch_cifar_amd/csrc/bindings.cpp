@@ -89,6 +89,8 @@ void scale_by_scalar_launch(const float*, const float*, size_t, float*, hipStrea
 void sgd_launch(const int64_t*, int, float* const*, const float* const*, float* const*,
                 bf16* const*, const float*, float, float, float, float, int, int, hipStream_t);
 void se_scale_fwd_launch(const bf16*, const float*, int, int, int, bf16*, hipStream_t);
+void dpn_merge_fwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, hipStream_t);
+void dpn_merge_bwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, bf16*, hipStream_t);
 void se_scale_bwd_launch(const bf16*, const bf16*, const float*, int, int, int, bf16*, float*,
                          hipStream_t);
 void act_fwd_launch(const bf16*, size_t, int, bf16*, hipStream_t);
@@ -704,6 +706,31 @@ std::vector<Tensor> se_scale_bwd(const Tensor& dout, const Tensor& x, const Tens
   return {dx, ds};
 }
 
+// DPN dual-path merge: x [N,H,W,Cx], o [N,H,W,Co] NHWC bf16 -> relu(cat[x[:d]+o[:d], x[d:], o[d:]])
+Tensor dpn_merge_fwd(const Tensor& x, const Tensor& o, int d) {
+  check_bf16(x, "x");
+  check_bf16(o, "o");
+  const int Cx = x.size(3), Co = o.size(3);
+  TORCH_CHECK(x.size(0) == o.size(0) && x.size(1) == o.size(1) && x.size(2) == o.size(2), "dpn_merge: pixel mismatch");
+  TORCH_CHECK(d % 8 == 0 && Cx % 8 == 0 && Co % 8 == 0 && d <= Cx && d <= Co, "dpn_merge: channels must be multiples of 8");
+  const int P = x.size(0) * x.size(1) * x.size(2);
+  auto y = at::empty({x.size(0), x.size(1), x.size(2), Cx + Co - d}, x.options());
+  pca::dpn_merge_fwd_launch(ptr<bf16>(x), ptr<bf16>(o), P, Cx, Co, d, ptr<bf16>(y), cur_stream());
+  return y;
+}
+
+std::vector<Tensor> dpn_merge_bwd(const Tensor& dy, const Tensor& y, int Cx, int Co, int d) {
+  check_bf16(dy, "dy");
+  check_bf16(y, "y");
+  TORCH_CHECK(dy.sizes() == y.sizes() && y.size(3) == Cx + Co - d, "dpn_merge_bwd: shape");
+  const int P = y.size(0) * y.size(1) * y.size(2);
+  auto dx = at::empty({y.size(0), y.size(1), y.size(2), Cx}, y.options());
+  auto dout = at::empty({y.size(0), y.size(1), y.size(2), Co}, y.options());
+  pca::dpn_merge_bwd_launch(ptr<bf16>(dy), ptr<bf16>(y), P, Cx, Co, d, ptr<bf16>(dx),
+                            ptr<bf16>(dout), cur_stream());
+  return {dx, dout};
+}
+
 Tensor act_fwd(const Tensor& x, int act) {
   check_bf16(x, "x");
   auto y = at::empty_like(x);
@@ -890,6 +917,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_step", &sgd_step);
   m.def("se_scale_fwd", &se_scale_fwd);
   m.def("se_scale_bwd", &se_scale_bwd);
+  m.def("dpn_merge_fwd", &dpn_merge_fwd);
+  m.def("dpn_merge_bwd", &dpn_merge_bwd);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("add_act", &add_act);

@@ -314,6 +314,70 @@ __global__ __launch_bounds__(256) void maxpool_bwd8_kernel(const bf16* __restric
   }
 }
 
+// ---- DPN dual-path merge (dpn.py:29-31): y = relu(cat[x[:d] + o[:d], x[d:], o[d:]]) in one
+// pass over 8-channel groups (d, Cx, Co % 8 == 0), replacing two channel-slice copies, the
+// add, two ReLUs and the concatenation; backward routes relu'(y) * dy to dX / dO the same way.
+__global__ __launch_bounds__(256) void dpn_merge_fwd_kernel(const bf16* __restrict__ x,
+                                                            const bf16* __restrict__ o, int P,
+                                                            int Cx, int Co, int d,
+                                                            bf16* __restrict__ y) {
+  const int Ct = Cx + Co - d, G = Ct >> 3;
+  const int total = P * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G, p = i / G;
+    const int j = gi * 8;
+    float a[8];
+    if (j < d) {
+      float b[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + (size_t)p * Cx + j), a);
+      unpack8(*reinterpret_cast<const uint4*>(o + (size_t)p * Co + j), b);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) a[v] += b[v];
+    } else if (j < Cx) {
+      unpack8(*reinterpret_cast<const uint4*>(x + (size_t)p * Cx + j), a);
+    } else {
+      unpack8(*reinterpret_cast<const uint4*>(o + (size_t)p * Co + j - Cx + d), a);
+    }
+#pragma unroll
+    for (int v = 0; v < 8; ++v) a[v] = fmaxf(a[v], 0.f);
+    *reinterpret_cast<uint4*>(y + (size_t)i * 8) = pack8(a);
+  }
+}
+
+__global__ __launch_bounds__(256) void dpn_merge_bwd_kernel(const bf16* __restrict__ dy,
+                                                            const bf16* __restrict__ y, int P,
+                                                            int Cx, int Co, int d,
+                                                            bf16* __restrict__ dx,
+                                                            bf16* __restrict__ dout) {
+  const int Ct = Cx + Co - d, G = Ct >> 3;
+  const int total = P * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G, p = i / G;
+    const int j = gi * 8;
+    float g[8], yy[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + (size_t)i * 8), g);
+    unpack8(*reinterpret_cast<const uint4*>(y + (size_t)i * 8), yy);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) g[v] = yy[v] > 0.f ? g[v] : 0.f;
+    const uint4 gv = pack8(g);
+    if (j < Cx) *reinterpret_cast<uint4*>(dx + (size_t)p * Cx + j) = gv;
+    if (j < d) *reinterpret_cast<uint4*>(dout + (size_t)p * Co + j) = gv;
+    else if (j >= Cx) *reinterpret_cast<uint4*>(dout + (size_t)p * Co + j - Cx + d) = gv;
+  }
+}
+
+void dpn_merge_fwd_launch(const bf16* x, const bf16* o, int P, int Cx, int Co, int d, bf16* y,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(dpn_merge_fwd_kernel, dim3(grid_cap((size_t)P * (Cx + Co - d) / 8)), dim3(256),
+                     0, st, x, o, P, Cx, Co, d, y);
+}
+
+void dpn_merge_bwd_launch(const bf16* dy, const bf16* y, int P, int Cx, int Co, int d, bf16* dx,
+                          bf16* dout, hipStream_t st) {
+  hipLaunchKernelGGL(dpn_merge_bwd_kernel, dim3(grid_cap((size_t)P * (Cx + Co - d) / 8)), dim3(256),
+                     0, st, dy, y, P, Cx, Co, d, dx, dout);
+}
+
 // ----------------------------------------------------------------------- cross-entropy
 // logits[N][K] fp32, targets int64. One 256-thread block, deterministic reductions.
 // Writes loss (mean), dlogits = (softmax - onehot) / N, and accumulates

@@ -2,7 +2,7 @@
 
 Bottleneck: 1x1 -> grouped 3x3 (32 groups, 3..24 channels per group: direct-conv kernel) -> 1x1,
 then the dual path: residual-add of the first ``out_planes`` channels and dense concatenation of
-the rest, followed by ReLU (the add+ReLU of the residual slice is one native pass)."""
+the rest, followed by ReLU — one native pass each way (``F.dpn_merge``)."""
 import torch.nn as tnn
 
 from ..nn import BatchNorm2d, Conv2d, Linear, Sequential
@@ -31,8 +31,7 @@ class Bottleneck(tnn.Module):
         out = self.bn2(self.conv2(out), act="relu")
         out = self.bn3(self.conv3(out))
         x = self.shortcut(x)
-        d = self.out_planes
-        return F.cat([F.add_act(x[:, :d], out[:, :d], "relu"), F.relu(x[:, d:]), F.relu(out[:, d:])], 1)
+        return F.dpn_merge(x, out, self.out_planes)
 
 
 class DPN(tnn.Module):

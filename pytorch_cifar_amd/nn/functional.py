@@ -12,6 +12,7 @@ from ..ops.functional import (  # noqa: F401
     cat,
     channel_shuffle,
     cross_entropy,
+    dpn_merge,
     dropout,
     global_avg_pool,
     max_pool2d,

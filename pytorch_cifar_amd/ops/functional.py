@@ -829,6 +829,29 @@ def add_act(a, b, act=None):
     return to_nchw(_AddAct.apply(to_nhwc(a), to_nhwc(b), ACT[act]))
 
 
+class _DPNMerge(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, o, d):
+        y = _C().dpn_merge_fwd(x, o, d)
+        ctx.save_for_backward(y)
+        ctx.geom = (x.shape[-1], o.shape[-1], d)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dx, do = _C().dpn_merge_bwd(dy.contiguous(), y, *ctx.geom)
+        return dx, do, None
+
+
+def dpn_merge(x, out, d):
+    """DPN dual-path join relu(cat[x[:, :d] + out[:, :d], x[:, d:], out[:, d:]]) (dpn.py:29-31)
+    as one native pass each way (no channel-slice copies / separate add, ReLU and concat)."""
+    if _ref(x) or d % 8 or x.shape[1] % 8 or out.shape[1] % 8:
+        return torch.cat([add_act(x[:, :d], out[:, :d], "relu"), relu(x[:, d:]), relu(out[:, d:])], 1)
+    return to_nchw(_DPNMerge.apply(to_nhwc(x), to_nhwc(out), d))
+
+
 # ---------------------------------------------------------------------------- pooling
 class _GAP(torch.autograd.Function):
     @staticmethod

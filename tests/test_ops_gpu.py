@@ -240,3 +240,22 @@ def test_group_padded_conv_matches_fp32(Cin, Cout, G, k, s):
     y.backward(dy.to(y.dtype))
     assert rel(xn.grad, x.grad) < 2e-2
     assert rel(wn.grad, w.grad) < 2e-2
+
+
+def test_dpn_merge_matches_torch():
+    """Native DPN dual-path join vs relu(cat[x[:d] + o[:d], x[d:], o[d:]]) and its gradients."""
+    from pytorch_cifar_amd.ops import functional as OF
+
+    torch.manual_seed(8)
+    d = 64
+    x = torch.randn(3, 80, 6, 6, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    o = torch.randn(3, 96, 6, 6, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xr, orr = x.float().requires_grad_(True), o.float().requires_grad_(True)
+    ref = torch.relu(torch.cat([xr[:, :d] + orr[:, :d], xr[:, d:], orr[:, d:]], 1))
+    xn, on = x.clone().requires_grad_(True), o.clone().requires_grad_(True)
+    y = OF.dpn_merge(xn, on, d)
+    assert y.shape == ref.shape and rel(y, ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    y.backward(dy.contiguous(memory_format=torch.channels_last))
+    assert rel(xn.grad, xr.grad) < 1e-2 and rel(on.grad, orr.grad) < 1e-2
