@@ -116,6 +116,34 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ i
   out[(size_t)blockIdx.y * L + c] = s;
 }
 
+// ---- bias gradient: db[c] (+)= sum_r stat[r][0][c] (the per-channel sums of dY from the
+// bn_stats partials), 64 channels x 16 row lanes per block, lanes added in a fixed order; written
+// straight into the gradient arena (no separate reduce + accumulate-add launches)
+__global__ __launch_bounds__(1024) void bias_grad_fold_kernel(const float* __restrict__ stat,
+                                                              int R, int C, int accumulate,
+                                                              float* __restrict__ db) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < C)
+    for (int r = rl; r < R; r += 16) s += stat[(size_t)r * 2 * C + c];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    db[c] = accumulate ? db[c] + t : t;
+  }
+}
+
+void bias_grad_fold_launch(const float* stat, int R, int C, int accumulate, float* db,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(bias_grad_fold_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C,
+                     accumulate, db);
+}
+
 // ---- forward finalize: stat[R][2][C] -> aux[4][C] = {mean, invstd, scale, shift} ----
 // One 1024-thread block per 64 channels: 16 row-lanes fold the R (<= 1024) partial rows in
 // parallel (coalesced 256-byte row segments), then lane-row 0 combines them in fp64.

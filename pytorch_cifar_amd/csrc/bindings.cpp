@@ -59,6 +59,7 @@ int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int
 int bn_row_blocks(int M, int C);
 void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t);
 int colsum_launch(const float*, int, int, float*, hipStream_t);
+void bias_grad_fold_launch(const float*, int, int, int, float*, hipStream_t);
 void bn_finalize_launch(const float*, int, int, double, const float*, const float*, float*, float*,
                         int64_t*, float, float, int, int, float*, hipStream_t);
 void bn_apply_launch(const bf16*, const float*, int, size_t, const bf16*, const bf16*,
@@ -420,6 +421,24 @@ Tensor bn_stats(const Tensor& x) {
   auto partial = at::empty({P, 2, C}, x.options().dtype(at::kFloat));
   pca::bn_stats_launch(ptr<bf16>(x), M, C, ptr<float>(partial), P, cur_stream());
   return partial;
+}
+
+// conv bias gradient: per-channel sum of dY [.., C] (bf16), added into `accum` (fp32 [C], e.g.
+// the bias's gradient-arena view) when given, else returned as a new tensor
+Tensor bias_grad(const Tensor& dy, const optional<Tensor>& accum) {
+  check_bf16(dy, "dy");
+  const int C = dy.size(-1);
+  const int M = dy.numel() / C;
+  const int P = pca::bn_row_blocks(M, C);
+  auto partial = at::empty({P, 2, C}, dy.options().dtype(at::kFloat));
+  pca::bn_stats_launch(ptr<bf16>(dy), M, C, ptr<float>(partial), P, cur_stream());
+  const bool acc = accum.has_value() && accum->defined();
+  Tensor db = acc ? *accum : at::empty({C}, dy.options().dtype(at::kFloat));
+  if (acc)
+    TORCH_CHECK(db.scalar_type() == at::kFloat && db.is_contiguous() && db.numel() == C,
+                "bias_grad: accum must be contiguous fp32 [C]");
+  pca::bias_grad_fold_launch(ptr<float>(partial), P, C, acc ? 1 : 0, ptr<float>(db), cur_stream());
+  return db;
 }
 
 // partial [R, 2, C] (or undefined in eval) -> aux [4, C] = {mean, invstd, scale, shift}
@@ -896,6 +915,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weight_prep", &weight_prep);
   m.def("weight_prep_multi", &weight_prep_multi);
   m.def("bn_stats", &bn_stats);
+  m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("accum") = py::none());
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply);
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("mask"), py::arg("y"),

@@ -416,11 +416,16 @@ class _ConvMFMA(torch.autograd.Function):
                 else:
                     dw_ret = dw.permute(0, 3, 1, 2)
         if bias is not None and bias.requires_grad:
-            db = C.bn_stats(dy)[:, 0].sum(0)
-            if bias.is_leaf:
-                G.accumulate(bias, db)
+            bbuf = G.grad_buffer(bias) if bias.is_leaf else None
+            if bbuf is not None:
+                C.bias_grad(dy, bbuf)        # summed straight into the gradient arena
+                G.fire(bias)
             else:
-                db_ret = db
+                db = C.bias_grad(dy)
+                if bias.is_leaf:
+                    G.accumulate(bias, db)
+                else:
+                    db_ret = db
         return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None
 
 
@@ -595,11 +600,16 @@ class _AddBias(torch.autograd.Function):
         b = ctx.bias
         db_ret = None
         if b.requires_grad:
-            db = _C().bn_stats(dy.contiguous())[:, 0].sum(0)
-            if b.is_leaf:
-                G.accumulate(b, db)
+            bbuf = G.grad_buffer(b) if b.is_leaf else None
+            if bbuf is not None:
+                _C().bias_grad(dy.contiguous(), bbuf)
+                G.fire(b)
             else:
-                db_ret = db
+                db = _C().bias_grad(dy.contiguous())
+                if b.is_leaf:
+                    G.accumulate(b, db)
+                else:
+                    db_ret = db
         return dy, db_ret
 
 
