@@ -498,10 +498,20 @@ static int dwk_kind(const DwGeom& g) {
     return e && e[0] == '0';
   }();
   if (off || g.mult != 1 || g.KH != g.KW || (g.s != 1 && g.s != 2)) return 0;
-  if (g.KH == 3 && g.p == 1 && g.C % 8 == 0) return 3;
-  if (g.KH == 5 && g.p == 2 && g.C % 4 == 0) return 5;
-  if (g.KH == 7 && g.p == 3 && g.C % 2 == 0) return 7;   // PNASNet SepConv k7 (pnasnet.py:14-17)
+  if (g.C % 2) return 0;
+  if (g.KH == 3 && g.p == 1) return 3;
+  if (g.KH == 5 && g.p == 2) return 5;
+  if (g.KH == 7 && g.p == 3) return 7;   // PNASNet SepConv k7 (pnasnet.py:14-17)
   return 0;
+}
+
+// channels per thread: the widest vector C allows, capped per K by the register budget
+// (ShuffleNetV2's 58/116/232-channel branches take V = 2 / 4 at k3)
+static int dwk_vec(int kind, int C) {
+  const int vmax = kind == 3 ? 8 : kind == 5 ? 4 : 2;
+  if (vmax >= 8 && C % 8 == 0) return 8;
+  if (vmax >= 4 && C % 4 == 0) return 4;
+  return 2;
 }
 
 static int dwk_rpt(int Ho) { return Ho < 8 ? Ho : 8; }
@@ -522,9 +532,17 @@ static void dwk_fwd_t(const bf16* x, const float* wT, const DwGeom& g, bool flip
 
 static void dwk_fwd(int kind, const bf16* x, const float* wT, const DwGeom& g, bool flip, bf16* y,
                     hipStream_t st) {
-  if (kind == 3) dwk_fwd_t<3, 8>(x, wT, g, flip, y, st);
-  else if (kind == 5) dwk_fwd_t<5, 4>(x, wT, g, flip, y, st);
-  else dwk_fwd_t<7, 2>(x, wT, g, flip, y, st);
+  const int v = dwk_vec(kind, g.C);
+  if (kind == 3) {
+    if (v == 8) dwk_fwd_t<3, 8>(x, wT, g, flip, y, st);
+    else if (v == 4) dwk_fwd_t<3, 4>(x, wT, g, flip, y, st);
+    else dwk_fwd_t<3, 2>(x, wT, g, flip, y, st);
+  } else if (kind == 5) {
+    if (v == 4) dwk_fwd_t<5, 4>(x, wT, g, flip, y, st);
+    else dwk_fwd_t<5, 2>(x, wT, g, flip, y, st);
+  } else {
+    dwk_fwd_t<7, 2>(x, wT, g, flip, y, st);
+  }
 }
 
 template <int K, int V>
@@ -595,8 +613,12 @@ void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, 
   const int T = KH * KW;
   if (const int kind = dwk_kind(g)) {
     // chunks = partial rows = blocks (grid.x) of the strip-walking kernel
-    if (kind == 3) dwk_wgrad_t<3, 8>(x, dy, g, chunks, partial, st);
-    else if (kind == 5) dwk_wgrad_t<5, 4>(x, dy, g, chunks, partial, st);
+    const int v = dwk_vec(kind, Co);
+    if (kind == 3 && v == 8) dwk_wgrad_t<3, 8>(x, dy, g, chunks, partial, st);
+    else if (kind == 3 && v == 4) dwk_wgrad_t<3, 4>(x, dy, g, chunks, partial, st);
+    else if (kind == 3) dwk_wgrad_t<3, 2>(x, dy, g, chunks, partial, st);
+    else if (kind == 5 && v == 4) dwk_wgrad_t<5, 4>(x, dy, g, chunks, partial, st);
+    else if (kind == 5) dwk_wgrad_t<5, 2>(x, dy, g, chunks, partial, st);
     else dwk_wgrad_t<7, 2>(x, dy, g, chunks, partial, st);
     hipLaunchKernelGGL(dw_wgrad_final4_kernel, dim3(cdiv(T * Co, 32)), dim3(256), 0, st, partial,
                        chunks, T, Co, dw, accum);

@@ -304,9 +304,10 @@ def test_pools_and_gap(C, Cc):
                                             (24, 1, 3, 1, 9), (144, 1, 5, 2, 16), (36, 1, 5, 1, 8),
                                             (1152, 1, 5, 1, 2), (672, 1, 5, 2, 4), (2304, 1, 3, 1, 4),
                                             (20, 1, 5, 1, 6), (44, 1, 7, 1, 8), (88, 1, 7, 2, 8),
-                                            (176, 1, 7, 1, 4), (30, 1, 7, 2, 9)])
+                                            (176, 1, 7, 1, 4), (30, 1, 7, 2, 9), (58, 1, 3, 1, 8),
+                                            (116, 1, 3, 2, 8), (58, 1, 5, 1, 6), (26, 1, 3, 1, 5)])
 def test_depthwise(C, Cin, mult, k, s, H):
-    """Multiplier 1 with k3 (C % 8 == 0), k5 (C % 4 == 0) or k7 (C % 2 == 0) takes the rolling-window fast paths
+    """Multiplier 1, k3/k5/k7, even C takes the rolling-window fast paths (8/4/2 channels per thread)
     (dwk_*, incl. > 256 channel groups split over grid.y in wgrad), the rest the generic
     kernels; both against torch's fp32 grouped conv."""
     torch.manual_seed(5)
