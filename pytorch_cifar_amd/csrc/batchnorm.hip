@@ -32,10 +32,22 @@ static inline RowPar make_rowpar(int C, int vec) {
   return r;
 }
 
+// VEC = 8 / 4 / 2 / 1 channels per access (16 / 8 / 4 / 2 bytes): the widest that divides C, so
+// odd-width nets (ShuffleNet 58/116/232, PNASNet 44, densenet growth 12) are not scalar
 template <int VEC>
 __device__ __forceinline__ void load_vec(const bf16* p, float* f) {
   if constexpr (VEC == 8) {
     unpack8(*reinterpret_cast<const uint4*>(p), f);
+  } else if constexpr (VEC == 4) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    f[0] = __uint_as_float(u.x << 16);
+    f[1] = __uint_as_float(u.x & 0xffff0000u);
+    f[2] = __uint_as_float(u.y << 16);
+    f[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else if constexpr (VEC == 2) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(p);
+    f[0] = __uint_as_float(u << 16);
+    f[1] = __uint_as_float(u & 0xffff0000u);
   } else {
     f[0] = bf2f(*p);
   }
@@ -45,6 +57,10 @@ template <int VEC>
 __device__ __forceinline__ void store_vec(bf16* p, const float* f) {
   if constexpr (VEC == 8) {
     *reinterpret_cast<uint4*>(p) = pack8(f);
+  } else if constexpr (VEC == 4) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<uint32_t*>(p) = pack2(f[0], f[1]);
   } else {
     *p = f2bf(f[0]);
   }
@@ -622,8 +638,10 @@ static int grid_for(size_t nvec) {
   return (int)(b < 4096 ? (b ? b : 1) : 4096);
 }
 
+static int bn_vec(int C) { return C % 8 == 0 ? 8 : C % 4 == 0 ? 4 : C % 2 == 0 ? 2 : 1; }
+
 int bn_row_blocks(int M, int C) {
-  const int vec = (C % 8 == 0) ? 8 : 1;
+  const int vec = bn_vec(C);
   RowPar rp = make_rowpar(C, vec);
   int P = cdiv(M, rp.RPP * 8);
   if (P > 1024) P = 1024;
@@ -633,12 +651,15 @@ int bn_row_blocks(int M, int C) {
 
 void bn_stats_launch(const bf16* x, int M, int C, float* partial, int P, hipStream_t st) {
   const int rows = cdiv(M, P);
-  if (C % 8 == 0) {
-    RowPar rp = make_rowpar(C, 8);
-    hipLaunchKernelGGL(bn_stats_kernel<8>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial);
-  } else {
-    RowPar rp = make_rowpar(C, 1);
-    hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial);
+  switch (bn_vec(C)) {
+#define PCA_STATS(V)                                                                              \
+  case V: {                                                                                       \
+    RowPar rp = make_rowpar(C, V);                                                                \
+    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial); \
+    break;                                                                                        \
+  }
+    PCA_STATS(8) PCA_STATS(4) PCA_STATS(2) PCA_STATS(1)
+#undef PCA_STATS
   }
 }
 
@@ -683,12 +704,18 @@ void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const
 #undef PCA_APPLY
     return;
   }
-  if (C % 8 == 0) {
-    hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, y, aux, C,
-                       total, res, y2, aux2, act, out, mask);
-  } else {
-    hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(total)), dim3(256), 0, st, y, aux, C,
-                       total, res, y2, aux2, act, out, (uint8_t*)nullptr);
+  switch (bn_vec(C)) {
+    case 8:
+      hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, y, aux, C,
+                         total, res, y2, aux2, act, out, mask);
+      break;
+#define PCA_APPLY_V(V)                                                                             \
+  case V:                                                                                          \
+    hipLaunchKernelGGL(bn_apply_kernel<V>, dim3(grid_for(total / V)), dim3(256), 0, st, y, aux, C, \
+                       total, res, y2, aux2, act, out, (uint8_t*)nullptr);                         \
+    break;
+    PCA_APPLY_V(4) PCA_APPLY_V(2) PCA_APPLY_V(1)
+#undef PCA_APPLY_V
   }
 }
 
@@ -697,22 +724,20 @@ void bn_bwd_reduce_launch(const bf16* dout, const bf16* out, const uint8_t* mask
                           const bf16* y2, const float* aux2, int act, int M, int C,
                           float* partial, int P, hipStream_t st) {
   const int rows = cdiv(M, P);
-  if (C % 8 == 0) {
-    RowPar rp = make_rowpar(C, 8);
-    if (y2)
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<8, 3>), dim3(P), dim3(256), 0, st, dout, out, mask, y, aux,
-                         y2, aux2, act, M, rp, rows, partial);
-    else
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<8, 2>), dim3(P), dim3(256), 0, st, dout, out, mask, y, aux,
-                         y2, aux2, act, M, rp, rows, partial);
-  } else {
-    RowPar rp = make_rowpar(C, 1);
-    if (y2)
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, 3>), dim3(P), dim3(256), 0, st, dout, out, mask, y, aux,
-                         y2, aux2, act, M, rp, rows, partial);
-    else
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, 2>), dim3(P), dim3(256), 0, st, dout, out, mask, y, aux,
-                         y2, aux2, act, M, rp, rows, partial);
+  switch (bn_vec(C)) {
+#define PCA_RED(V)                                                                                 \
+  case V: {                                                                                        \
+    RowPar rp = make_rowpar(C, V);                                                                 \
+    if (y2)                                                                                        \
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<V, 3>), dim3(P), dim3(256), 0, st, dout, out, mask, \
+                         y, aux, y2, aux2, act, M, rp, rows, partial);                             \
+    else                                                                                           \
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<V, 2>), dim3(P), dim3(256), 0, st, dout, out, mask, \
+                         y, aux, y2, aux2, act, M, rp, rows, partial);                             \
+    break;                                                                                         \
+  }
+    PCA_RED(8) PCA_RED(4) PCA_RED(2) PCA_RED(1)
+#undef PCA_RED
   }
 }
 
@@ -757,12 +782,19 @@ void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask,
 #undef PCA_BWD
     return;
   }
-  if (C % 8 == 0) {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, dout,
-                       out, mask, y, aux, coef, act, C, total, dy, dres, y2, dy2);
-  } else {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(grid_for(total)), dim3(256), 0, st, dout, out,
-                       (const uint8_t*)nullptr, y, aux, coef, act, C, total, dy, dres, y2, dy2);
+  switch (bn_vec(C)) {
+    case 8:
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, dout,
+                         out, mask, y, aux, coef, act, C, total, dy, dres, y2, dy2);
+      break;
+#define PCA_BWD_V(V)                                                                              \
+  case V:                                                                                         \
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<V>, dim3(grid_for(total / V)), dim3(256), 0, st, dout, \
+                       out, (const uint8_t*)nullptr, y, aux, coef, act, C, total, dy, dres, y2,   \
+                       dy2);                                                                      \
+    break;
+    PCA_BWD_V(4) PCA_BWD_V(2) PCA_BWD_V(1)
+#undef PCA_BWD_V
   }
 }
 

@@ -188,7 +188,8 @@ def test_wgrad_every_config(C, case):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("C_,act,res", [(64, 1, False), (64, 1, True), (24, 0, False), (116, 1, True), (96, 2, False)])
+@pytest.mark.parametrize("C_,act,res", [(64, 1, False), (64, 1, True), (24, 0, False), (116, 1, True), (96, 2, False),
+                                        (58, 1, False), (44, 2, False), (7, 1, True), (58, 0, True)])
 def test_bn_fwd_bwd(C, C_, act, res):
     torch.manual_seed(1)
     N, H = 4, 8
