@@ -90,6 +90,13 @@ void scale_by_scalar_launch(const float*, const float*, size_t, float*, hipStrea
 void sgd_launch(const int64_t*, int, float* const*, const float* const*, float* const*,
                 bf16* const*, const float*, float, float, float, float, int, int, hipStream_t);
 void se_scale_fwd_launch(const bf16*, const float*, int, int, int, bf16*, hipStream_t);
+struct CatArgs {
+  const bf16* src[8];
+  bf16* dst[8];
+  int off[9];
+  int k;
+};
+void cat_nhwc_launch(const CatArgs&, bf16*, int, bool, hipStream_t);
 void dpn_merge_fwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, hipStream_t);
 void dpn_merge_bwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, bf16*, hipStream_t);
 void se_scale_bwd_launch(const bf16*, const bf16*, const float*, int, int, int, bf16*, float*,
@@ -725,6 +732,44 @@ std::vector<Tensor> se_scale_bwd(const Tensor& dout, const Tensor& x, const Tens
   return {dx, ds};
 }
 
+// channel concat of NHWC bf16 tensors [N,H,W,C_i] (<= 8 pieces) -> [N,H,W,sum C_i]
+Tensor cat_nhwc(const std::vector<Tensor>& xs) {
+  TORCH_CHECK(!xs.empty() && xs.size() <= 8, "cat_nhwc: 1..8 inputs");
+  pca::CatArgs a{};
+  a.k = (int)xs.size();
+  a.off[0] = 0;
+  for (int j = 0; j < a.k; ++j) {
+    check_bf16(xs[j], "x");
+    TORCH_CHECK(xs[j].dim() == 4 && xs[j].size(0) == xs[0].size(0) && xs[j].size(1) == xs[0].size(1) &&
+                    xs[j].size(2) == xs[0].size(2), "cat_nhwc: pixel mismatch");
+    a.src[j] = ptr<bf16>(xs[j]);
+    a.off[j + 1] = a.off[j] + (int)xs[j].size(3);
+  }
+  const int P = xs[0].size(0) * xs[0].size(1) * xs[0].size(2);
+  auto out = at::empty({xs[0].size(0), xs[0].size(1), xs[0].size(2), a.off[a.k]}, xs[0].options());
+  pca::cat_nhwc_launch(a, ptr<bf16>(out), P, false, cur_stream());
+  return out;
+}
+
+// inverse: [N,H,W,sum C_i] -> pieces of widths `sizes`
+std::vector<Tensor> split_nhwc(const Tensor& whole, const std::vector<int64_t>& sizes) {
+  check_bf16(whole, "whole");
+  TORCH_CHECK(!sizes.empty() && sizes.size() <= 8, "split_nhwc: 1..8 pieces");
+  pca::CatArgs a{};
+  a.k = (int)sizes.size();
+  a.off[0] = 0;
+  std::vector<Tensor> outs;
+  for (int j = 0; j < a.k; ++j) {
+    outs.push_back(at::empty({whole.size(0), whole.size(1), whole.size(2), sizes[j]}, whole.options()));
+    a.dst[j] = ptr<bf16>(outs.back());
+    a.off[j + 1] = a.off[j] + (int)sizes[j];
+  }
+  TORCH_CHECK(a.off[a.k] == whole.size(3), "split_nhwc: widths must sum to the channel count");
+  const int P = whole.size(0) * whole.size(1) * whole.size(2);
+  pca::cat_nhwc_launch(a, ptr<bf16>(whole), P, true, cur_stream());
+  return outs;
+}
+
 // DPN dual-path merge: x [N,H,W,Cx], o [N,H,W,Co] NHWC bf16 -> relu(cat[x[:d]+o[:d], x[d:], o[d:]])
 Tensor dpn_merge_fwd(const Tensor& x, const Tensor& o, int d) {
   check_bf16(x, "x");
@@ -938,6 +983,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("se_scale_fwd", &se_scale_fwd);
   m.def("se_scale_bwd", &se_scale_bwd);
   m.def("dpn_merge_fwd", &dpn_merge_fwd);
+  m.def("cat_nhwc", &cat_nhwc);
+  m.def("split_nhwc", &split_nhwc);
   m.def("dpn_merge_bwd", &dpn_merge_bwd);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);

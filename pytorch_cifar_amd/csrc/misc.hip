@@ -13,6 +13,8 @@
 //   eltwise     : residual add(+act) for the non-fused paths, act backward
 #include "common.h"
 
+#include <type_traits>
+
 namespace pca {
 
 static int grid_cap(size_t work, int per_block = 256, int cap = 8192) {
@@ -376,6 +378,51 @@ void dpn_merge_bwd_launch(const bf16* dy, const bf16* y, int P, int Cx, int Co, 
                           bf16* dout, hipStream_t st) {
   hipLaunchKernelGGL(dpn_merge_bwd_kernel, dim3(grid_cap((size_t)P * (Cx + Co - d) / 8)), dim3(256),
                      0, st, dy, y, P, Cx, Co, d, dx, dout);
+}
+
+// ---- channel concatenation of NHWC tensors (DenseNet / DLA / GoogLeNet / DPN joins) and its
+// inverse split (the backward): out[p][off_i + c] <-> in_i[p][c], one launch for all pieces,
+// V-channel vectors (the widest that divides every width); SPLIT scatters out -> pieces.
+struct CatArgs {
+  const bf16* src[8];
+  bf16* dst[8];
+  int off[9];   // prefix channel offsets, off[k] = total
+  int k;
+};
+
+template <int V, bool SPLIT>
+__global__ __launch_bounds__(256) void cat_nhwc_kernel(CatArgs a, bf16* __restrict__ whole, int P) {
+  const int Ct = a.off[a.k], G = Ct / V;
+  const int total = P * G;
+  using T = typename std::conditional<V == 8, uint4, typename std::conditional<V == 4, uint2,
+            typename std::conditional<V == 2, uint32_t, uint16_t>::type>::type>::type;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G, p = i / G;
+    const int c = gi * V;
+    int j = 0;
+#pragma unroll 1
+    while (j + 1 < a.k && c >= a.off[j + 1]) ++j;
+    const int w = a.off[j + 1] - a.off[j];
+    const size_t piece = (size_t)p * w + (c - a.off[j]);
+    T* wh = reinterpret_cast<T*>(whole + (size_t)p * Ct + c);
+    if constexpr (SPLIT) *reinterpret_cast<T*>(a.dst[j] + piece) = *wh;
+    else *wh = *reinterpret_cast<const T*>(a.src[j] + piece);
+  }
+}
+
+void cat_nhwc_launch(const CatArgs& a, bf16* whole, int P, bool split, hipStream_t st) {
+  int g = 0;
+  for (int j = 0; j < a.k; ++j) g |= (a.off[j + 1] - a.off[j]);
+  const int V = (g & 7) == 0 ? 8 : (g & 3) == 0 ? 4 : (g & 1) == 0 ? 2 : 1;
+  const dim3 grid(grid_cap((size_t)P * a.off[a.k] / V)), block(256);
+#define PCA_CAT(VV)                                                                           \
+  if (V == VV) {                                                                              \
+    if (split) hipLaunchKernelGGL((cat_nhwc_kernel<VV, true>), grid, block, 0, st, a, whole, P); \
+    else hipLaunchKernelGGL((cat_nhwc_kernel<VV, false>), grid, block, 0, st, a, whole, P);      \
+    return;                                                                                   \
+  }
+  PCA_CAT(8) PCA_CAT(4) PCA_CAT(2) PCA_CAT(1)
+#undef PCA_CAT
 }
 
 // ----------------------------------------------------------------------- cross-entropy

@@ -1013,7 +1013,25 @@ def channel_shuffle(x, groups):
     return out
 
 
+class _CatNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        ctx.sizes = [x.shape[-1] for x in xs]
+        return _C().cat_nhwc(list(xs))
+
+    @staticmethod
+    def backward(ctx, dy):
+        return tuple(_C().split_nhwc(dy.contiguous(), ctx.sizes))
+
+
 def cat(xs, dim=1):
+    """Channel concatenation (densenet.py:20, dla*.py Root, googlenet.py:53, dpn.py:31): on the
+    GPU one native NHWC pass each way (the channel dim is innermost, so torch.cat / its
+    backward's narrow copies are strided gathers)."""
+    xs = list(xs)
+    if (dim == 1 and 1 < len(xs) <= 8 and not _ref(xs[0]) and xs[0].dim() == 4
+            and all(x.dtype == COMPUTE_DTYPE for x in xs)):
+        return to_nchw(_CatNHWC.apply(*[to_nhwc(x) for x in xs]))
     out = torch.cat(xs, dim)
     if not _ref(out) and out.dim() == 4:
         out = out.contiguous(memory_format=torch.channels_last)

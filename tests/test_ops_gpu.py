@@ -259,3 +259,22 @@ def test_dpn_merge_matches_torch():
     ref.backward(dy.float())
     y.backward(dy.contiguous(memory_format=torch.channels_last))
     assert rel(xn.grad, xr.grad) < 1e-2 and rel(on.grad, orr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("widths", [(32, 64), (12, 24, 36), (58, 58), (3, 5, 7)])
+def test_native_channel_cat_matches_torch(widths):
+    """Native NHWC channel concat / split (forward + backward) vs torch.cat."""
+    from pytorch_cifar_amd.ops import functional as OF
+
+    torch.manual_seed(9)
+    xs = [torch.randn(2, w, 5, 5, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+          .requires_grad_(True) for w in widths]
+    refs = [x.detach().float().requires_grad_(True) for x in xs]
+    y = OF.cat(xs, 1)
+    ref = torch.cat(refs, 1)
+    assert torch.equal(y.float(), ref)
+    dy = torch.randn_like(ref).bfloat16()
+    y.backward(dy.contiguous(memory_format=torch.channels_last))
+    ref.backward(dy.float())
+    for x, r in zip(xs, refs):
+        assert torch.equal(x.grad.float(), r.grad)
