@@ -278,3 +278,27 @@ def test_native_channel_cat_matches_torch(widths):
     ref.backward(dy.float())
     for x, r in zip(xs, refs):
         assert torch.equal(x.grad.float(), r.grad)
+
+
+@pytest.mark.parametrize("Cin,Cout,G,k,s", [(12, 44, 1, 3, 1), (96, 96, 32, 3, 2), (3, 6, 1, 5, 1)])
+def test_direct_conv_fallback_matches_fp32(Cin, Cout, G, k, s, monkeypatch):
+    """The scalar direct-conv kernels (PCA_GROUP_PAD=0 fallback): y, dX, dW, db vs fp32."""
+    import torch.nn.functional as F
+    from pytorch_cifar_amd.ops import functional as OF
+
+    monkeypatch.setattr(OF, "_GROUP_PAD", False)
+    torch.manual_seed(10)
+    p = k // 2
+    x = torch.randn(2, Cin, 9, 9, device="cuda").bfloat16().float().requires_grad_(True)
+    w = (torch.randn(Cout, Cin // G, k, k, device="cuda") * 0.2).requires_grad_(True)
+    b = torch.randn(Cout, device="cuda").requires_grad_(True)
+    ref = F.conv2d(x, w, b, s, p, 1, G)
+    dy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(dy)
+    xn = x.detach().bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wn = w.detach().clone().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    bn = b.detach().clone().requires_grad_(True)
+    y, _ = OF.conv2d(xn, wn, bn, s, p, G, False)
+    assert rel(y, ref) < 1e-2
+    y.backward(dy.to(y.dtype))
+    assert rel(xn.grad, x.grad) < 2e-2 and rel(wn.grad, w.grad) < 2e-2 and rel(bn.grad, b.grad) < 2e-2
