@@ -97,6 +97,7 @@ struct CatArgs {
   int k;
 };
 void cat_nhwc_launch(const CatArgs&, bf16*, int, bool, hipStream_t);
+void interleave2_launch(bf16*, bf16*, bf16*, int, int, bool, hipStream_t);
 void dpn_merge_fwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, hipStream_t);
 void dpn_merge_bwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, bf16*, hipStream_t);
 void se_scale_bwd_launch(const bf16*, const bf16*, const float*, int, int, int, bf16*, float*,
@@ -770,6 +771,28 @@ std::vector<Tensor> split_nhwc(const Tensor& whole, const std::vector<int64_t>& 
   return outs;
 }
 
+// shuffle(cat[a, b], 2) for equal widths: a, b [N,H,W,C] -> [N,H,W,2C] interleaved; and back
+Tensor interleave2(const Tensor& a, const Tensor& b) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  TORCH_CHECK(a.sizes() == b.sizes() && a.dim() == 4, "interleave2: equal NHWC shapes");
+  const int P = a.size(0) * a.size(1) * a.size(2), C = a.size(3);
+  auto y = at::empty({a.size(0), a.size(1), a.size(2), 2 * C}, a.options());
+  pca::interleave2_launch(ptr<bf16>(a), ptr<bf16>(b), ptr<bf16>(y), P, C, false, cur_stream());
+  return y;
+}
+
+std::vector<Tensor> deinterleave2(const Tensor& y) {
+  check_bf16(y, "y");
+  TORCH_CHECK(y.dim() == 4 && y.size(3) % 2 == 0, "deinterleave2: even channel count");
+  const int P = y.size(0) * y.size(1) * y.size(2), C = y.size(3) / 2;
+  auto a = at::empty({y.size(0), y.size(1), y.size(2), C}, y.options());
+  auto b = at::empty_like(a);
+  pca::interleave2_launch(ptr<bf16>(a), ptr<bf16>(b), const_cast<bf16*>(ptr<bf16>(y)), P, C, true,
+                          cur_stream());
+  return {a, b};
+}
+
 // DPN dual-path merge: x [N,H,W,Cx], o [N,H,W,Co] NHWC bf16 -> relu(cat[x[:d]+o[:d], x[d:], o[d:]])
 Tensor dpn_merge_fwd(const Tensor& x, const Tensor& o, int d) {
   check_bf16(x, "x");
@@ -984,6 +1007,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("se_scale_bwd", &se_scale_bwd);
   m.def("dpn_merge_fwd", &dpn_merge_fwd);
   m.def("cat_nhwc", &cat_nhwc);
+  m.def("interleave2", &interleave2);
+  m.def("deinterleave2", &deinterleave2);
   m.def("split_nhwc", &split_nhwc);
   m.def("dpn_merge_bwd", &dpn_merge_bwd);
   m.def("act_fwd", &act_fwd);

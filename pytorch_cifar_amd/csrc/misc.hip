@@ -425,6 +425,79 @@ void cat_nhwc_launch(const CatArgs& a, bf16* whole, int P, bool split, hipStream
 #undef PCA_CAT
 }
 
+// ---- ShuffleNetV2 join: shuffle(cat[a, b], groups=2) with equal widths C is the channel
+// interleave y[p][2i] = a[p][i], y[p][2i+1] = b[p][i] (shufflenetv2.py:49/73, ShuffleBlock
+// 10-19); one vectorized pass instead of a concat and a transposing copy. INV de-interleaves
+// (the backward).
+// word-level interleave of two bf16 pairs: (a0 a1), (b0 b1) -> (a0 b0), (a1 b1) and back
+__device__ __forceinline__ void il_words(uint32_t ua, uint32_t ub, uint32_t& lo, uint32_t& hi) {
+  lo = (ua & 0xffffu) | (ub << 16);
+  hi = (ua >> 16) | (ub & 0xffff0000u);
+}
+
+template <int V, bool INV>
+__global__ __launch_bounds__(256) void interleave2_kernel(bf16* __restrict__ a, bf16* __restrict__ b,
+                                                          bf16* __restrict__ y, int P, int C) {
+  const int G = C / V;
+  const int total = P * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G, p = i / G;
+    const size_t ia = (size_t)p * C + gi * V;         // element index in a / b
+    const size_t iy = (size_t)p * 2 * C + gi * 2 * V; // element index in y
+    if constexpr (V == 4) {
+      if constexpr (!INV) {
+        const uint2 va = *reinterpret_cast<const uint2*>(a + ia);
+        const uint2 vb = *reinterpret_cast<const uint2*>(b + ia);
+        uint4 o;
+        il_words(va.x, vb.x, o.x, o.y);
+        il_words(va.y, vb.y, o.z, o.w);
+        *reinterpret_cast<uint4*>(y + iy) = o;
+      } else {
+        const uint4 o = *reinterpret_cast<const uint4*>(y + iy);
+        uint2 va, vb;
+        il_words(o.x, o.y, va.x, vb.x);   // the same word shuffle is its own inverse
+        il_words(o.z, o.w, va.y, vb.y);
+        *reinterpret_cast<uint2*>(a + ia) = va;
+        *reinterpret_cast<uint2*>(b + ia) = vb;
+      }
+    } else if constexpr (V == 2) {
+      if constexpr (!INV) {
+        uint2 o;
+        il_words(*reinterpret_cast<const uint32_t*>(a + ia), *reinterpret_cast<const uint32_t*>(b + ia),
+                 o.x, o.y);
+        *reinterpret_cast<uint2*>(y + iy) = o;
+      } else {
+        const uint2 o = *reinterpret_cast<const uint2*>(y + iy);
+        uint32_t ua, ub;
+        il_words(o.x, o.y, ua, ub);
+        *reinterpret_cast<uint32_t*>(a + ia) = ua;
+        *reinterpret_cast<uint32_t*>(b + ia) = ub;
+      }
+    } else {
+      if constexpr (!INV) {
+        y[iy] = a[ia];
+        y[iy + 1] = b[ia];
+      } else {
+        a[ia] = y[iy];
+        b[ia] = y[iy + 1];
+      }
+    }
+  }
+}
+
+void interleave2_launch(bf16* a, bf16* b, bf16* y, int P, int C, bool inverse, hipStream_t st) {
+  const int V = C % 4 == 0 ? 4 : C % 2 == 0 ? 2 : 1;
+  const dim3 grid(grid_cap((size_t)P * C / V)), block(256);
+#define PCA_IL(VV)                                                                                  \
+  if (V == VV) {                                                                                    \
+    if (inverse) hipLaunchKernelGGL((interleave2_kernel<VV, true>), grid, block, 0, st, a, b, y, P, C); \
+    else hipLaunchKernelGGL((interleave2_kernel<VV, false>), grid, block, 0, st, a, b, y, P, C);        \
+    return;                                                                                         \
+  }
+  PCA_IL(4) PCA_IL(2) PCA_IL(1)
+#undef PCA_IL
+}
+
 // ----------------------------------------------------------------------- cross-entropy
 // logits[N][K] fp32, targets int64. One 256-thread block, deterministic reductions.
 // Writes loss (mean), dlogits = (softmax - onehot) / N, and accumulates

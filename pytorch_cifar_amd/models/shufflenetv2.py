@@ -25,7 +25,7 @@ class SplitBlock(tnn.Module):
 
     def forward(self, x):
         c = int(x.size(1) * self.ratio)
-        return x[:, :c, :, :], x[:, c:, :, :]
+        return F.split_channels(x, c)
 
 
 class BasicBlock(tnn.Module):
@@ -46,7 +46,12 @@ class BasicBlock(tnn.Module):
         out = self.bn1(self.conv1(x2), act="relu")
         out = self.bn2(self.conv2(out))
         out = self.bn3(self.conv3(out), act="relu")
-        return self.shuffle(F.cat([x1, out], 1))
+        return self._join(x1, out)
+
+    def _join(self, a, b):
+        if self.shuffle.groups == 2 and a.shape == b.shape:
+            return F.cat_shuffle2(a, b)          # == shuffle(cat([a, b])), one native pass
+        return self.shuffle(F.cat([a, b], 1))
 
 
 class DownBlock(tnn.Module):
@@ -70,6 +75,8 @@ class DownBlock(tnn.Module):
         left = self.bn2(self.conv2(self.bn1(self.conv1(x))), act="relu")
         right = self.bn3(self.conv3(x), act="relu")
         right = self.bn5(self.conv5(self.bn4(self.conv4(right))), act="relu")
+        if self.shuffle.groups == 2 and left.shape == right.shape:
+            return F.cat_shuffle2(left, right)
         return self.shuffle(F.cat([left, right], 1))
 
 

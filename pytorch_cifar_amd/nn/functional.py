@@ -10,6 +10,7 @@ from ..ops.functional import (  # noqa: F401
     add_act,
     avg_pool2d,
     cat,
+    cat_shuffle2,
     channel_shuffle,
     cross_entropy,
     dpn_merge,
@@ -18,6 +19,7 @@ from ..ops.functional import (  # noqa: F401
     max_pool2d,
     relu,
     se_excite,
+    split_channels,
 )
 
 

@@ -1024,6 +1024,51 @@ class _CatNHWC(torch.autograd.Function):
         return tuple(_C().split_nhwc(dy.contiguous(), ctx.sizes))
 
 
+class _SplitChannels(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, c):
+        ctx.sizes = [c, x.shape[-1] - c]
+        a, b = _C().split_nhwc(x, ctx.sizes)
+        return a, b
+
+    @staticmethod
+    def backward(ctx, da, db):
+        ref = da if da is not None else db
+        shp = list(ref.shape[:-1])
+        da = da.contiguous() if da is not None else ref.new_zeros(shp + [ctx.sizes[0]])
+        db = db.contiguous() if db is not None else ref.new_zeros(shp + [ctx.sizes[1]])
+        return _C().cat_nhwc([da, db]), None
+
+
+def split_channels(x, c):
+    """(x[:, :c], x[:, c:]) as two dense tensors (shufflenetv2.py:22-29 SplitBlock): one native
+    pass, backward one native concat — instead of strided slice copies whose autograd backward
+    zero-fills and adds two full-size tensors."""
+    if _ref(x) or x.dtype != COMPUTE_DTYPE or x.dim() != 4:
+        return x[:, :c], x[:, c:]
+    a, b = _SplitChannels.apply(to_nhwc(x), c)
+    return to_nchw(a), to_nchw(b)
+
+
+class _Interleave2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        return _C().interleave2(a, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        da, db = _C().deinterleave2(dy.contiguous())
+        return da, db
+
+
+def cat_shuffle2(a, b):
+    """channel_shuffle(cat([a, b], 1), groups=2) for equal widths (ShuffleNetV2 joins,
+    shufflenetv2.py:49/73 + ShuffleBlock 10-19): a single channel interleave each way."""
+    if _ref(a) or a.shape != b.shape or a.dtype != COMPUTE_DTYPE or b.dtype != COMPUTE_DTYPE:
+        return channel_shuffle(cat([a, b], 1), 2)
+    return to_nchw(_Interleave2.apply(to_nhwc(a), to_nhwc(b)))
+
+
 def cat(xs, dim=1):
     """Channel concatenation (densenet.py:20, dla*.py Root, googlenet.py:53, dpn.py:31): on the
     GPU one native NHWC pass each way (the channel dim is innermost, so torch.cat / its

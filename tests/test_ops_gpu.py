@@ -302,3 +302,24 @@ def test_direct_conv_fallback_matches_fp32(Cin, Cout, G, k, s, monkeypatch):
     assert rel(y, ref) < 1e-2
     y.backward(dy.to(y.dtype))
     assert rel(xn.grad, x.grad) < 2e-2 and rel(wn.grad, w.grad) < 2e-2 and rel(bn.grad, b.grad) < 2e-2
+
+
+@pytest.mark.parametrize("C", [116, 58, 7])
+def test_split_and_cat_shuffle2_match_torch(C):
+    """Native channel split and fused shuffle(cat([a, b]), 2) vs the torch slice / cat / view
+    composition, forward and backward (bitwise: pure data movement)."""
+    from pytorch_cifar_amd.ops import functional as OF
+
+    torch.manual_seed(11)
+    x = torch.randn(2, 2 * C, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xn, xr = x.clone().requires_grad_(True), x.float().requires_grad_(True)
+    a, b = OF.split_channels(xn, C)
+    ar, br = xr[:, :C], xr[:, C:]
+    assert torch.equal(a.float(), ar) and torch.equal(b.float(), br)
+    y = OF.cat_shuffle2(b, a)
+    yr = torch.cat([br, ar], 1).view(2, 2, C, 4, 4).transpose(1, 2).reshape(2, 2 * C, 4, 4)
+    assert torch.equal(y.float(), yr)
+    dy = torch.randn_like(yr).bfloat16()
+    y.backward(dy.contiguous(memory_format=torch.channels_last))
+    yr.backward(dy.float())
+    assert torch.equal(xn.grad.float(), xr.grad)
