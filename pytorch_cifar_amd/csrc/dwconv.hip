@@ -613,7 +613,12 @@ void dw_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, 
   const int T = KH * KW;
   if (const int kind = dwk_kind(g)) {
     // chunks = partial rows = blocks (grid.x) of the strip-walking kernel
-    const int v = dwk_vec(kind, Co);
+    static const int vcap = [] {   // debug knob: cap the wgrad vector width (register budget A/B)
+      const char* e = getenv("PCA_DWK_WGRAD_V");
+      return e ? atoi(e) : 8;
+    }();
+    int v = dwk_vec(kind, Co);
+    while (v > vcap && v > 2) v >>= 1;
     if (kind == 3 && v == 8) dwk_wgrad_t<3, 8>(x, dy, g, chunks, partial, st);
     else if (kind == 3 && v == 4) dwk_wgrad_t<3, 4>(x, dy, g, chunks, partial, st);
     else if (kind == 3) dwk_wgrad_t<3, 2>(x, dy, g, chunks, partial, st);
