@@ -555,8 +555,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
 # Convs whose per-group widths are not multiples of 8 (ShuffleNet's 25/50/100-channel
 # groups, shufflenet.py:26-33; DPN's groups=32 with 3..24 channels, dpn.py:15; ResNeXt29_32x4d's
 # 4, resnext.py:19; LeNet 3->6->16, densenet_cifar's growth 12, PNASNet-A's 44) run on the MFMA
-# implicit GEMM with every group
-# zero-padded to a multiple of 8 channels on both sides: pad (input, weight) and slice (output,
+# implicit GEMM with every group zero-padded to a multiple of 8 channels on both sides: pad
+# (input, weight) and slice (output,
 # BN statistics) are plain differentiable tensor ops, so autograd carries the gradients back
 # through them. Even where the padded group leaves most of a 64-wide MFMA tile empty (DPN's
 # 3-channel groups) this beats the scalar direct kernels by 10-30x (tools/zoo_bench.py).
