@@ -69,6 +69,34 @@ def _common_flags(incs, abi):
     return flags
 
 
+def source_digest() -> str:
+    """sha256 over every csrc source/header (name + bytes): identifies what a built .so is of."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".cpp", ".h")):
+            h.update(f.encode())
+            with open(os.path.join(CSRC, f), "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()
+
+
+def digest_path() -> str:
+    return ext_path() + ".srchash"
+
+
+def is_stale() -> bool:
+    """True when the in-tree .so is missing or was built from different csrc contents."""
+    if not os.path.exists(ext_path()):
+        return True
+    try:
+        with open(digest_path()) as fh:
+            return fh.read().strip() != source_digest()
+    except OSError:
+        return True
+
+
 def _headers():
     return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
 
@@ -124,7 +152,24 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    with open(digest_path(), "w") as fh:
+        fh.write(source_digest() + "\n")
     return out
+
+
+def build_locked(**kw) -> str:
+    """``build`` under an exclusive file lock, so concurrent ranks build once and then reuse."""
+    import fcntl
+
+    os.makedirs(os.path.dirname(OBJ_DIR), exist_ok=True)
+    with open(os.path.join(os.path.dirname(OBJ_DIR), ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if not is_stale() and not kw.get("force"):
+                return ext_path()
+            return build(**kw)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
 
 
 def main(argv=None):

@@ -62,6 +62,16 @@ def lib():
     global _lib, _err
     if _lib is not None:
         return _wrap(_lib)
+    from . import _build
+
+    if _build.is_stale():
+        # the .so is missing or was built from other csrc contents: never run a stale kernel
+        # library silently (a stale .so ships with the tree to the GPU box)
+        if os.environ.get("PCA_NO_AUTOBUILD", "0") == "1":
+            raise RuntimeError(
+                "pytorch_cifar_amd native extension is missing or stale (csrc changed since it was "
+                "built); run `python -m pytorch_cifar_amd._build`")
+        _build.build_locked()
     try:
         from . import _C  # noqa: F401
 
@@ -70,9 +80,7 @@ def lib():
     except ImportError as e:  # not built yet
         _err = e
     if os.environ.get("PCA_NO_AUTOBUILD", "0") != "1":
-        from . import _build
-
-        _build.build()
+        _build.build_locked(force=True)
         from . import _C  # noqa: F811
 
         _lib = _C

@@ -61,10 +61,13 @@ __global__ void augment_kernel(const uint8_t* __restrict__ data, const int64_t* 
     const int b = i / (H * W);
     const int hw = i % (H * W);
     const int h = hw / W, w = hw % W;
+    // augmentation word k drawn uniformly in [0, span^2 * 2): dy = k % span,
+    // dx = (k / span) % span, flip = k / span^2 (span = 2 * pad + 1) -> exactly uniform offsets
     const int r = rnd[b];
-    const int dy = (r & 0xff) % (2 * pad + 1);
-    const int dx = ((r >> 8) & 0xff) % (2 * pad + 1);
-    const bool flip = (r >> 16) & 1;
+    const int span = 2 * pad + 1;
+    const int dy = r % span;
+    const int dx = (r / span) % span;
+    const bool flip = (r / (span * span)) & 1;
     const int sh = h + dy - pad;
     const int sw0 = flip ? (W - 1 - w) : w;
     const int sw = sw0 + dx - pad;

@@ -7,9 +7,11 @@ augmentation kernel per batch gathers the sampled images, applies crop/flip/norm
 the bf16 NHWC tensor the first conv consumes (RGB padded to 8 channels).  No host work or H2D
 traffic per step, and the augmentation is capturable into the training step's hipGraph.
 
-Sharding follows ``torch.utils.data.DistributedSampler`` exactly (seed + epoch permutation,
+Training shards follow ``torch.utils.data.DistributedSampler`` exactly (seed + epoch permutation,
 padding to a multiple of the world size, ``indices[rank::world]``), with ``set_epoch`` honoured
-(the reference never calls it, main_dist.py:110 — SURVEY App. B #7).
+(the reference never calls it, main_dist.py:110 — SURVEY App. B #7). Evaluation shards are not
+padded, so the all-reduced test accuracy counts each of the 10,000 images exactly once (the
+reference evaluated the full set on every rank, main_dist.py:129-132).
 """
 from __future__ import annotations
 
@@ -26,11 +28,16 @@ from .cifar10 import MEAN, STD
 class ShardSampler:
     """DistributedSampler-equivalent index generator (CPU-side, once per epoch)."""
 
-    def __init__(self, n, world=1, rank=0, shuffle=True, seed=0, drop_last=False):
+    def __init__(self, n, world=1, rank=0, shuffle=True, seed=0, drop_last=False, pad=True):
         self.n, self.world, self.rank = n, world, rank
         self.shuffle, self.seed, self.drop_last = shuffle, seed, drop_last
+        # pad=False (evaluation): no duplicated samples, ranks differ by at most one sample and the
+        # all-reduced counts cover the dataset exactly once
+        self.pad = pad
         self.epoch = 0
-        if drop_last and n % world:
+        if not pad:
+            self.num_samples = len(range(rank, n, world))
+        elif drop_last and n % world:
             self.num_samples = math.ceil((n - world) / world)
         else:
             self.num_samples = math.ceil(n / world)
@@ -46,6 +53,8 @@ class ShardSampler:
             idx = torch.randperm(self.n, generator=g)
         else:
             idx = torch.arange(self.n)
+        if not self.pad:
+            return idx[self.rank::self.world]
         if not self.drop_last:
             pad = self.total_size - idx.numel()
             if pad > 0:
@@ -77,7 +86,8 @@ class DeviceLoader:
         self.fp32 = False
         self.mean, self.std = tuple(mean), tuple(std)
         self.drop_last = drop_last
-        self.sampler = ShardSampler(len(labels), world, rank, shuffle, seed, drop_last=False)
+        self.sampler = ShardSampler(len(labels), world, rank, shuffle, seed, drop_last=False,
+                                    pad=train)
         self.images = torch.from_numpy(np.ascontiguousarray(images)).to(self.device)
         self.labels = torch.from_numpy(np.asarray(labels, dtype=np.int64)).to(self.device)
         self.gen = torch.Generator(device="cpu")
@@ -100,16 +110,17 @@ class DeviceLoader:
             yield idx[b * self.batch_size: (b + 1) * self.batch_size]
 
     def random_words(self, n: int) -> torch.Tensor:
-        """Per-sample augmentation word: crop dy | dx << 8 | flip << 16 (int32)."""
+        """Per-sample augmentation word k (int32), uniform over every (dy, dx, flip) triple:
+        dy = k % span, dx = (k // span) % span, flip = k // span**2 with span = 2 * crop_pad + 1
+        (torchvision RandomCrop / RandomHorizontalFlip draw each offset and the flip uniformly)."""
         p = self.crop_pad
+        span = 2 * p + 1
         if not self.train or (p == 0 and not self.flip):
-            return torch.full((n,), p | (p << 8), dtype=torch.int32, device=self.device)
+            return torch.full((n,), p + p * span, dtype=torch.int32, device=self.device)
         # GPU: the default (graph-safe, philox) generator so the draw is captured into hipGraphs
         gen = None if self.device.type == "cuda" else self.gen
-        r = torch.randint(0, 2 ** 30, (n,), generator=gen, device=self.device, dtype=torch.int32)
-        if not self.flip:
-            r = r & 0xFFFF
-        return r
+        hi = span * span * (2 if self.flip else 1)
+        return torch.randint(0, hi, (n,), generator=gen, device=self.device, dtype=torch.int32)
 
     def make_batch(self, idx: torch.Tensor, rnd: torch.Tensor | None = None):
         """Gather + augment the samples ``idx`` -> (NCHW-shaped inputs, int64 targets)."""
@@ -131,14 +142,14 @@ class DeviceLoader:
         if p:
             H, W = x.shape[2], x.shape[3]
             xp = torch.nn.functional.pad(x, (p, p, p, p))
-            dy = ((rnd & 0xFF) % (2 * p + 1)).long()
-            dx = (((rnd >> 8) & 0xFF) % (2 * p + 1)).long()
+            dy = (rnd % (2 * p + 1)).long()
+            dx = ((rnd // (2 * p + 1)) % (2 * p + 1)).long()
             rows = (dy[:, None] + torch.arange(H)).view(n, 1, H, 1).expand(n, 3, H, W + 2 * p)
             xr = xp.gather(2, rows)
             cols = (dx[:, None] + torch.arange(W)).view(n, 1, 1, W).expand(n, 3, H, W)
             x = xr.gather(3, cols)
         if self.flip:
-            f = ((rnd >> 16) & 1).bool()
+            f = ((rnd // ((2 * p + 1) ** 2)) & 1).bool()
             x[f] = x[f].flip(3)
         m = torch.tensor(self.mean).view(1, 3, 1, 1)
         s = torch.tensor(self.std).view(1, 3, 1, 1)

@@ -12,6 +12,7 @@ Resume tolerates a ``module.`` prefix mismatch (the reference's resume fails on 
 from __future__ import annotations
 
 import os
+import warnings
 
 import torch
 
@@ -51,4 +52,9 @@ def load_checkpoint(path, net, optimizer=None, scheduler=None, map_location="cpu
         optimizer.load_state_dict(ck["optimizer"])
     if scheduler is not None and "scheduler" in ck:
         scheduler.load_state_dict(ck["scheduler"])
+        # The entry points checkpoint inside epoch e, before that epoch's scheduler.step(); the
+        # resumed run starts at e + 1, so advance the schedule once to train e + 1 at lr(e + 1).
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")   # "scheduler.step() before optimizer.step()"
+            scheduler.step()
     return float(ck.get("acc", 0.0)), int(ck.get("epoch", 0))

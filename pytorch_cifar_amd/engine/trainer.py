@@ -62,13 +62,58 @@ class TrainStep:
             self.opt.step()
         return loss
 
+    def _state_tensors(self):
+        """Every tensor a training step mutates: parameters, BN buffers, momenta, metrics."""
+        inner = getattr(self.net, "module", self.net)
+        seen, out = set(), []
+
+        def add(t):
+            if t is not None and id(t) not in seen:
+                seen.add(id(t))
+                out.append(t)
+
+        arena = getattr(self.opt, "arena", None)
+        if arena is not None:
+            add(arena.param_flat)
+            add(arena.mom_flat)
+        else:
+            for p in inner.parameters():
+                add(p.data)
+            for st in self.opt.state.values():
+                add(st.get("momentum_buffer"))
+        for b in inner.buffers():
+            add(b)
+        add(self.metrics)
+        return out
+
     def _capture(self):
+        # The warm-up bodies below are real steps (SGD update, BN running stats, metrics). Snapshot
+        # the state first and roll it back before capture, so the first captured replay is the
+        # first step this batch takes (N graph steps == N eager steps).
+        state = self._state_tensors()
+        snap = [t.clone() for t in state]
+        first = getattr(self.opt, "_arena_first", None)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(3):
                 self._body(self.static_idx)
         torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            for t, v in zip(state, snap):
+                t.copy_(v)
+            known = {id(t) for t in state}
+            for st in self.opt.state.values():   # momenta created by the warm-ups start at zero
+                b = st.get("momentum_buffer")
+                if b is not None and id(b) not in known and getattr(self.opt, "arena", None) is None:
+                    b.zero_()
+        del snap
+        # If this is the run's first step, the restored momenta are zero and the captured
+        # steady-state rule buf = 0.9 * buf + d equals the first-step rule buf = d (dampening 0),
+        # so the graph is exact from its first replay; keep recording the steady-state rule.
+        if first and self.opt.param_groups[0].get("dampening", 0) != 0:
+            raise RuntimeError("hipGraph capture of the first SGD step needs dampening == 0")
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         self.opt.capturing = True
@@ -276,6 +321,7 @@ class Trainer:
                 loss_sum, correct, total = metrics.tolist()
                 self.progress(b, n, "Loss: %.3f | Acc: %.3f%% (%d/%d)"
                               % (loss_sum / (b + 1), 100.0 * correct / max(total, 1), correct, total))
-        loss_sum, correct, total = self._reduce(metrics.tolist())
-        steps = max(1, n) * self.ctx.world
+        # ranks may hold one batch more or less (unpadded eval shards): reduce the batch count too
+        loss_sum, correct, total, steps = self._reduce(metrics.tolist() + [float(min(n, b + 1) if n else 0)])
+        steps = max(1.0, steps)
         return loss_sum / steps, 100.0 * correct / max(total, 1), int(correct), int(total)

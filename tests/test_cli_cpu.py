@@ -52,14 +52,17 @@ def test_checkpoint_optimizer_state(tmp_path):
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10)
     net(torch.randn(2, 3, 32, 32)).sum().backward()
     opt.step()
-    sched.step()
+    sched.step()                      # end of epoch 0
+    opt.step()                        # epoch 1 trains, then the entry points checkpoint ...
     path = str(tmp_path / "c.pth")
     save_checkpoint(path, net, 10.0, 1, optimizer=opt, scheduler=sched)
+    sched.step()                      # ... and only then step the schedule
     net2 = models.LeNet()
     opt2 = SGD(net2.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4)
     sched2 = torch.optim.lr_scheduler.CosineAnnealingLR(opt2, T_max=10)
-    load_checkpoint(path, net2, opt2, sched2)
-    assert sched2.last_epoch == 1
+    _, ep = load_checkpoint(path, net2, opt2, sched2)
+    # resume continues at epoch ep + 1 = 2 with lr(2), not lr(1) (one-epoch lag)
+    assert ep == 1 and sched2.last_epoch == 2
     assert abs(opt2.param_groups[0]["lr"] - opt.param_groups[0]["lr"]) < 1e-12
 
 

@@ -116,3 +116,44 @@ def test_ddp_rccl_inside_hipgraph_matches_eager():
     # same seeds -> same batches and augmentation draws; deterministic wgrad and a world-1 average
     # (sum / 1) make the two runs bitwise comparable
     torch.testing.assert_close(finals[1], finals[0], rtol=0, atol=0)
+
+
+def test_graph_steps_equal_eager_steps():
+    """the hipGraph warm-up bodies must not leak into training state. N captured
+    steps leave parameters, momenta, BN running stats and the metrics buffer where N eager
+    steps leave them (no augmentation randomness: crop 0, flip off)."""
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.data.loader import DeviceLoader
+    from pytorch_cifar_amd.data.synthetic import synthetic_cifar10
+    from pytorch_cifar_amd.engine.arena import ParamArena
+    from pytorch_cifar_amd.engine.optim import SGD
+    from pytorch_cifar_amd.engine.trainer import TrainStep
+
+    import pytorch_cifar_amd
+
+    pytorch_cifar_amd.set_deterministic(True)
+    imgs, labs = synthetic_cifar10(256, seed=7)
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        model = models.ResNet18().cuda()
+        arena = ParamArena(model.parameters())
+        opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4).attach_arena(arena)
+        loader = DeviceLoader(imgs, labs, 64, "cuda", crop_pad=0, flip=False, drop_last=True, seed=0)
+        step = TrainStep(model, opt, loader, 64, graph=graph)
+        loader.set_epoch(0)
+        for idx in loader.batch_indices():
+            step(idx)
+        torch.cuda.synchronize()
+        if graph:
+            assert step.graph is not None, f"graph capture failed: {step.graph_error!r}"
+        runs.append((arena.param_flat.clone(), arena.mom_flat.clone(),
+                     model.bn1.running_mean.clone(), int(model.bn1.num_batches_tracked),
+                     step.metrics.clone()))
+    pytorch_cifar_amd.set_deterministic(False)
+    (p0, m0, r0, n0, k0), (p1, m1, r1, n1, k1) = runs
+    assert n0 == n1 == 4
+    torch.testing.assert_close(k1, k0, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(r1, r0, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p1, p0, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m1, m0, rtol=1e-5, atol=1e-6)

@@ -364,8 +364,9 @@ def test_layout_and_augment(C):
     assert rel_err(back, x) < 1e-2
     data = torch.randint(0, 256, (5, 32, 32, 3), dtype=torch.uint8, device="cuda")
     idx = torch.tensor([4, 0, 2], device="cuda")
-    # crop offsets (dy=4, dx=4 -> identity) and flip on sample 1
-    rnd = torch.tensor([4 | (4 << 8), 4 | (4 << 8) | (1 << 16), 0], dtype=torch.int32, device="cuda")
+    # word k: dy = k % 9, dx = (k // 9) % 9, flip = k // 81; (4, 4) is the identity crop,
+    # sample 1 flips, sample 2 is dy = dx = 0
+    rnd = torch.tensor([4 + 4 * 9, 4 + 4 * 9 + 81, 0], dtype=torch.int32, device="cuda")
     mean, std = [0.4914, 0.4822, 0.4465], [0.2023, 0.1994, 0.2010]
     out = C.augment(data, idx, rnd, 4, mean, std)
     m = torch.tensor(mean, device="cuda")
