@@ -96,11 +96,13 @@ def test_resnet18_trains():
     from pytorch_cifar_amd.engine.trainer import TrainStep, read_metrics
 
     torch.manual_seed(0)
-    imgs, labs = synthetic_cifar10(512, seed=3)
+    # no augmentation: the 256 images are memorised within a few epochs (CPU fp32 run of the same
+    # recipe: 2.39 -> 1.51 -> 0.52 -> 0.04), so a working step must drive the loss well down
+    imgs, labs = synthetic_cifar10(256, seed=3)
     model = models.ResNet18().cuda()
     arena = ParamArena(model.parameters())
     opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4).attach_arena(arena)
-    loader = DeviceLoader(imgs, labs, 128, "cuda", crop_pad=4, flip=True, drop_last=True)
+    loader = DeviceLoader(imgs, labs, 128, "cuda", crop_pad=0, flip=False, drop_last=True)
     step = TrainStep(model, opt, loader, 128, graph=True)
     losses = []
     for ep in range(4):
@@ -111,7 +113,7 @@ def test_resnet18_trains():
         losses.append(m[0] / len(loader))
     assert step.graph is not None, f"graph capture failed: {step.graph_error!r}"
     assert all(torch.isfinite(torch.tensor(losses))), losses
-    assert losses[-1] < losses[0], losses
+    assert losses[-1] < 0.5 * losses[0], losses
 
 
 GPU_ZOO = ["LeNet", "VGG11", "PreActResNet18", "GoogLeNet", "densenet_cifar", "ResNeXt29_2x64d",

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Per-kernel timeline of ONE training step from a rocprofv3 kernel trace.
+
+Reads ``*_kernel_trace.csv`` (``rocprofv3 --kernel-trace --output-format csv``), cuts the last
+complete step at the per-step optimizer launch (``--marker``, default ``sgd_kernel``) and prints,
+in dispatch order, each kernel's start offset, duration and the idle gap before it, plus totals:
+busy time (union of kernel intervals), summed kernel time, and idle time. With hipGraph replay or
+a side stream, overlapping kernels show as negative gaps.
+
+  python tools/step_timeline.py gpurun_out/prof/run_kernel_trace.csv [--step -2] [--md]
+"""
+import argparse
+import csv
+import re
+
+
+def load(path):
+    rows = list(csv.DictReader(open(path)))
+    out = []
+    for r in rows:
+        name = r.get("Kernel_Name") or r.get("KernelName") or r.get("Name")
+        s = int(r.get("Start_Timestamp") or r.get("BeginNs") or r.get("start"))
+        e = int(r.get("End_Timestamp") or r.get("EndNs") or r.get("end"))
+        out.append((s, e, name))
+    out.sort()
+    return out
+
+
+def short(name, n=90):
+    name = re.sub(r"\(.*", "", name) if "(" in name else name
+    name = name.replace("void ", "").replace("pca::", "")
+    return name[:n]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("path")
+    ap.add_argument("--marker", default="sgd_kernel")
+    ap.add_argument("--step", type=int, default=-2, help="which step window (python index over windows)")
+    ap.add_argument("--md", action="store_true")
+    a = ap.parse_args()
+    ks = load(a.path)
+    marks = [i for i, k in enumerate(ks) if a.marker in k[2]]
+    if len(marks) < 2:
+        raise SystemExit("need at least two marker kernels")
+    wins = list(zip(marks[:-1], marks[1:]))
+    i0, i1 = wins[a.step]
+    step = ks[i0 + 1: i1 + 1]
+    t0 = ks[i0][1]
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _ in step:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    wall = step[-1][1] - t0
+    ksum = sum(e - s for s, e, _ in step)
+    print(f"kernels: {len(step)}; step wall (marker to marker): {wall / 1e3:.1f} us; "
+          f"busy (union): {busy / 1e3:.1f} us; summed kernel time: {ksum / 1e3:.1f} us; "
+          f"idle: {(wall - busy) / 1e3:.1f} us\n")
+    if a.md:
+        print("| # | start us | dur us | gap us | kernel |\n|---:|---:|---:|---:|---|")
+    prev_e = t0
+    for j, (s, e, n) in enumerate(step):
+        gap = (s - prev_e) / 1e3
+        if a.md:
+            print(f"| {j} | {(s - t0) / 1e3:.1f} | {(e - s) / 1e3:.1f} | {gap:.1f} | `{short(n)}` |")
+        else:
+            print(f"{j:4d} {(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {gap:6.1f}  {short(n)}")
+        prev_e = max(prev_e, e)
+
+
+if __name__ == "__main__":
+    main()
