@@ -21,8 +21,10 @@ def set_deterministic(on: bool = True) -> None:
     """Bitwise-reproducible training: weight gradients are reduced through ordered slab rows
     instead of fp32 atomics (all other native kernels are already order-deterministic)."""
     from . import _native
+    from .ops import functional
 
     _native.lib().set_deterministic(bool(on))
+    functional.set_deterministic_flag(on)
 
 
 def set_debug_sync(on: bool = True) -> None:

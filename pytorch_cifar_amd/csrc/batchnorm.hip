@@ -17,6 +17,10 @@
 
 namespace pca {
 
+static int g_stat_shards = 0;
+int stat_shards() { return g_stat_shards; }
+void set_stat_shards(int shards) { g_stat_shards = shards; }
+
 // Row-parallel geometry for an [M][C] NHWC matrix: TPR threads cover a row's granules
 // (VEC channels each), RPP rows are processed per pass by one 256-thread block.
 struct RowPar {
@@ -70,7 +74,7 @@ __device__ __forceinline__ void store_vec(bf16* p, const float* f) {
 template <int VEC>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ x, int M,
                                                        RowPar rp, int rows_per_block,
-                                                       float* __restrict__ partial) {
+                                                       float* __restrict__ partial, int shards) {
   __shared__ float red[256 * VEC * 2];
   const int t = threadIdx.x;
   const int gx = t % rp.TPR, ry = t / rp.TPR;
@@ -107,13 +111,12 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ 
           q[v] += red[(tt * VEC + v) * 2 + 1];
         }
       }
-      float* prow = partial + (size_t)blockIdx.x * 2 * rp.C;
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
         const int c = gi * VEC + v;
         if (c < rp.C) {
-          prow[c] = s[v];
-          prow[rp.C + c] = q[v];
+          stat_out(partial, blockIdx.x, shards, 2 * rp.C, c, s[v]);
+          stat_out(partial, blockIdx.x, shards, 2 * rp.C, rp.C + c, q[v]);
         }
       }
     }
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16* __restrict__ dout, const bf16* __restrict__ out, const uint8_t* __restrict__ mask,
     const bf16* __restrict__ y, const float* __restrict__ aux, const bf16* __restrict__ y2,
     const float* __restrict__ aux2, int act, int M, RowPar rp, int rows_per_block,
-    float* __restrict__ partial) {
+    float* __restrict__ partial, int shards) {
   __shared__ float red[256 * VEC * NS];
   const int t = threadIdx.x;
   const int gx = t % rp.TPR, ry = t / rp.TPR;
@@ -381,13 +384,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 #pragma unroll
           for (int v = 0; v < VEC; ++v) acc[k][v] += red[(tt * VEC + v) * NS + k];
       }
-      float* prow = partial + (size_t)blockIdx.x * NS * C;
 #pragma unroll
       for (int k = 0; k < NS; ++k)
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
           const int c = c0 + v;
-          if (c < C) prow[k * C + c] = acc[k][v];
+          if (c < C) stat_out(partial, blockIdx.x, shards, NS * C, k * C + c, acc[k][v]);
         }
     }
     __syncthreads();
@@ -401,8 +403,16 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     const float* __restrict__ gamma, const float* __restrict__ aux2,
     const float* __restrict__ gamma2, int training, float* __restrict__ dgamma,
     float* __restrict__ dbeta, float* __restrict__ dgamma2, float* __restrict__ dbeta2,
-    float* __restrict__ coef, int accumulate) {
+    float* __restrict__ coef, int accumulate, float* __restrict__ zero1, int zero1_n,
+    float* __restrict__ zero2, int zero2_n) {
   __shared__ float red[16][64][3];
+  // block 0 also clears the forward accumulators this BN consumed (sharded-sum mode)
+  if (blockIdx.x == 0) {
+    if (zero1)
+      for (int i = threadIdx.x; i < zero1_n; i += blockDim.x) zero1[i] = 0.f;
+    if (zero2)
+      for (int i = threadIdx.x; i < zero2_n; i += blockDim.x) zero2[i] = 0.f;
+  }
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float acc[3] = {0.f, 0.f, 0.f};
@@ -481,11 +491,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 // coefficients live in registers for the whole kernel (the generic grid-stride kernels re-load
 // them per vector); consecutive threads still read consecutive 16-byte chunks of NHWC rows, and
 // two rows are in flight per thread.
+// `scale`/`shift` (and `scale2`/`shift2`) point at [C] coefficient vectors in global memory
+// (aux rows 2 and 3) or in LDS (the fused-finalize kernels below).
 template <bool RES, bool DUAL, int ACT>
-__global__ __launch_bounds__(256) void bn_apply_rows_kernel(
-    const bf16* __restrict__ y, const float* __restrict__ aux, int C, int M,
-    const bf16* __restrict__ res, const bf16* __restrict__ y2, const float* __restrict__ aux2,
-    bf16* __restrict__ out, uint8_t* __restrict__ mask) {
+__device__ __forceinline__ void bn_apply_rows_body(
+    const bf16* __restrict__ y, const float* scale, const float* shift, int C, int M,
+    const bf16* __restrict__ res, const bf16* __restrict__ y2, const float* scale2,
+    const float* shift2, bf16* __restrict__ out, uint8_t* __restrict__ mask) {
   const int TPR = C >> 3, RPB = 256 / TPR;
   const int g = threadIdx.x % TPR, ro = threadIdx.x / TPR;
   if (ro >= RPB) return;
@@ -493,11 +505,11 @@ __global__ __launch_bounds__(256) void bn_apply_rows_kernel(
   float sc[8], sh[8], sc2[8], sh2[8];
 #pragma unroll
   for (int v = 0; v < 8; ++v) {
-    sc[v] = aux[2 * C + c0 + v];
-    sh[v] = aux[3 * C + c0 + v];
+    sc[v] = scale[c0 + v];
+    sh[v] = shift[c0 + v];
     if constexpr (DUAL) {
-      sc2[v] = aux2[2 * C + c0 + v];
-      sh2[v] = aux2[3 * C + c0 + v];
+      sc2[v] = scale2[c0 + v];
+      sh2[v] = shift2[c0 + v];
     }
   }
   const int rstep = gridDim.x * RPB;
@@ -538,11 +550,22 @@ __global__ __launch_bounds__(256) void bn_apply_rows_kernel(
   }
 }
 
+template <bool RES, bool DUAL, int ACT>
+__global__ __launch_bounds__(256) void bn_apply_rows_kernel(
+    const bf16* __restrict__ y, const float* __restrict__ aux, int C, int M,
+    const bf16* __restrict__ res, const bf16* __restrict__ y2, const float* __restrict__ aux2,
+    bf16* __restrict__ out, uint8_t* __restrict__ mask) {
+  bn_apply_rows_body<RES, DUAL, ACT>(y, aux + 2 * C, aux + 3 * C, C, M, res, y2,
+                                     DUAL ? aux2 + 2 * C : nullptr, DUAL ? aux2 + 3 * C : nullptr,
+                                     out, mask);
+}
+
 // KIND: 0 = no activation, 1 = ReLU through the 1-bit mask, 2 = swish (z recomputed from y)
+// `coef` = [3|6][C] affine coefficients in global memory or LDS (fused-finalize kernel below)
 template <bool RES, bool DUAL, int KIND>
-__global__ __launch_bounds__(256) void bn_bwd_apply_rows_kernel(
+__device__ __forceinline__ void bn_bwd_apply_rows_body(
     const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
-    const float* __restrict__ coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
+    const float* coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
     const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux) {
   constexpr bool MASK = KIND == 1;
   const int TPR = C >> 3, RPB = 256 / TPR;
@@ -617,6 +640,161 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows_kernel(
   }
 }
 
+template <bool RES, bool DUAL, int KIND>
+__global__ __launch_bounds__(256) void bn_bwd_apply_rows_kernel(
+    const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
+    const float* __restrict__ coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux) {
+  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, coef, C, M, dy, dres, y2, dy2, aux);
+}
+
+// ---- fused finalize + apply (sharded accumulators, no finalize launch) ----
+// The producer (conv epilogue / dgrad epilogue / reduce kernel) added its per-channel partial
+// sums into acc[R][NS][C] (stat_out with shards = R). Every block of the consumer folds the R
+// shard rows of all C channels into LDS coefficients (R*NS*C <= 4096 floats for C >= 64,
+// L2-resident), block 0 also publishes aux / running stats / parameter gradients, then the body
+// runs exactly as the unfused kernel. Re-zeroing: each BN's accumulators are zeroed by the OTHER
+// pass of the same BN — the forward kernel's block 0 clears the backward accumulator (its
+// producer, the dgrad epilogue, runs later in the step) and the backward kernel's block 0 clears
+// the forward accumulator(s) (consumed earlier in the step, refilled next step). No ticket, no
+// memset launch, stable addresses for hipGraph replay.
+struct BnFin {
+  float* acc;            // [R][NS][C] this kernel folds
+  int R;
+  float count;           // elements per channel (N*H*W)
+  const float* gamma;
+  const float* beta;
+  float* rmean;          // running stats (forward, may be null)
+  float* rvar;
+  int64_t* nbt;
+  float momentum, eps;
+  float* aux;            // forward out: [4][C] mean, invstd, scale, shift (block 0)
+  const float* aux_in;   // backward in: the forward's [mean | invstd] rows
+  float* dgamma;         // backward out (block 0, accumulated; may be null)
+  float* dbeta;
+  float* zero;           // block 0 zeroes [zero, zero + zero_n) (the other pass's accumulator)
+  int zero_n;
+};
+
+// The fold of the R shard rows is spread over the block: TPC lanes (consecutive threads, a
+// power of two <= R) share a channel, each loads every TPC-th row (independent loads, unrolled),
+// and the lanes combine with shuffles; 256 / TPC channels per pass.
+__device__ __forceinline__ int fin_tpc(int C, int R) {
+  int t = 1;
+  while (t * 2 <= R && t * 2 * C <= 256) t *= 2;
+  return t;
+}
+
+template <int NS_>
+__device__ __forceinline__ void fin_fold(const float* acc, int R, int NS, int C, int c, int j,
+                                         int tpc, bool ok, float* sum) {
+#pragma unroll
+  for (int k = 0; k < NS_; ++k) sum[k] = 0.f;
+  if (ok) {
+#pragma unroll 8
+    for (int r = j; r < R; r += tpc)
+#pragma unroll
+      for (int k = 0; k < NS_; ++k) sum[k] += acc[((size_t)r * NS + k) * C + c];
+  }
+  for (int o = 1; o < tpc; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < NS_; ++k) sum[k] += __shfl_xor(sum[k], o, 64);
+}
+
+__device__ __forceinline__ void bn_fin_forward(const BnFin& f, int C, float* sc, float* sh) {
+  const int tpc = fin_tpc(C, f.R), cpp = blockDim.x / tpc;
+  const int j = threadIdx.x % tpc;
+  for (int cb = 0; cb < C; cb += cpp) {
+    const int c = cb + threadIdx.x / tpc;
+    float sum[2];
+    fin_fold<2>(f.acc, f.R, 2, C, c, j, tpc, c < C, sum);
+    if (j != 0 || c >= C) continue;
+    const double m = (double)sum[0] / f.count;
+    double v = (double)sum[1] / f.count - m * m;
+    if (v < 0.0) v = 0.0;
+    const float mean = (float)m;
+    const float istd = rsqrtf((float)v + f.eps);
+    const float gm = f.gamma ? f.gamma[c] : 1.f;
+    const float bt = f.beta ? f.beta[c] : 0.f;
+    sc[c] = gm * istd;
+    sh[c] = bt - mean * gm * istd;
+    if (blockIdx.x == 0) {
+      f.aux[c] = mean;
+      f.aux[C + c] = istd;
+      f.aux[2 * C + c] = gm * istd;
+      f.aux[3 * C + c] = bt - mean * gm * istd;
+      if (f.rmean) {
+        const double unb = f.count > 1.f ? v * f.count / (f.count - 1.0) : v;
+        f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * mean;
+        f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * (float)unb;
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+}
+
+// training-mode BN backward coefficients: dy = A*dz + B*y + D (per channel); sums = {dz, dz*xhat
+// [, dz*xhat2]}; BN k (0 or 1) uses sums 0 and 1 + k
+template <int NS>
+__device__ __forceinline__ void bn_fin_backward(const BnFin& f, const BnFin& f2, int C,
+                                                float* cf) {
+  const int tpc = fin_tpc(C, f.R), cpp = blockDim.x / tpc;
+  const int j = threadIdx.x % tpc;
+  for (int cb = 0; cb < C; cb += cpp) {
+    const int c = cb + threadIdx.x / tpc;
+    float sum[NS];
+    fin_fold<NS>(f.acc, f.R, NS, C, c, j, tpc, c < C, sum);
+    if (j != 0 || c >= C) continue;
+#pragma unroll
+    for (int k = 0; k < NS - 1; ++k) {
+      const BnFin& b = k == 0 ? f : f2;
+      const float mean = b.aux_in[c], istd = b.aux_in[C + c];
+      const float gm = b.gamma ? b.gamma[c] : 1.f;
+      const float dg = sum[1 + k], db = sum[0];
+      float* o = cf + (size_t)k * 3 * C;
+      o[c] = gm * istd;
+      o[C + c] = -gm * istd * istd * dg / f.count;
+      o[2 * C + c] = -gm * istd * db / f.count + gm * istd * istd * mean * dg / f.count;
+      if (blockIdx.x == 0) {
+        if (b.dgamma) b.dgamma[c] += dg;
+        if (b.dbeta) b.dbeta[c] += db;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void bn_fin_zero(const BnFin& f) {
+  if (blockIdx.x == 0 && f.zero)
+    for (int i = threadIdx.x; i < f.zero_n; i += blockDim.x) f.zero[i] = 0.f;
+}
+
+template <bool RES, bool DUAL, int ACT>
+__global__ __launch_bounds__(256) void bn_apply_acc_rows_kernel(
+    const bf16* __restrict__ y, BnFin f, BnFin f2, int C, int M, const bf16* __restrict__ res,
+    const bf16* __restrict__ y2, bf16* __restrict__ out, uint8_t* __restrict__ mask) {
+  extern __shared__ float lds[];   // [sc | sh | sc2 | sh2][C]
+  bn_fin_forward(f, C, lds, lds + C);
+  if constexpr (DUAL) bn_fin_forward(f2, C, lds + 2 * C, lds + 3 * C);
+  bn_fin_zero(f);
+  __syncthreads();
+  bn_apply_rows_body<RES, DUAL, ACT>(y, lds, lds + C, C, M, res, y2, lds + 2 * C, lds + 3 * C,
+                                     out, mask);
+}
+
+template <bool RES, bool DUAL, int KIND>
+__global__ __launch_bounds__(256) void bn_bwd_apply_acc_rows_kernel(
+    const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
+    BnFin f, BnFin f2, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux) {
+  extern __shared__ float lds[];   // coef [3|6][C]
+  constexpr int NS = DUAL ? 3 : 2;
+  bn_fin_backward<NS>(f, f2, C, lds);
+  bn_fin_zero(f);
+  bn_fin_zero(f2);
+  __syncthreads();
+  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, lds, C, M, dy, dres, y2, dy2, aux);
+}
+
 static bool rows_enabled() {
   static const bool on = [] {
     const char* e = getenv("PCA_BN_ROWS");
@@ -655,7 +833,7 @@ void bn_stats_launch(const bf16* x, int M, int C, float* partial, int P, hipStre
 #define PCA_STATS(V)                                                                              \
   case V: {                                                                                       \
     RowPar rp = make_rowpar(C, V);                                                                \
-    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial); \
+    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial, g_stat_shards); \
     break;                                                                                        \
   }
     PCA_STATS(8) PCA_STATS(4) PCA_STATS(2) PCA_STATS(1)
@@ -730,10 +908,10 @@ void bn_bwd_reduce_launch(const bf16* dout, const bf16* out, const uint8_t* mask
     RowPar rp = make_rowpar(C, V);                                                                 \
     if (y2)                                                                                        \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<V, 3>), dim3(P), dim3(256), 0, st, dout, out, mask, \
-                         y, aux, y2, aux2, act, M, rp, rows, partial);                             \
+                         y, aux, y2, aux2, act, M, rp, rows, partial, g_stat_shards);              \
     else                                                                                           \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<V, 2>), dim3(P), dim3(256), 0, st, dout, out, mask, \
-                         y, aux, y2, aux2, act, M, rp, rows, partial);                             \
+                         y, aux, y2, aux2, act, M, rp, rows, partial, g_stat_shards);              \
     break;                                                                                         \
   }
     PCA_RED(8) PCA_RED(4) PCA_RED(2) PCA_RED(1)
@@ -745,15 +923,16 @@ void bn_bwd_finalize_launch(const float* stat, int R, int NS, int C, float count
                             const float* aux, const float* gamma, const float* aux2,
                             const float* gamma2, int training, float* dgamma, float* dbeta,
                             float* dgamma2, float* dbeta2, float* coef, int accumulate,
-                            hipStream_t st) {
+                            hipStream_t st, float* zero1, int zero1_n, float* zero2,
+                            int zero2_n) {
   if (NS == 3)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<3>, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C,
                        count, aux, gamma, aux2, gamma2, training, dgamma, dbeta, dgamma2, dbeta2,
-                       coef, accumulate);
+                       coef, accumulate, zero1, zero1_n, zero2, zero2_n);
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<2>, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C,
                        count, aux, gamma, aux2, gamma2, training, dgamma, dbeta, dgamma2, dbeta2,
-                       coef, accumulate);
+                       coef, accumulate, zero1, zero1_n, zero2, zero2_n);
 }
 
 void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask, const bf16* y,
@@ -796,6 +975,77 @@ void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask,
     PCA_BWD_V(4) PCA_BWD_V(2) PCA_BWD_V(1)
 #undef PCA_BWD_V
   }
+}
+
+// ---- fused finalize + apply launchers (sharded accumulators); false = not eligible ----
+static int acc_rows_grid(int M, int C) { return rows_grid(M, C); }
+
+bool bn_apply_acc_launch(const bf16* y, int C, int M, float count, float* acc, int R,
+                         const float* gamma, const float* beta, float* rmean, float* rvar,
+                         int64_t* nbt, float momentum, float eps, float* aux, float* acc2, int R2,
+                         const float* gamma2, const float* beta2, float* rmean2, float* rvar2,
+                         int64_t* nbt2, float momentum2, float eps2, float* aux2, const bf16* res,
+                         const bf16* y2, int act, bf16* out, uint8_t* mask, float* zero,
+                         int zero_n, hipStream_t st) {
+  if (!(rows_enabled() && C % 8 == 0 && C <= 2048 &&
+        (act == ACT_RELU || act == ACT_NONE || (act == ACT_SWISH && !res && !y2)) && !(res && y2)))
+    return false;
+  BnFin f{acc, R, count, gamma, beta, rmean, rvar, nbt, momentum, eps, aux, nullptr, nullptr, nullptr,
+          zero, zero_n};
+  BnFin f2{acc2, R2, count, gamma2, beta2, rmean2, rvar2, nbt2, momentum2, eps2, aux2, nullptr,
+           nullptr, nullptr, nullptr, 0};
+  const dim3 gr(acc_rows_grid(M, C)), bl(256);
+  const size_t lds = (size_t)(y2 ? 4 : 2) * C * sizeof(float);
+#define PCA_APPLY(R_, D, A) \
+  hipLaunchKernelGGL((bn_apply_acc_rows_kernel<R_, D, A>), gr, bl, lds, st, y, f, f2, C, M, res, y2, out, mask)
+  if (act == ACT_SWISH) {
+    PCA_APPLY(false, false, ACT_SWISH);
+  } else if (act == ACT_RELU) {
+    if (res) PCA_APPLY(true, false, ACT_RELU);
+    else if (y2) PCA_APPLY(false, true, ACT_RELU);
+    else PCA_APPLY(false, false, ACT_RELU);
+  } else {
+    if (res) PCA_APPLY(true, false, ACT_NONE);
+    else if (y2) PCA_APPLY(false, true, ACT_NONE);
+    else PCA_APPLY(false, false, ACT_NONE);
+  }
+#undef PCA_APPLY
+  return true;
+}
+
+bool bn_bwd_apply_acc_launch(const bf16* dout, const uint8_t* mask, const bf16* y, int C, int M,
+                             float count, float* acc, int R, const float* aux, const float* gamma,
+                             float* dgamma, float* dbeta, const float* aux2, const float* gamma2,
+                             float* dgamma2, float* dbeta2, int act, bf16* dy, bf16* dres,
+                             const bf16* y2, bf16* dy2, float* zero, int zero_n, float* zero2,
+                             int zero2_n, hipStream_t st) {
+  const bool masked = act == ACT_RELU && mask != nullptr;
+  const bool swish = act == ACT_SWISH && !dres && !y2;
+  if (!(rows_enabled() && C % 8 == 0 && C <= 2048 && (masked || act == ACT_NONE || swish)))
+    return false;
+  BnFin f{acc, R, count, gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, aux, dgamma,
+          dbeta, zero, zero_n};
+  BnFin f2{acc, R, count, gamma2, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, aux2,
+           dgamma2, dbeta2, zero2, zero2_n};
+  const dim3 gr(acc_rows_grid(M, C)), bl(256);
+  const size_t lds = (size_t)(y2 ? 6 : 3) * C * sizeof(float);
+#define PCA_BWD(R_, D, K) \
+  hipLaunchKernelGGL((bn_bwd_apply_acc_rows_kernel<R_, D, K>), gr, bl, lds, st, dout, mask, y, f, f2, C, M, dy, dres, y2, dy2, aux)
+  if (masked) {
+    if (dres && y2) PCA_BWD(true, true, 1);
+    else if (dres) PCA_BWD(true, false, 1);
+    else if (y2) PCA_BWD(false, true, 1);
+    else PCA_BWD(false, false, 1);
+  } else if (swish) {
+    PCA_BWD(false, false, 2);
+  } else {
+    if (dres && y2) PCA_BWD(true, true, 0);
+    else if (dres) PCA_BWD(true, false, 0);
+    else if (y2) PCA_BWD(false, true, 0);
+    else PCA_BWD(false, false, 0);
+  }
+#undef PCA_BWD
+  return true;
 }
 
 }  // namespace pca

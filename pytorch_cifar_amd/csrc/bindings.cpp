@@ -68,10 +68,26 @@ void bn_bwd_reduce_launch(const bf16*, const bf16*, const uint8_t*, const bf16*,
                           const bf16*, const float*, int, int, int, float*, int, hipStream_t);
 void bn_bwd_finalize_launch(const float*, int, int, int, float, const float*, const float*,
                             const float*, const float*, int, float*, float*, float*, float*,
-                            float*, int, hipStream_t);
+                            float*, int, hipStream_t, float* zero1 = nullptr, int zero1_n = 0,
+                            float* zero2 = nullptr, int zero2_n = 0);
 void bn_bwd_apply_launch(const bf16*, const bf16*, const uint8_t*, const bf16*, const float*,
                          const float*, int, int, size_t, bf16*, bf16*, const bf16*, bf16*,
                          hipStream_t);
+int stat_shards();
+void set_stat_shards(int shards);
+bool bn_apply_acc_launch(const bf16* y, int C, int M, float count, float* acc, int R,
+                         const float* gamma, const float* beta, float* rmean, float* rvar,
+                         int64_t* nbt, float momentum, float eps, float* aux, float* acc2, int R2,
+                         const float* gamma2, const float* beta2, float* rmean2, float* rvar2,
+                         int64_t* nbt2, float momentum2, float eps2, float* aux2, const bf16* res,
+                         const bf16* y2, int act, bf16* out, uint8_t* mask, float* zero,
+                         int zero_n, hipStream_t st);
+bool bn_bwd_apply_acc_launch(const bf16* dout, const uint8_t* mask, const bf16* y, int C, int M,
+                             float count, float* acc, int R, const float* aux, const float* gamma,
+                             float* dgamma, float* dbeta, const float* aux2, const float* gamma2,
+                             float* dgamma2, float* dbeta2, int act, bf16* dy, bf16* dres,
+                             const bf16* y2, bf16* dy2, float* zero, int zero_n, float* zero2,
+                             int zero2_n, hipStream_t st);
 // misc.hip
 void nchw_to_nhwc_launch(const float*, int, int, int, int, bf16*, hipStream_t);
 void nhwc_to_nchw_launch(const bf16*, int, int, int, int, float*, hipStream_t);
@@ -215,8 +231,22 @@ static void autotune_conv(int kind, int N, int H, int W, int Cin, int Cout, int 
                          pick.first, pick.second);
 }
 
+// RAII: the BN partial-sum form of the producer launches in scope (0 = slab rows)
+struct ShardScope {
+  int prev;
+  explicit ShardScope(int s) : prev(pca::stat_shards()) { pca::set_stat_shards(s); }
+  ~ShardScope() { pca::set_stat_shards(prev); }
+};
+
+// zero-at-rest accumulator [R][NS][C] for the sharded BN partial sums
+void check_acc(const Tensor& acc, int R, int NS, int C) {
+  check_f32(acc, "stat accumulator");
+  TORCH_CHECK(R >= 1 && acc.numel() >= (int64_t)R * NS * C, "stat accumulator must hold R*NS*C floats");
+}
+
 std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<Tensor>& bias,
-                             int stride, int pad, int groups, bool want_stats) {
+                             int stride, int pad, int groups, bool want_stats,
+                             const optional<Tensor>& stat_acc, int acc_rows) {
   check_bf16(x, "x");
   check_bf16(wb, "weight");
   TORCH_CHECK(x.dim() == 4 && wb.dim() == 4, "conv_fwd expects x[N,H,W,C], w[Cout,KH,KW,Cin/G]");
@@ -249,10 +279,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
   }
   auto y = at::empty({N, Ho, Wo, Cout}, x.options());
   Tensor stats;
-  if (want_stats) {
+  const bool use_acc = want_stats && stat_acc.has_value() && stat_acc->defined();
+  if (use_acc) {
+    check_acc(*stat_acc, acc_rows, 2, Cout);
+    stats = *stat_acc;
+  } else if (want_stats) {
     const int gm = pca::conv_fwd_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
     stats = at::empty({gm, 2, Cout}, x.options().dtype(at::kFloat));
   }
+  ShardScope shards(use_acc ? acc_rows : 0);
   if (bias.has_value() && bias->defined()) {
     check_f32(*bias, "bias");
     TORCH_CHECK(bias->numel() == Cout, "bias size");
@@ -275,7 +310,9 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
 std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, int W, int stride,
                                     int pad, int groups, const optional<Tensor>& addend,
                                     const optional<Tensor>& bn_y, const optional<Tensor>& bn_mask,
-                                    const optional<Tensor>& bn_aux) {
+                                    const optional<Tensor>& bn_aux,
+                                    const optional<Tensor>& bn_acc = c10::nullopt,
+                                    int acc_rows = 0) {
   check_bf16(dy, "dy");
   check_bf16(wt, "wt");
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
@@ -324,7 +361,14 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
   const int rows = want_bn ? pca::conv_dgrad_bn_rows(N, H, W, Cin, Cout, KH, KW, stride, pad,
                                                      groups, Ho, Wo)
                            : 0;
-  if (rows > 0) part = at::empty({rows, 2, Cin}, dy.options().dtype(at::kFloat));
+  const bool use_acc = rows > 0 && bn_acc.has_value() && bn_acc->defined();
+  if (use_acc) {
+    check_acc(*bn_acc, acc_rows, 2, Cin);
+    part = *bn_acc;
+  } else if (rows > 0) {
+    part = at::empty({rows, 2, Cin}, dy.options().dtype(at::kFloat));
+  }
+  ShardScope shards(use_acc ? acc_rows : 0);
   pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dx), N, H, W, Cin, Cout, KH, KW,
                          stride, pad, groups, Ho, Wo, cur_stream(), add,
                          wsn > 0 ? ptr<float>(ws) : nullptr,
@@ -504,6 +548,72 @@ std::vector<Tensor> bn_apply(const Tensor& y, const Tensor& aux, const optional<
   return {out, mask};
 }
 
+// Training BN(+act, +residual | +second BN) whose batch sums sit in sharded accumulators (the
+// producing convs added them): finalize folded into the apply kernel. `zero` (this BN's backward
+// accumulator, or none) is cleared by the kernel's block 0. Returns {out, mask, aux, aux2}.
+// Falls back to finalize + apply (+ memset of `zero`) where the fused row kernel does not apply.
+std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, double count,
+                                 const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                                 const Tensor& rmean, const Tensor& rvar,
+                                 const optional<Tensor>& nbt, double momentum, double eps,
+                                 const optional<Tensor>& res, const optional<Tensor>& y2,
+                                 const optional<Tensor>& acc2, int R2,
+                                 const optional<Tensor>& gamma2, const optional<Tensor>& beta2,
+                                 const optional<Tensor>& rmean2, const optional<Tensor>& rvar2,
+                                 const optional<Tensor>& nbt2, double momentum2, double eps2,
+                                 int act, bool want_mask, const optional<Tensor>& zero) {
+  check_bf16(y, "y");
+  const int C = y.size(-1);
+  const int M = y.numel() / C;
+  check_acc(acc, R, 2, C);
+  const bool dual = y2.has_value() && y2->defined();
+  if (dual) {
+    check_bf16(*y2, "y2");
+    TORCH_CHECK(y2->sizes() == y.sizes(), "second BN input shape mismatch");
+    TORCH_CHECK(acc2.has_value() && acc2->defined() && rmean2.has_value() && rvar2.has_value(),
+                "dual BN needs the second accumulator and running stats");
+    check_acc(*acc2, R2, 2, C);
+  }
+  if (res.has_value() && res->defined()) {
+    check_bf16(*res, "res");
+    TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
+  }
+  auto fopt = y.options().dtype(at::kFloat);
+  auto out = at::empty_like(y);
+  Tensor mask;
+  if (want_mask && act == 1 && C % 8 == 0)
+    mask = at::empty({(int64_t)(y.numel() / 8)}, y.options().dtype(at::kByte));
+  auto aux = at::empty({4, C}, fopt);
+  Tensor aux2;
+  if (dual) aux2 = at::empty({4, C}, fopt);
+  const auto st = cur_stream();
+  const bool has_zero = zero.has_value() && zero->defined();
+  if (has_zero) check_f32(*zero, "zero");
+  const bool fused = pca::bn_apply_acc_launch(
+      ptr<bf16>(y), C, M, (float)count, ptr<float>(acc), R, optr<float>(gamma), optr<float>(beta),
+      ptr<float>(rmean), ptr<float>(rvar), optr<int64_t>(nbt), (float)momentum, (float)eps,
+      ptr<float>(aux), dual ? ptr<float>(*acc2) : nullptr, R2, optr<float>(gamma2),
+      optr<float>(beta2), optr<float>(rmean2), optr<float>(rvar2), optr<int64_t>(nbt2),
+      (float)momentum2, (float)eps2, dual ? ptr<float>(aux2) : nullptr, optr<bf16>(res),
+      optr<bf16>(y2), act, ptr<bf16>(out), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr,
+      has_zero ? ptr<float>(*zero) : nullptr, has_zero ? (int)zero->numel() : 0, st);
+  if (!fused) {
+    pca::bn_finalize_launch(ptr<float>(acc), R, C, count, optr<float>(gamma), optr<float>(beta),
+                            ptr<float>(rmean), ptr<float>(rvar), optr<int64_t>(nbt),
+                            (float)momentum, (float)eps, 1, 1, ptr<float>(aux), st);
+    if (dual)
+      pca::bn_finalize_launch(ptr<float>(*acc2), R2, C, count, optr<float>(gamma2),
+                              optr<float>(beta2), ptr<float>(*rmean2), ptr<float>(*rvar2),
+                              optr<int64_t>(nbt2), (float)momentum2, (float)eps2, 1, 1,
+                              ptr<float>(aux2), st);
+    if (has_zero) zero->zero_();
+    pca::bn_apply_launch(ptr<bf16>(y), ptr<float>(aux), C, y.numel(), optr<bf16>(res),
+                         optr<bf16>(y2), dual ? ptr<float>(aux2) : nullptr, act, ptr<bf16>(out),
+                         mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, st);
+  }
+  return {out, mask, aux, aux2};
+}
+
 // Full BN backward: returns {dy, dres, dy2, dgamma, dbeta, dgamma2, dbeta2}
 std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
                                 const optional<Tensor>& mask, const Tensor& y,
@@ -514,7 +624,9 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
                                 const optional<Tensor>& dbeta_acc,
                                 const optional<Tensor>& dgamma2_acc,
                                 const optional<Tensor>& dbeta2_acc,
-                                const optional<Tensor>& partial_in) {
+                                const optional<Tensor>& partial_in,
+                                const optional<Tensor>& acc_in, int acc_rows, bool acc_filled,
+                                const optional<Tensor>& zero1, const optional<Tensor>& zero2) {
   check_bf16(dout, "dout");
   check_bf16(y, "y");
   const int C = y.size(-1);
@@ -528,6 +640,100 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
   const uint8_t* mk = has_mask ? mask->data_ptr<uint8_t>() : nullptr;
   auto st = cur_stream();
   auto fopt = y.options().dtype(at::kFloat);
+  // Parameter gradients are accumulated straight into the caller's .grad buffers when given
+  // (the flat gradient arena); otherwise fresh tensors are returned.
+  auto pick = [&](const optional<Tensor>& acc) {
+    if (acc.has_value() && acc->defined()) {
+      check_f32(*acc, "grad accumulator");
+      TORCH_CHECK(acc->numel() == C, "grad accumulator size");
+      return *acc;
+    }
+    return at::zeros({C}, fopt);
+  };
+  if (training && acc_in.has_value() && acc_in->defined()) {
+    // sharded accumulator path: sums from the consumer conv's dgrad epilogue (acc_filled) or
+    // from the reduce kernel below, folded by the fused apply kernel (which re-zeroes it)
+    const Tensor& acc = *acc_in;
+    check_acc(acc, acc_rows, NS, C);
+    const bool z1 = zero1.has_value() && zero1->defined();
+    const bool z2 = zero2.has_value() && zero2->defined();
+    if (z1) check_f32(*zero1, "zero1");
+    if (z2) check_f32(*zero2, "zero2");
+    float* zp1 = z1 ? ptr<float>(*zero1) : nullptr;
+    float* zp2 = z2 ? ptr<float>(*zero2) : nullptr;
+    const int zn1 = z1 ? (int)zero1->numel() : 0, zn2 = z2 ? (int)zero2->numel() : 0;
+    if (!acc_filled) {
+      // no dgrad epilogue delivered the sums: a separate reduce pass over dout. Its ~1024
+      // blocks would serialise on the accumulator's few shard rows (same-address atomics), so
+      // this case keeps ordered slab rows + the finalize kernel (whose block 0 clears the
+      // forward accumulators) and the accumulator stays untouched.
+      const int P = pca::bn_row_blocks(M, C);
+      auto partial = at::empty({P, NS, C}, fopt);
+      pca::bn_bwd_reduce_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
+                                optr<bf16>(y2), optr<float>(aux2), act, M, C, ptr<float>(partial),
+                                P, st);
+      const float* stat = ptr<float>(partial);
+      int R = P;
+      Tensor folded;
+      if (R > 1024) {
+        folded = at::empty({64, NS, C}, fopt);
+        R = pca::colsum_launch(stat, R, NS * C, ptr<float>(folded), st);
+        stat = ptr<float>(folded);
+      }
+      auto dgamma = pick(dgamma_acc), dbeta = pick(dbeta_acc);
+      Tensor dgamma2, dbeta2;
+      if (dual) {
+        dgamma2 = pick(dgamma2_acc);
+        dbeta2 = pick(dbeta2_acc);
+      }
+      auto coef = at::empty({dual ? 6 : 3, C}, fopt);
+      pca::bn_bwd_finalize_launch(stat, R, NS, C, (float)M, ptr<float>(aux), optr<float>(gamma),
+                                  optr<float>(aux2), optr<float>(gamma2), 1, ptr<float>(dgamma),
+                                  ptr<float>(dbeta), dual ? ptr<float>(dgamma2) : nullptr,
+                                  dual ? ptr<float>(dbeta2) : nullptr, ptr<float>(coef), 1, st,
+                                  zp1, zn1, zp2, zn2);
+      auto dy = at::empty_like(y);
+      Tensor dres, dy2;
+      if (need_dres) dres = at::empty_like(y);
+      if (dual) dy2 = at::empty_like(y);
+      pca::bn_bwd_apply_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
+                               ptr<float>(coef), act, C, y.numel(), ptr<bf16>(dy),
+                               need_dres ? ptr<bf16>(dres) : nullptr, optr<bf16>(y2),
+                               dual ? ptr<bf16>(dy2) : nullptr, st);
+      return {dy, dres, dy2, dgamma, dbeta, dgamma2, dbeta2};
+    }
+    auto dgamma = pick(dgamma_acc), dbeta = pick(dbeta_acc);
+    Tensor dgamma2, dbeta2;
+    if (dual) {
+      dgamma2 = pick(dgamma2_acc);
+      dbeta2 = pick(dbeta2_acc);
+    }
+    auto dy = at::empty_like(y);
+    Tensor dres, dy2;
+    if (need_dres) dres = at::empty_like(y);
+    if (dual) dy2 = at::empty_like(y);
+    const bool fused = pca::bn_bwd_apply_acc_launch(
+        ptr<bf16>(dout), mk, ptr<bf16>(y), C, M, (float)M, ptr<float>(acc), acc_rows,
+        ptr<float>(aux), optr<float>(gamma), ptr<float>(dgamma), ptr<float>(dbeta),
+        optr<float>(aux2), optr<float>(gamma2), dual ? ptr<float>(dgamma2) : nullptr,
+        dual ? ptr<float>(dbeta2) : nullptr, act, ptr<bf16>(dy),
+        need_dres ? ptr<bf16>(dres) : nullptr, optr<bf16>(y2), dual ? ptr<bf16>(dy2) : nullptr,
+        zp1, zn1, zp2, zn2, st);
+    if (!fused) {
+      auto coef = at::empty({dual ? 6 : 3, C}, fopt);
+      pca::bn_bwd_finalize_launch(ptr<float>(acc), acc_rows, NS, C, (float)M, ptr<float>(aux),
+                                  optr<float>(gamma), optr<float>(aux2), optr<float>(gamma2), 1,
+                                  ptr<float>(dgamma), ptr<float>(dbeta),
+                                  dual ? ptr<float>(dgamma2) : nullptr,
+                                  dual ? ptr<float>(dbeta2) : nullptr, ptr<float>(coef), 1, st,
+                                  zp1, zn1, zp2, zn2);
+      pca::bn_bwd_apply_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
+                               ptr<float>(coef), act, C, y.numel(), ptr<bf16>(dy),
+                               need_dres ? ptr<bf16>(dres) : nullptr, optr<bf16>(y2),
+                               dual ? ptr<bf16>(dy2) : nullptr, st);
+    }
+    return {dy, dres, dy2, dgamma, dbeta, dgamma2, dbeta2};
+  }
   Tensor partial;
   int R;
   if (partial_in.has_value() && partial_in->defined() && partial_in->numel() > 0) {
@@ -552,16 +758,6 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
     R = pca::colsum_launch(stat, R, NS * C, ptr<float>(folded), st);
     stat = ptr<float>(folded);
   }
-  // Parameter gradients are accumulated straight into the caller's .grad buffers when given
-  // (the flat gradient arena); otherwise fresh tensors are returned.
-  auto pick = [&](const optional<Tensor>& acc) {
-    if (acc.has_value() && acc->defined()) {
-      check_f32(*acc, "grad accumulator");
-      TORCH_CHECK(acc->numel() == C, "grad accumulator size");
-      return *acc;
-    }
-    return at::zeros({C}, fopt);
-  };
   auto dgamma = pick(dgamma_acc), dbeta = pick(dbeta_acc);
   Tensor dgamma2, dbeta2;
   if (dual) {
@@ -958,12 +1154,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? std::string() : std::string(hipGetErrorString(e));
   }, "hipGetLastError() of this thread as a string ('' = no error); clears it");
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wb"), py::arg("bias"), py::arg("stride"),
+        py::arg("pad"), py::arg("groups"), py::arg("want_stats"), py::arg("stat_acc") = py::none(),
+        py::arg("acc_rows") = 0);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend") = py::none());
   m.def("conv_dgrad_bn", &conv_dgrad_impl, py::arg("dy"), py::arg("wt"), py::arg("H"),
         py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend"),
-        py::arg("bn_y"), py::arg("bn_mask"), py::arg("bn_aux"),
+        py::arg("bn_y"), py::arg("bn_mask"), py::arg("bn_aux"), py::arg("bn_acc") = py::none(),
+        py::arg("acc_rows") = 0,
         "dgrad + fused backward reduce of the producing BN+ReLU -> (dx, partial[rows][2][C])");
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
@@ -990,7 +1189,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("aux"), py::arg("gamma"), py::arg("y2"), py::arg("aux2"), py::arg("gamma2"),
         py::arg("act"), py::arg("training"), py::arg("need_dres"), py::arg("dgamma_acc"),
         py::arg("dbeta_acc"), py::arg("dgamma2_acc"), py::arg("dbeta2_acc"),
-        py::arg("partial_in") = py::none());
+        py::arg("partial_in") = py::none(), py::arg("acc") = py::none(), py::arg("acc_rows") = 0,
+        py::arg("acc_filled") = false, py::arg("zero1") = py::none(),
+        py::arg("zero2") = py::none());
+  m.def("bn_apply_acc", &bn_apply_acc, py::arg("y"), py::arg("acc"), py::arg("R"),
+        py::arg("count"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
+        py::arg("nbt"), py::arg("momentum"), py::arg("eps"), py::arg("res"), py::arg("y2"),
+        py::arg("acc2"), py::arg("R2"), py::arg("gamma2"), py::arg("beta2"), py::arg("rmean2"),
+        py::arg("rvar2"), py::arg("nbt2"), py::arg("momentum2"), py::arg("eps2"), py::arg("act"),
+        py::arg("want_mask"), py::arg("zero") = py::none(),
+        "training BN(+act/+res/+BN2) with the finalize folded in from sharded accumulators");
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("nhwc_to_nchw", &nhwc_to_nchw);
   m.def("augment", &augment);

@@ -5,8 +5,9 @@
 //   * parameters are fp32 masters whose *physical* layout is [Cout][KH][KW][Cin/G]
 //     (torch.channels_last strides on the reference [Cout,Cin,KH,KW] shape), so a conv
 //     weight is already the K-contiguous GEMM operand the MFMA B-fragment wants;
-//   * all reductions accumulate in fp32; per-block partials are written to slabs and
-//     folded by a finalize kernel (deterministic, no cross-XCD atomics on hot counters).
+//   * all reductions accumulate in fp32; per-block partials are written to slabs and folded by
+//     a finalize kernel (deterministic mode), or added into small sharded accumulators that the
+//     consumer folds in its prologue (default; see stat_out below).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -79,6 +80,24 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, x = orig % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
 }
+
+// BatchNorm partial sums leave a producer kernel in one of two forms:
+//   shards == 0: slab row `row` of [rows][rowlen] (deterministic; folded by a finalize kernel),
+//   shards  > 0: an fp32 atomic add into accumulator row `row % shards` of [shards][rowlen].
+// The sharded accumulator is zero at rest: the consuming BN kernel folds it while normalizing and
+// its last workgroup (ticket) zeroes it again, so no finalize launch and no memset per step.
+__device__ __forceinline__ void stat_out(float* base, int row, int shards, size_t rowlen, int col,
+                                         float v) {
+  if (shards > 0)
+    atomicAdd(base + (size_t)(row % shards) * rowlen + col, v);
+  else
+    base[(size_t)row * rowlen + col] = v;
+}
+
+// Process-wide shard count the next producer launch writes with (0 = slab rows); set by the
+// host bindings around a launch (batchnorm.hip).
+int stat_shards();
+void set_stat_shards(int shards);
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_SIGMOID = 3 };
 

@@ -29,6 +29,7 @@ struct C64Geom {
   const uint8_t* bn_mask;
   const float* bn_aux;
   float* bn_part;   // [gridDim.x][2][64]
+  int shards;       // stats / bn_part: 0 = slab rows, >0 = sharded atomic accumulator
 };
 
 namespace c64 {
@@ -275,9 +276,8 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
         s += red[(w * 64 + tid) * 2 + 0];
         q += red[(w * 64 + tid) * 2 + 1];
       }
-      float* srow = stats + (size_t)blockIdx.x * 2 * 64;
-      srow[tid] = s;
-      srow[64 + tid] = q;
+      stat_out(stats, blockIdx.x, g.shards, 128, tid, s);
+      stat_out(stats, blockIdx.x, g.shards, 128, 64 + tid, q);
     }
   } else {
     wait_vmcnt<0>();
@@ -297,11 +297,10 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
         for (int j = tid; j < 256; j += 8)
 #pragma unroll
           for (int q = 0; q < 16; ++q) a[q] += red[j * 16 + q];
-        float* r0 = g.bn_part + (size_t)blockIdx.x * 128 + tid * 8;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          r0[q] = a[q];
-          r0[64 + q] = a[8 + q];
+          stat_out(g.bn_part, blockIdx.x, g.shards, 128, tid * 8 + q, a[q]);
+          stat_out(g.bn_part, blockIdx.x, g.shards, 128, 64 + tid * 8 + q, a[8 + q]);
         }
       }
     }
@@ -346,6 +345,7 @@ void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const 
   g.bn_mask = bn_mask;
   g.bn_aux = bn_aux;
   g.bn_part = dgrad ? bn_part : nullptr;
+  g.shards = stat_shards();
   const dim3 grid(c64_grid(g.tiles)), block(256);
   if (dgrad)
     hipLaunchKernelGGL((conv3x3_c64_kernel<true, false>), grid, block, 0, st, a, w, y, nullptr,

@@ -59,6 +59,7 @@ struct ConvGeom {
   const uint8_t* bn_mask;
   const float* bn_aux;  // [mean | istd | ...][Co]
   float* bn_part;       // [rows][2][Co]
+  int shards;           // BN partial sums (stats / bn_part): 0 = slab rows, >0 = sharded atomics
 };
 
 // dz = dX * relu'(y), accumulated as (sum dz, sum dz * xhat) for 8 channels
@@ -81,7 +82,7 @@ __device__ __forceinline__ void bn_fuse_acc(const uint4& v, const bf16* y, uint8
 template <int NT>
 __device__ __forceinline__ void bn_fuse_flush(float* red, const float* s1, const float* s2,
                                               int CG, int ch0, int cvalid, int Co, float* part,
-                                              int row) {
+                                              int row, int shards) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -96,11 +97,10 @@ __device__ __forceinline__ void bn_fuse_flush(float* red, const float* s1, const
     for (int j = tid; j < NT; j += CG)
 #pragma unroll
       for (int q = 0; q < 16; ++q) a[q] += red[j * 16 + q];
-    float* r0 = part + (size_t)row * 2 * Co + ch0 + tid * 8;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      r0[q] = a[q];
-      r0[Co + q] = a[8 + q];
+      stat_out(part, row, shards, 2 * Co, ch0 + tid * 8 + q, a[q]);
+      stat_out(part, row, shards, 2 * Co, Co + ch0 + tid * 8 + q, a[8 + q]);
     }
   }
 }
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
     if (bnf) {   // slab row per (M-walker, parity class); channels of this block's N tile
       const int row = PARITY ? (int)blockIdx.x * 4 + cls : (int)blockIdx.x;
       bn_fuse_flush<NT>(reinterpret_cast<float*>(smem), bs1, bs2, CG_, grp * g.Cn + n0,
-                        g.Cn - n0, g.Co, g.bn_part, row);
+                        g.Cn - n0, g.Co, g.bn_part, row, g.shards);
     }
   }
   if constexpr (STATS && !SPLITK) {
@@ -522,9 +522,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       }
       const int c = n0 + tid;
       if (c < g.Cn) {
-        float* srow = stats + (size_t)blockIdx.x * 2 * g.Co;
-        srow[grp * g.Cn + c] = s;
-        srow[g.Co + grp * g.Cn + c] = q;
+        stat_out(stats, blockIdx.x, g.shards, 2 * g.Co, grp * g.Cn + c, s);
+        stat_out(stats, blockIdx.x, g.shards, 2 * g.Co, g.Co + grp * g.Cn + c, q);
       }
     }
   }
@@ -866,9 +865,8 @@ __global__ __launch_bounds__(WAVES * 64) void conv_igemm_ph_kernel(const bf16* _
       const float q = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
       const int c = n0 + tid;
       if (c < g.Cn) {
-        float* srow = stats + (size_t)blockIdx.x * 2 * g.Co;
-        srow[grp * g.Cn + c] = s;
-        srow[g.Co + grp * g.Cn + c] = q;
+        stat_out(stats, blockIdx.x, g.shards, 2 * g.Co, grp * g.Cn + c, s);
+        stat_out(stats, blockIdx.x, g.shards, 2 * g.Co, g.Co + grp * g.Cn + c, q);
       }
     }
   }
@@ -1217,7 +1215,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                            const bf16* __restrict__ bn_y,
                                                            const uint8_t* __restrict__ bn_mask,
                                                            const float* __restrict__ bn_aux,
-                                                           float* __restrict__ bn_part) {
+                                                           float* __restrict__ bn_part,
+                                                           int shards) {
   __shared__ float red[2 * 2048];
   const int CG = Co >> 3;             // 8-channel groups per row (Co <= 2048: CG <= 256)
   const int RP = 256 / CG;            // rows per pass
@@ -1277,15 +1276,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       red[(rr * Co + cg * 8 + q) * 2 + 1] = active ? bs2[q] : 0.f;
     }
     __syncthreads();
-    float* prow = bn_part + (size_t)blockIdx.x * 2 * Co;
     for (int c = tid; c < Co; c += 256) {
       float s0 = 0.f, q0 = 0.f;
       for (int k = 0; k < RP; ++k) {
         s0 += red[(k * Co + c) * 2 + 0];
         q0 += red[(k * Co + c) * 2 + 1];
       }
-      prow[c] = s0;
-      prow[Co + c] = q0;
+      stat_out(bn_part, blockIdx.x, shards, 2 * Co, c, s0);
+      stat_out(bn_part, blockIdx.x, shards, 2 * Co, Co + c, q0);
     }
     return;
   }
@@ -1298,15 +1296,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       }
     }
     __syncthreads();
-    float* srow = stats + (size_t)blockIdx.x * 2 * Co;
     for (int c = tid; c < Co; c += 256) {
       float s0 = 0.f, q0 = 0.f;
       for (int k = 0; k < RP; ++k) {
         s0 += red[(k * Co + c) * 2 + 0];
         q0 += red[(k * Co + c) * 2 + 1];
       }
-      srow[c] = s0;
-      srow[Co + c] = q0;
+      stat_out(stats, blockIdx.x, shards, 2 * Co, c, s0);
+      stat_out(stats, blockIdx.x, shards, 2 * Co, Co + c, q0);
     }
   }
 }
@@ -1337,6 +1334,7 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   g.bn_mask = nullptr;
   g.bn_aux = nullptr;
   g.bn_part = nullptr;
+  g.shards = stat_shards();
   return g;
 }
 
@@ -1483,10 +1481,10 @@ static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, co
     const int gx = splitk_reduce_grid(M, g.Co, &rpb);
     if (stats)
       hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
-                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part);
+                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards);
     else
       hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
-                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part);
+                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards);
     return;
   }
   const ConvGeom& g = g0;
@@ -2070,7 +2068,7 @@ std::vector<std::pair<int, int>> wgrad_tune_candidates(int N, int H, int W, int 
   const int64_t P = (int64_t)N * ((H + 2 * pad - KH) / stride + 1) * ((W + 2 * pad - KW) / stride + 1);
   std::vector<std::pair<int, int>> c;
   for (int cfg : cfgs)
-    for (int sp : {-1, 1, 2, 4, 8, 16, 32, -2, -4, -8}) {
+    for (int sp : {-1, 1, 2, 4, 8, 16, 32, 64, -2, -4, -8, -16, -32, -64, -128}) {
       if (sp > 1 && P / sp < 256) continue;
       if (sp <= -2 && (cfg < 16 || P / -sp < 256)) continue;   // slab counts: halo / wide only
       c.emplace_back(cfg, sp);

@@ -35,10 +35,17 @@ class Conv2d(nn.Conv2d):
     def forward(self, x, want_stats=None):
         if want_stats is None:
             want_stats = self.training
+        want_stats = bool(want_stats and not OF._ref(x))
+        acc = None
+        # once a fusable BatchNorm consumed this conv's statistics (it sets _pca_acc_ok), they
+        # travel through the conv's sharded accumulator instead of a slab (ops.functional.StatAcc)
+        if want_stats and self.__dict__.get("_pca_acc_ok") and OF.acc_enabled(self.out_channels, x.device):
+            acc = OF.stat_acc(self, "fwd", self.out_channels, 2, x.device)
         y, stats = OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.groups,
-                             bool(want_stats and not OF._ref(x)))
+                             want_stats, acc)
         if stats is not None:
             setattr(y, _STATS_ATTR, stats)
+            y._pca_stats_src = self
         return y
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):

@@ -319,20 +319,110 @@ def set_fuse_bn_backward(on: bool) -> None:
 
 
 class _BNSrc:
-    __slots__ = ("y", "mask", "aux", "part", "dx")
+    __slots__ = ("y", "mask", "aux", "part", "dx", "acc")
 
-    def __init__(self, y, mask, aux):
+    def __init__(self, y, mask, aux, acc=None):
         self.y, self.mask, self.aux = y, mask, aux
         self.part = None
         self.dx = None
+        self.acc = acc        # the BN's backward StatAcc (sharded-accumulator mode) or None
+
+
+# ------------------------------------------------- sharded BatchNorm-sum accumulators
+# Training BatchNorm needs per-channel batch sums before it can normalize (forward: sum, sumsq of
+# the conv output; backward: sum dz, sum dz*xhat). Their producers (conv / dgrad epilogues, the
+# reduce kernels) add per-workgroup partials with fp32 atomics into a small accumulator of R shard
+# rows (persistent, owned by the producing conv / the BN); the consuming BN kernel folds the R
+# rows in its prologue. Each accumulator is re-zeroed by block 0 of the OTHER pass of the same BN
+# (the forward kernel clears the BN's backward accumulator, the backward kernel the forward
+# one(s)), so a training step needs no finalize launch (37 per ResNet-18 step), no memset and no
+# cross-block ticket, and the buffers stay valid under hipGraph replay. A small state machine
+# (clean -> filled -> used) falls back to a memset only when a pass is skipped (a forward without
+# backward). Deterministic mode (ordered slab rows + finalize kernel) and PCA_BN_ACC=0 turn it off.
+_BN_ACC = os.environ.get("PCA_BN_ACC", "1") != "0"
+_DETERMINISTIC = False
+
+
+def set_deterministic_flag(on: bool) -> None:
+    global _DETERMINISTIC
+    _DETERMINISTIC = bool(on)
+
+
+def acc_shards(C: int) -> int:
+    """Shard rows of a C-channel accumulator: the consumer folds R*2*C <= 4096 floats per block
+    (64 <= C <= 1024) while the producers' same-address atomics spread over R rows."""
+    return max(2, min(32, 2048 // max(1, C)))
+
+
+class StatAcc:
+    """[R][NS][C] fp32 accumulator of sharded BN partial sums.
+
+    ``state``: "clean" (all zero), "filled" (a producer added into it), "used" (a consumer folded
+    it; it is cleared by the other pass of its BN, or by a memset before the next production)."""
+
+    __slots__ = ("buf", "R", "NS", "C", "state")
+
+    def __init__(self, C, NS, device):
+        self.C, self.NS, self.R = C, NS, acc_shards(C)
+        self.buf = torch.zeros(self.R * NS * C, dtype=torch.float32, device=device)
+        self.state = "clean"
+
+    def slab(self, ns=2):
+        """[R][ns][C] view (finalize fallback path)."""
+        return self.buf[: self.R * ns * self.C].view(self.R, ns, self.C)
+
+    def ensure_clean(self):
+        if self.state != "clean":
+            self.buf.zero_()
+            self.state = "clean"
+
+    def begin(self):
+        """Called before a producer adds in."""
+        self.ensure_clean()
+        self.state = "filled"
+
+
+def acc_enabled(C: int, device) -> bool:
+    return (_BN_ACC and device.type == "cuda" and C % 8 == 0 and C <= 2048
+            and not _FORCE_REFERENCE and not (_DETERMINISTIC or _C().deterministic()))
+
+
+def stat_acc(owner, role: str, C: int, NS: int, device) -> StatAcc:
+    """The persistent accumulator of ``owner`` (a module) for ``role`` on ``device``."""
+    d = owner.__dict__.get("_pca_acc")
+    if d is None:
+        d = owner.__dict__["_pca_acc"] = {}
+    key = (role, device.index if device.index is not None else torch.cuda.current_device())
+    a = d.get(key)
+    if a is None or a.C != C or a.NS < NS:
+        a = d[key] = StatAcc(C, NS, device)
+    return a
+
+
+def _bn_fusable(C, act, has_res, dual, bn, bn2=None):
+    """Can the fused finalize+apply row kernel serve this BN (training mode)?"""
+    a = ACT[act]
+    if not (C % 8 == 0 and C <= 2048 and (a in (0, 1) or (a == 2 and not has_res and not dual))
+            and not (has_res and dual)):
+        return False
+    return bn.running_mean is not None and (bn2 is None or bn2.running_mean is not None)
 
 
 def _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add):
     if src is None:
         return C.conv_dgrad(dy, wt, H, W, stride, padding, groups, add)
-    dx, part = C.conv_dgrad_bn(dy, wt, H, W, stride, padding, groups, add, src.y, src.mask, src.aux)
+    acc = src.acc
+    if acc is not None:
+        acc.begin()
+        dx, part = C.conv_dgrad_bn(dy, wt, H, W, stride, padding, groups, add, src.y, src.mask,
+                                   src.aux, acc.buf, acc.R)
+    else:
+        dx, part = C.conv_dgrad_bn(dy, wt, H, W, stride, padding, groups, add, src.y, src.mask,
+                                   src.aux)
     if part.numel():
         src.part, src.dx = part, dx   # the reference to dx keeps autograd from adding into it
+    elif acc is not None:
+        acc.state = "clean"           # the selected kernel could not fuse: nothing was added
     return dx
 
 
@@ -341,7 +431,7 @@ class _ConvMFMA(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, groups, want_stats, cin_pad, slot=None,
-                owner=False, bnsrc=None):
+                owner=False, bnsrc=None, acc=None):
         C = _C()
         ctx.slot, ctx.owner = slot, owner
         ctx.bnsrc = bnsrc
@@ -355,7 +445,12 @@ class _ConvMFMA(torch.autograd.Function):
             wb, wt = C.weight_prep(w_phys, groups, need_dx)
         else:
             wb, wt = _prepped_weight(weight, groups, w_phys, need_dx)
-        y, stats = C.conv_fwd(x, wb, bias, stride, padding, groups, want_stats)
+        if acc is not None and want_stats:
+            acc.begin()
+            y, _ = C.conv_fwd(x, wb, bias, stride, padding, groups, True, acc.buf, acc.R)
+            stats = None                  # delivered through the accumulator (conv2d returns it)
+        else:
+            y, stats = C.conv_fwd(x, wb, bias, stride, padding, groups, want_stats)
         ctx.geom = (stride, padding, groups, cin_pad, x.shape[1], x.shape[2])
         ctx.save_for_backward(x, wt if need_dx else None)
         ctx.weight = weight
@@ -371,7 +466,7 @@ class _ConvMFMA(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return (None,) * 11
+            return (None,) * 12
         C = _C()
         x, wt = ctx.saved_tensors
         stride, padding, groups, cin_pad, H, W = ctx.geom
@@ -426,7 +521,7 @@ class _ConvMFMA(torch.autograd.Function):
                     G.accumulate(bias, db)
                 else:
                     db_ret = db
-        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None
+        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None, None
 
 
 class _ConvDirect(torch.autograd.Function):
@@ -512,8 +607,9 @@ class _ConvDepthwise(torch.autograd.Function):
         return dx, dw_ret, None, None
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False):
-    """NCHW-shaped conv. On GPU returns (y, stats) where stats are BN partials (or None)."""
+def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False, acc=None):
+    """NCHW-shaped conv. On GPU returns (y, stats) where stats are BN partials (a slab tensor, or
+    ``acc`` — a :class:`StatAcc` the epilogue added into — when one is given), or None."""
     if isinstance(stride, (tuple, list)):
         assert stride[0] == stride[1]
         stride = stride[0]
@@ -539,7 +635,9 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
         slot, owner = _slot_for_conv(x)
         bnsrc = getattr(x, "_pca_bnsrc", None) if x.requires_grad else None
         y, stats = _ConvMFMA.apply(to_nhwc(x), weight, bias, stride, padding, groups, want_stats, 0,
-                                   slot, owner, bnsrc)
+                                   slot, owner, bnsrc, acc if want_stats else None)
+        if want_stats and acc is not None:
+            return to_nchw(y), acc
         return to_nchw(y), (stats if want_stats else None)
     if groups == 1 and cout_g % 8 == 0 and Cin < 8 * 2 and Cout >= 16:
         # stem conv on 3-channel images: pad channels to 8 and run on MFMA
@@ -619,14 +717,21 @@ def add_bias(y_nhwc, bias):
 
 # -------------------------------------------------------------------------- batch norm
 class _BNCfg:
-    __slots__ = ("bn", "bn2", "act", "training", "count", "src")
+    __slots__ = ("bn", "bn2", "act", "training", "count", "src", "bacc", "faccs")
 
     def __init__(self, bn, bn2, act, training, count):
         self.bn, self.bn2, self.act, self.training, self.count = bn, bn2, act, training, count
         self.src = None
+        self.bacc = None      # the BN's backward StatAcc (sharded sums of dz, dz*xhat[, dz*xhat2])
+        self.faccs = ()       # forward StatAccs this BN consumed (cleared by its backward kernel)
 
 
 def _bn_aux(C, bn, y, stats, training, count):
+    if isinstance(stats, StatAcc):
+        # an accumulator the fused kernel cannot consume here: finalize from its shard rows
+        aux = _bn_aux(C, bn, y, stats.slab(), training, count)
+        stats.state = "used"
+        return aux
     use_batch = training or bn.running_mean is None
     rm = bn.running_mean
     rv = bn.running_var
@@ -650,12 +755,50 @@ class _BatchNormAct(torch.autograd.Function):
     def forward(ctx, y, gamma, beta, res, y2, gamma2, beta2, stats, stats2, cfg, slot=None):
         C = _C()
         ctx.slot = slot
-        aux = _bn_aux(C, cfg.bn, y, stats if stats is not None and stats.numel() else None, cfg.training, cfg.count)
-        aux2 = None
-        if y2 is not None:
-            aux2 = _bn_aux(C, cfg.bn2, y2, stats2 if stats2 is not None and stats2.numel() else None, cfg.training, cfg.count)
         relu = ACT[cfg.act] == 1
-        out, mask = C.bn_apply(y, aux, res, y2, aux2, ACT[cfg.act], relu)
+        bn, bn2 = cfg.bn, cfg.bn2
+        fused = (cfg.training and isinstance(stats, StatAcc) and
+                 (y2 is None or isinstance(stats2, StatAcc)) and
+                 _bn_fusable(y.shape[-1], cfg.act, res is not None, y2 is not None, bn, bn2))
+        if fused:
+            def mom(b):
+                return b.momentum if b.momentum is not None else 0.1
+
+            a2 = stats2 if y2 is not None else None
+            out, mask, aux, aux2 = C.bn_apply_acc(
+                y, stats.buf, stats.R, float(cfg.count),
+                bn.weight.detach() if bn.weight is not None else None,
+                bn.bias.detach() if bn.bias is not None else None,
+                bn.running_mean, bn.running_var, bn.num_batches_tracked, mom(bn), bn.eps,
+                res, y2, a2.buf if a2 is not None else None, a2.R if a2 is not None else 0,
+                bn2.weight.detach() if (a2 is not None and bn2.weight is not None) else None,
+                bn2.bias.detach() if (a2 is not None and bn2.bias is not None) else None,
+                bn2.running_mean if a2 is not None else None,
+                bn2.running_var if a2 is not None else None,
+                bn2.num_batches_tracked if a2 is not None else None,
+                mom(bn2) if a2 is not None else 0.1, bn2.eps if a2 is not None else 1e-5,
+                ACT[cfg.act], relu, cfg.bacc.buf if cfg.bacc is not None else None)
+            if cfg.bacc is not None:
+                cfg.bacc.state = "clean"      # block 0 cleared this BN's backward accumulator
+            stats.state = "used"
+            cfg.faccs = (stats,) if a2 is None else (stats, a2)
+            if a2 is not None:
+                a2.state = "used"
+            if aux2 is not None and not aux2.numel():
+                aux2 = None
+            if mask is not None and not mask.numel():
+                mask = None
+        else:
+            aux = _bn_aux(C, bn, y, stats if isinstance(stats, StatAcc) or (stats is not None and stats.numel()) else None,
+                          cfg.training, cfg.count)
+            aux2 = None
+            if y2 is not None:
+                aux2 = _bn_aux(C, bn2, y2, stats2 if isinstance(stats2, StatAcc) or (stats2 is not None and stats2.numel()) else None,
+                               cfg.training, cfg.count)
+            out, mask = C.bn_apply(y, aux, res, y2, aux2, ACT[cfg.act], relu)
+            if cfg.bacc is not None:
+                cfg.bacc.ensure_clean()
+            cfg.faccs = tuple(a for a in (stats, stats2) if isinstance(a, StatAcc))
         ctx.cfg = cfg
         ctx.has_res = res is not None
         # ReLU backward needs only the sign of the output: keep the 1-bit mask when the kernel
@@ -666,7 +809,7 @@ class _BatchNormAct(torch.autograd.Function):
         ctx.bnsrc = None
         # (grad mode is off inside Function.forward: the caller decided it in cfg.src)
         if cfg.src is not None and relu and has_mask and y2 is None:
-            ctx.bnsrc = cfg.src = _BNSrc(y, mask, aux)
+            ctx.bnsrc = cfg.src = _BNSrc(y, mask, aux, cfg.bacc)
         else:
             cfg.src = None
         return out
@@ -690,18 +833,37 @@ class _BatchNormAct(torch.autograd.Function):
             g2, b2 = acc(bn2.weight), acc(bn2.bias)
         part = None
         src = ctx.bnsrc
+        acc = cfg.bacc if (cfg.training or bn.running_mean is None) else None
         if src is not None:
             if src.part is not None and src.dx is not None and dout.data_ptr() == src.dx.data_ptr() \
                     and dout.shape == src.dx.shape:
                 part = src.part           # reduced by the consumer conv's dgrad epilogue
             src.part = src.dx = None
             ctx.bnsrc = None
+        filled = False
+        zeros = [None, None]
+        if acc is not None:
+            if part is not None and part.data_ptr() == acc.buf.data_ptr():
+                filled = True             # the dgrad epilogue added into the accumulator
+            else:
+                acc.ensure_clean()        # filled by a dgrad whose output is not dout: discard
+            part = None
+            # unfilled: the backward takes its slab-reduce path and leaves the accumulator clean
+            acc.state = "used" if filled else "clean"
+            # the forward accumulators this BN consumed are cleared by the backward kernel
+            for i, fa in enumerate(cfg.faccs):
+                if fa.state == "used":
+                    zeros[i] = fa.buf
+                    fa.state = "clean"
+            cfg.faccs = ()
         dy, dres, dy2, dg, db, dg2, db2 = C.bn_backward(
             dout, out, mask, y, aux,
             bn.weight.detach() if bn.weight is not None else None,
             y2, aux2,
             bn2.weight.detach() if (bn2 is not None and bn2.weight is not None) else None,
-            ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2, part)
+            ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2, part,
+            acc.buf if acc is not None else None, acc.R if acc is not None else 0, filled,
+            zeros[0], zeros[1])
         ret = {}
 
         def deliver(p, buf, val, slot):
@@ -776,6 +938,17 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
     cfg = _BNCfg(bn, bn2, act, training, N * H * W)
     if _FUSE_BN_BWD and torch.is_grad_enabled() and training:
         cfg.src = True                # request: forward replaces it with the _BNSrc record
+    if training and acc_enabled(Cc, y.device) and \
+            _bn_fusable(Cc, act, residual is not None, bn2 is not None, bn, bn2):
+        # (also without grad: the forward kernel then just keeps it clear)
+        cfg.bacc = stat_acc(bn, "bwd", Cc, 3 if bn2 is not None else 2, y.device)
+        # the producing conv(s) may deliver their statistics through accumulators from now on
+        p1 = getattr(x, "_pca_stats_src", None)
+        p2 = getattr(residual_bn[1], "_pca_stats_src", None) if residual_bn is not None else None
+        if p1 is not None and (bn2 is None or p2 is not None):
+            p1._pca_acc_ok = True
+            if p2 is not None:
+                p2._pca_acc_ok = True
     out = _BatchNormAct.apply(y, bn.weight, bn.bias, res, y2,
                               bn2.weight if bn2 is not None else None,
                               bn2.bias if bn2 is not None else None, stats, st2, cfg,

@@ -40,11 +40,23 @@ def _run(model, x, y, device, stock=False):
     return out.float()
 
 
-def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True):
+def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True, warm=0,
+                  return_models=False):
     torch.manual_seed(0)
     ref = ctor()
     native = copy.deepcopy(ref).cuda()
     stock = copy.deepcopy(ref).cuda()
+    for _ in range(warm):
+        # earlier training steps (running stats move, the convs switch their BN statistics to
+        # the sharded accumulators once a BN consumed them): compare the step after
+        xw = torch.randn(batch, 3, 32, 32)
+        yw = torch.randint(0, 10, (batch,))
+        _run(ref, xw, yw, "cpu")
+        _run(native, xw, yw, "cuda")
+        _run(stock, xw, yw, "cuda", stock=True)
+        for m in (ref, native, stock):
+            for p in m.parameters():
+                p.grad = None
     x = torch.randn(batch, 3, 32, 32)
     y = torch.randint(0, 10, (batch,))
     out_r = _run(ref, x, y, "cpu")
@@ -78,6 +90,8 @@ def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True):
                 assert en <= factor * es + slack or small, (n, en, es)
             else:
                 assert int(bn.item()) == int(br.item()), n
+    if return_models:
+        return e_n, e_s, native
     return e_n, e_s
 
 
@@ -150,6 +164,62 @@ def test_zoo_matches_reference(name, reproducible_convs):
         return m
 
     compare_model(ctor, batch=16)
+
+
+@pytest.fixture
+def static_tiles():
+    """Static conv tile heuristic (no timing-based autotune), non-deterministic mode (the sharded
+    BN accumulators are on)."""
+    from pytorch_cifar_amd import _native
+
+    C = _native.lib()
+    at, det = C.conv_autotune_enabled(), C.deterministic()
+    C.conv_autotune(False)
+    C.set_deterministic(False)
+    yield
+    C.conv_autotune(at)
+    C.set_deterministic(det)
+
+
+@pytest.mark.parametrize("name", ["ResNet18", "ResNet50", "PreActResNet18", "MobileNetV2",
+                                  "EfficientNetB0", "RegNetY_400MF", "densenet_cifar", "DLA"])
+def test_bn_accumulators_match_reference(name, static_tiles):
+    """Steps after the first route every conv->BN statistic and every BN-backward sum through the
+    sharded accumulators (fused finalize in the BN kernels): still as close to fp32 as stock
+    bf16, running stats / num_batches_tracked exact in count, and after the step every forward
+    accumulator is back at zero (cleared by its BN's backward kernel); the backward ones are
+    cleared by the next forward."""
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.ops.functional import StatAcc
+
+    def ctor():
+        m = models.MODEL_REGISTRY[name]()
+        if hasattr(m, "cfg") and isinstance(m.cfg, dict) and "dropout_rate" in m.cfg:
+            m.cfg = dict(m.cfg, dropout_rate=0.0)
+        return m
+
+    _, _, native = compare_model(ctor, batch=16, warm=2, return_models=True)
+    items = [(k, a) for mod in native.modules() for k, a in mod.__dict__.get("_pca_acc", {}).items()]
+    assert items, "no module switched to accumulator statistics"
+    torch.cuda.synchronize()
+    for k, a in items:
+        assert isinstance(a, StatAcc)
+        if k[0] == "fwd":
+            assert a.state == "clean", (k, a.state)
+        if a.state == "clean":
+            assert a.buf.abs().max().item() == 0, f"{k}: accumulator marked clean is not zero"
+    with torch.no_grad():
+        native(torch.randn(16, 3, 32, 32, device="cuda"))
+    torch.cuda.synchronize()
+    for k, a in items:
+        if k[0] == "bwd":
+            assert a.state == "clean" and a.buf.abs().max().item() == 0, k
+    if name == "ResNet18":
+        fwd = [a for k, a in items if k[0] == "fwd"]
+        bwd = [a for k, a in items if k[0] == "bwd"]
+        # 20 BNs: every conv feeds one; the 3 projection-shortcut BNs are folded into their
+        # block's second BN kernel (dual BN), which owns the shared backward accumulator
+        assert len(fwd) >= 19 and len(bwd) >= 17, (len(fwd), len(bwd))
 
 
 def test_batched_weight_prep_matches_per_conv():

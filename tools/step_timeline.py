@@ -10,8 +10,28 @@ a side stream, overlapping kernels show as negative gaps.
   python tools/step_timeline.py gpurun_out/prof/run_kernel_trace.csv [--step -2] [--md]
 """
 import argparse
+import collections
 import csv
 import re
+
+# kernel -> phase of the training step (pytorch_cifar_amd kernel names)
+CATEGORIES = [
+    ("conv fwd", r"conv_igemm_(ph_)?kernel<[^>]*, 0, |conv3x3_c64_kernel<false|splitk_reduce_kernel<true>|dw_fwd|direct_fwd"),
+    ("conv dgrad", r"conv_igemm_(ph_)?kernel<[^>]*, [12], |conv3x3_c64_kernel<true|splitk_reduce_kernel<false>|dw_dgrad|direct_dgrad"),
+    ("conv wgrad", r"wgrad|slab_reduce|dw_w"),
+    ("batchnorm fwd", r"bn_apply|bn_finalize|bn_stats|colsum"),
+    ("batchnorm bwd", r"bn_bwd"),
+    ("optimizer / weight prep", r"sgd_kernel|weight_prep"),
+    ("head (pool, linear, CE)", r"gap_|Cijk|ce_fused|scale_by_scalar|reduce_kernel"),
+    ("data (augment, gather)", r"augment|scatter_gather|copyBuffer"),
+]
+
+
+def category(name):
+    for cat, rx in CATEGORIES:
+        if re.search(rx, name):
+            return cat
+    return "other (fills, elementwise)"
 
 
 def load(path):
@@ -38,6 +58,7 @@ def main():
     ap.add_argument("--marker", default="sgd_kernel")
     ap.add_argument("--step", type=int, default=-2, help="which step window (python index over windows)")
     ap.add_argument("--md", action="store_true")
+    ap.add_argument("--categories", action="store_true", help="print only per-phase totals")
     a = ap.parse_args()
     ks = load(a.path)
     marks = [i for i, k in enumerate(ks) if a.marker in k[2]]
@@ -61,6 +82,15 @@ def main():
     print(f"kernels: {len(step)}; step wall (marker to marker): {wall / 1e3:.1f} us; "
           f"busy (union): {busy / 1e3:.1f} us; summed kernel time: {ksum / 1e3:.1f} us; "
           f"idle: {(wall - busy) / 1e3:.1f} us\n")
+    if a.categories:
+        agg = collections.defaultdict(lambda: [0.0, 0])
+        for s_, e_, n_ in step:
+            agg[category(n_)][0] += (e_ - s_) / 1e3
+            agg[category(n_)][1] += 1
+        print("| phase | us / step | % | kernels |\n|---|---:|---:|---:|")
+        for cat, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+            print(f"| {cat} | {t:.1f} | {100 * t * 1e3 / ksum:.1f} | {c} |")
+        return
     if a.md:
         print("| # | start us | dur us | gap us | kernel |\n|---:|---:|---:|---:|---|")
     prev_e = t0
