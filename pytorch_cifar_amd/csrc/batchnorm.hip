@@ -489,15 +489,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 // ---- row-tiled fast paths (C % 8 == 0, C <= 2048) ----
 // Thread t owns the 8-channel group g = t % TPR for every row it visits, so the per-channel
 // coefficients live in registers for the whole kernel (the generic grid-stride kernels re-load
-// them per vector); consecutive threads still read consecutive 16-byte chunks of NHWC rows, and
-// two rows are in flight per thread.
+// them per vector); consecutive threads still read consecutive 16-byte chunks of NHWC rows.
+// Each iteration handles kRowsInFlight rows per thread: every load of the iteration is issued
+// before any use, from clamped (always valid) row indices, and only the stores are predicated —
+// a conditional load would make the compiler branch around it and drain vmcnt per row, which
+// capped these kernels at ~2.5-2.9 TB/s (layer-1 shapes, bs1024).
 // `scale`/`shift` (and `scale2`/`shift2`) point at [C] coefficient vectors in global memory
 // (aux rows 2 and 3) or in LDS (the fused-finalize kernels below).
+constexpr int kRowsInFlight = 4;
+
 template <bool RES, bool DUAL, int ACT>
 __device__ __forceinline__ void bn_apply_rows_body(
     const bf16* __restrict__ y, const float* scale, const float* shift, int C, int M,
     const bf16* __restrict__ res, const bf16* __restrict__ y2, const float* scale2,
     const float* shift2, bf16* __restrict__ out, uint8_t* __restrict__ mask) {
+  constexpr int U = kRowsInFlight;
   const int TPR = C >> 3, RPB = 256 / TPR;
   const int g = threadIdx.x % TPR, ro = threadIdx.x / TPR;
   if (ro >= RPB) return;
@@ -513,39 +519,36 @@ __device__ __forceinline__ void bn_apply_rows_body(
     }
   }
   const int rstep = gridDim.x * RPB;
-  for (int r = blockIdx.x * RPB + ro; r < M; r += 2 * rstep) {
-    const int r2 = r + rstep;
-    const bool two = r2 < M;
-    const size_t e = (size_t)r * C + c0, e2 = (size_t)r2 * C + c0;
-    float f[8], f2[8], t[8], t2[8];
-    unpack8(*reinterpret_cast<const uint4*>(y + e), f);
-    if (two) unpack8(*reinterpret_cast<const uint4*>(y + e2), f2);
-    if constexpr (RES) {
-      unpack8(*reinterpret_cast<const uint4*>(res + e), t);
-      if (two) unpack8(*reinterpret_cast<const uint4*>(res + e2), t2);
-    }
-    if constexpr (DUAL) {
-      unpack8(*reinterpret_cast<const uint4*>(y2 + e), t);
-      if (two) unpack8(*reinterpret_cast<const uint4*>(y2 + e2), t2);
-    }
-    uint32_t b = 0, b2 = 0;
+  for (int r0 = blockIdx.x * RPB + ro; r0 < M; r0 += U * rstep) {
+    uint4 vy[U], vt[U];
+    size_t e[U];
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      float a = f[v] * sc[v] + sh[v], a2 = f2[v] * sc[v] + sh[v];
-      if constexpr (RES) { a += t[v]; a2 += t2[v]; }
-      if constexpr (DUAL) { a += t[v] * sc2[v] + sh2[v]; a2 += t2[v] * sc2[v] + sh2[v]; }
-      a = apply_act(a, ACT);
-      a2 = apply_act(a2, ACT);
-      b |= (a > 0.f ? 1u : 0u) << v;
-      b2 |= (a2 > 0.f ? 1u : 0u) << v;
-      f[v] = a;
-      f2[v] = a2;
+    for (int u = 0; u < U; ++u) {
+      const int r = min(r0 + u * rstep, M - 1);
+      e[u] = (size_t)r * C + c0;
+      vy[u] = *reinterpret_cast<const uint4*>(y + e[u]);
+      if constexpr (RES) vt[u] = *reinterpret_cast<const uint4*>(res + e[u]);
+      if constexpr (DUAL) vt[u] = *reinterpret_cast<const uint4*>(y2 + e[u]);
     }
-    *reinterpret_cast<uint4*>(out + e) = pack8(f);
-    if (two) *reinterpret_cast<uint4*>(out + e2) = pack8(f2);
-    if (mask) {
-      mask[e >> 3] = (uint8_t)b;
-      if (two) mask[e2 >> 3] = (uint8_t)b2;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float f[8], t[8];
+      unpack8(vy[u], f);
+      if constexpr (RES || DUAL) unpack8(vt[u], t);
+      uint32_t b = 0;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        float a = f[v] * sc[v] + sh[v];
+        if constexpr (RES) a += t[v];
+        if constexpr (DUAL) a += t[v] * sc2[v] + sh2[v];
+        a = apply_act(a, ACT);
+        b |= (a > 0.f ? 1u : 0u) << v;
+        f[v] = a;
+      }
+      if (r0 + u * rstep < M) {
+        *reinterpret_cast<uint4*>(out + e[u]) = pack8(f);
+        if (mask) mask[e[u] >> 3] = (uint8_t)b;
+      }
     }
   }
 }
@@ -568,6 +571,7 @@ __device__ __forceinline__ void bn_bwd_apply_rows_body(
     const float* coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
     const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux) {
   constexpr bool MASK = KIND == 1;
+  constexpr int U = kRowsInFlight;
   const int TPR = C >> 3, RPB = 256 / TPR;
   const int g = threadIdx.x % TPR, ro = threadIdx.x / TPR;
   if (ro >= RPB) return;
@@ -589,53 +593,45 @@ __device__ __forceinline__ void bn_bwd_apply_rows_body(
     }
   }
   const int rstep = gridDim.x * RPB;
-  for (int r = blockIdx.x * RPB + ro; r < M; r += 2 * rstep) {
-    const int r2 = r + rstep;
-    const bool two = r2 < M;
-    const size_t e = (size_t)r * C + c0, e2 = (size_t)r2 * C + c0;
-    float dz[8], dz2[8], yy[8], yy2[8];
-    unpack8(*reinterpret_cast<const uint4*>(dout + e), dz);
-    if (two) unpack8(*reinterpret_cast<const uint4*>(dout + e2), dz2);
-    unpack8(*reinterpret_cast<const uint4*>(y + e), yy);
-    if (two) unpack8(*reinterpret_cast<const uint4*>(y + e2), yy2);
-    if constexpr (MASK) {
-      const uint32_t m = mask[e >> 3];
-      const uint32_t m2 = two ? mask[e2 >> 3] : 0u;
+  for (int r0 = blockIdx.x * RPB + ro; r0 < M; r0 += U * rstep) {
+    uint4 vd[U], vy[U], v2[U];
+    uint32_t vm[U];
+    size_t e[U];
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        dz[v] = ((m >> v) & 1u) ? dz[v] : 0.f;
-        dz2[v] = ((m2 >> v) & 1u) ? dz2[v] : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int r = min(r0 + u * rstep, M - 1);
+      e[u] = (size_t)r * C + c0;
+      vd[u] = *reinterpret_cast<const uint4*>(dout + e[u]);
+      vy[u] = *reinterpret_cast<const uint4*>(y + e[u]);
+      if constexpr (MASK) vm[u] = mask[e[u] >> 3];
+      if constexpr (DUAL) v2[u] = *reinterpret_cast<const uint4*>(y2 + e[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float dz[8], yy[8], o[8];
+      unpack8(vd[u], dz);
+      unpack8(vy[u], yy);
+      if constexpr (MASK) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) dz[v] = ((vm[u] >> v) & 1u) ? dz[v] : 0.f;
       }
-    }
-    if constexpr (KIND == 2) {
+      if constexpr (KIND == 2) {
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        dz[v] *= act_grad(yy[v] * zs[v] + zb[v], ACT_SWISH);
-        dz2[v] *= act_grad(yy2[v] * zs[v] + zb[v], ACT_SWISH);
+        for (int v = 0; v < 8; ++v) dz[v] *= act_grad(yy[v] * zs[v] + zb[v], ACT_SWISH);
       }
-    }
-    float o[8], o2[8];
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      o[v] = ca[v] * dz[v] + cb[v] * yy[v] + cd[v];
-      o2[v] = ca[v] * dz2[v] + cb[v] * yy2[v] + cd[v];
-    }
-    *reinterpret_cast<uint4*>(dy + e) = pack8(o);
-    if (two) *reinterpret_cast<uint4*>(dy + e2) = pack8(o2);
-    if constexpr (RES) {
-      *reinterpret_cast<uint4*>(dres + e) = pack8(dz);
-      if (two) *reinterpret_cast<uint4*>(dres + e2) = pack8(dz2);
-    }
-    if constexpr (DUAL) {
-      unpack8(*reinterpret_cast<const uint4*>(y2 + e), yy);
-      if (two) unpack8(*reinterpret_cast<const uint4*>(y2 + e2), yy2);
-#pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        o[v] = ca2[v] * dz[v] + cb2[v] * yy[v] + cd2[v];
-        o2[v] = ca2[v] * dz2[v] + cb2[v] * yy2[v] + cd2[v];
+      for (int v = 0; v < 8; ++v) o[v] = ca[v] * dz[v] + cb[v] * yy[v] + cd[v];
+      const bool live = r0 + u * rstep < M;
+      if (live) *reinterpret_cast<uint4*>(dy + e[u]) = pack8(o);
+      if constexpr (RES) {
+        if (live) *reinterpret_cast<uint4*>(dres + e[u]) = pack8(dz);
       }
-      *reinterpret_cast<uint4*>(dy2 + e) = pack8(o);
-      if (two) *reinterpret_cast<uint4*>(dy2 + e2) = pack8(o2);
+      if constexpr (DUAL) {
+        unpack8(v2[u], yy);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) o[v] = ca2[v] * dz[v] + cb2[v] * yy[v] + cd2[v];
+        if (live) *reinterpret_cast<uint4*>(dy2 + e[u]) = pack8(o);
+      }
     }
   }
 }
@@ -805,7 +801,7 @@ static bool rows_enabled() {
 
 static int rows_grid(int M, int C) {
   const int RPB = 256 / (C >> 3);
-  int b = cdiv(M, RPB * 2);
+  int b = cdiv(M, RPB * kRowsInFlight);
   return b < 2048 ? (b ? b : 1) : 2048;
 }
 

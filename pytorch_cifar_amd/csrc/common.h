@@ -84,8 +84,8 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // BatchNorm partial sums leave a producer kernel in one of two forms:
 //   shards == 0: slab row `row` of [rows][rowlen] (deterministic; folded by a finalize kernel),
 //   shards  > 0: an fp32 atomic add into accumulator row `row % shards` of [shards][rowlen].
-// The sharded accumulator is zero at rest: the consuming BN kernel folds it while normalizing and
-// its last workgroup (ticket) zeroes it again, so no finalize launch and no memset per step.
+// The consuming BN kernel folds the sharded accumulator while normalizing (no finalize launch);
+// the other pass of the same BN re-zeroes it (batchnorm.hip, "fused finalize + apply").
 __device__ __forceinline__ void stat_out(float* base, int row, int shards, size_t rowlen, int col,
                                          float v) {
   if (shards > 0)
