@@ -95,6 +95,12 @@ void augment_launch(const uint8_t*, const int64_t*, const int32_t*, int, int, in
                     const float*, const float*, bf16*, hipStream_t);
 void gap_fwd_launch(const bf16*, int, int, int, float*, hipStream_t);
 void gap_bwd_launch(const float*, int, int, int, bf16*, hipStream_t);
+bool head_supported(int C, int K);
+bool head_batch_supported(int N, int K);
+void head_fwd_launch(const bf16*, int, int, int, const float*, const float*, int, float*, float*,
+                     hipStream_t);
+void head_bwd_launch(const float*, const float*, const float*, int, int, int, int, bf16*, float*,
+                     float*, hipStream_t);
 void avgpool_fwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, hipStream_t);
 void avgpool_bwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, hipStream_t);
 void maxpool_fwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, uint8_t*,
@@ -816,6 +822,50 @@ Tensor augment(const Tensor& data, const Tensor& idx, const Tensor& rnd, int pad
   return out;
 }
 
+// fused classifier head: x [N,H,W,C] bf16 -> (logits [N,K] fp32, pooled [N,C] fp32)
+std::vector<Tensor> head_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& b) {
+  check_bf16(x, "x");
+  check_f32(w, "weight");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  const int K = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == C, "weight must be [K, C]");
+  TORCH_CHECK(pca::head_supported(C, K) && pca::head_batch_supported(N, K),
+              "fused head needs C % 8 == 0, K <= 16 and N * K <= 12288");
+  if (b.has_value() && b->defined()) {
+    check_f32(*b, "bias");
+    TORCH_CHECK(b->numel() == K, "bias size");
+  }
+  auto fopt = x.options().dtype(at::kFloat);
+  auto logits = at::empty({N, K}, fopt);
+  auto pooled = at::empty({N, C}, fopt);
+  pca::head_fwd_launch(ptr<bf16>(x), N, HW, C, ptr<float>(w), optr<float>(b), K, ptr<float>(pooled),
+                       ptr<float>(logits), cur_stream());
+  return {logits, pooled};
+}
+
+// backward of head_fwd: returns {dx [N,H,W,C] bf16, dw [K,C], db [K]}; dw / db are added into
+// the given accumulators (gradient-arena views) when present, else fresh zero-based tensors
+std::vector<Tensor> head_bwd(const Tensor& dl, const Tensor& w, const Tensor& pooled, int H, int W,
+                             const optional<Tensor>& dw_acc, const optional<Tensor>& db_acc,
+                             bool want_db) {
+  check_f32(dl, "dlogits");
+  check_f32(w, "weight");
+  check_f32(pooled, "pooled");
+  const int N = dl.size(0), K = dl.size(1), C = w.size(1);
+  TORCH_CHECK(pooled.size(0) == N && pooled.size(1) == C && w.size(0) == K, "head shapes");
+  auto fopt = dl.options();
+  auto dx = at::empty({N, H, W, C}, dl.options().dtype(at::kBFloat16));
+  Tensor dw = (dw_acc.has_value() && dw_acc->defined()) ? *dw_acc : at::zeros({K, C}, fopt);
+  Tensor db;
+  if (want_db) db = (db_acc.has_value() && db_acc->defined()) ? *db_acc : at::zeros({K}, fopt);
+  TORCH_CHECK(dw.is_contiguous() && dw.numel() == (int64_t)K * C, "dw accumulator");
+  if (db.defined()) TORCH_CHECK(db.is_contiguous() && db.numel() == K, "db accumulator");
+  pca::head_bwd_launch(ptr<float>(dl), ptr<float>(w), ptr<float>(pooled), N, H * W, C, K,
+                       ptr<bf16>(dx), ptr<float>(dw), db.defined() ? ptr<float>(db) : nullptr,
+                       cur_stream());
+  return {dx, dw, db};
+}
+
 Tensor gap_fwd(const Tensor& x) {
   check_bf16(x, "x");
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
@@ -1203,6 +1253,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nhwc_to_nchw", &nhwc_to_nchw);
   m.def("augment", &augment);
   m.def("gap_fwd", &gap_fwd);
+  m.def("head_fwd", &head_fwd, "fused global-average-pool + Linear -> (logits, pooled)");
+  m.def("head_bwd", &head_bwd, py::arg("dl"), py::arg("w"), py::arg("pooled"), py::arg("H"),
+        py::arg("W"), py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none(),
+        py::arg("want_db") = true);
+  m.def("head_supported", [](int N, int C, int K) {
+    return pca::head_supported(C, K) && pca::head_batch_supported(N, K);
+  });
   m.def("gap_bwd", &gap_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);

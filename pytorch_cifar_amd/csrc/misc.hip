@@ -13,6 +13,8 @@
 //   eltwise     : residual add(+act) for the non-fused paths, act backward
 #include "common.h"
 
+#include <algorithm>
+
 #include <type_traits>
 
 namespace pca {
@@ -906,6 +908,173 @@ void augment_launch(const uint8_t* data, const int64_t* idx, const int32_t* rnd,
                      1.f / std[2], out);
 }
 static bool vec8_ok(int C) { return C % 8 == 0 && C <= 2048; }
+
+// ------------------------------------------------------------------- classifier head
+// Global average pool + Linear, fused (every zoo head: resnet.py:127-130 avg_pool2d(4) -> view ->
+// linear, mobilenetv2.py:74, efficientnet.py:145 ...). The reference runs a pooling kernel, a
+// cuBLAS addmm and, in backward, two GEMMs, a bias reduction, two AccumulateGrad adds and the
+// pooling backward; here the forward is one kernel and the backward one kernel.
+//   forward : block n pools x[n] (8-channel vectors, HW rows split over row lanes, LDS fold) and
+//             computes logits[n][k] = pooled . W[k] + b[k] (one wave per k, wave reduction);
+//             pooled is kept for dW.
+//   backward: blocks 0..N-1 write dx[n][hw][c] = sum_k dl[n][k] W[k][c] / HW; the other blocks
+//             each own 64 weight columns x 64 samples and add their share of
+//             dW[k][c] += sum_n dl[n][k] pooled[n][c] with fp32 atomics (deterministic mode uses the
+//             unfused path); the first of them also adds db[k] += sum_n dl[n][k].
+// Loops over the K classes are unrolled to kHeadMaxK with clamped (always issued) loads and a
+// zero multiplier past K: a load guarded by k < K would make the compiler branch around it and
+// wait for each one in turn (the first version spent 15-27 us on these latency chains).
+constexpr int kHeadMaxK = 16;
+constexpr int kHeadSamples = 64;   // samples per weight-gradient block
+
+__global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ x, int HW, int C,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ b, int K,
+                                                       float* __restrict__ pooled,
+                                                       float* __restrict__ logits) {
+  extern __shared__ float hs[];                  // [RL][C] row-lane partials; [4][K] wave sums
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const int CG = C >> 3;
+  const int RL = CG >= 256 ? 1 : 256 / CG;       // row lanes
+  const bf16* xn = x + (size_t)n * HW * C;
+  for (int g0 = 0; g0 < CG; g0 += 256) {
+    const int g = g0 + tid % (CG >= 256 ? 256 : CG), rl = CG >= 256 ? 0 : tid / CG;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (rl < RL && g < CG) {
+#pragma unroll 4
+      for (int hw = rl; hw < HW; hw += RL) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(xn + (size_t)hw * C + g * 8), f);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) acc[v] += f[v];
+      }
+#pragma unroll
+      for (int v = 0; v < 8; ++v) hs[rl * C + g * 8 + v] = acc[v];
+    }
+  }
+  __syncthreads();
+  // every thread: pooled channels c = tid, tid + 256, ... and the partial dot products of all K
+  // classes over them (K independent weight loads per channel), then one block reduction per k
+  const float inv = 1.f / HW;
+  float part[kHeadMaxK];
+#pragma unroll
+  for (int k = 0; k < kHeadMaxK; ++k) part[k] = 0.f;
+  for (int c = tid; c < C; c += 256) {
+    float t = 0.f;
+    for (int r = 0; r < RL; ++r) t += hs[r * C + c];
+    t *= inv;
+    pooled[(size_t)n * C + c] = t;
+#pragma unroll
+    for (int k = 0; k < kHeadMaxK; ++k) {
+      const float wk = w[(size_t)min(k, K - 1) * C + c];
+      part[k] += (k < K ? t : 0.f) * wk;
+    }
+  }
+  __syncthreads();                               // hs is reused for the wave sums below
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < kHeadMaxK; ++k) {
+    const float t = wave_sum(part[k]);
+    if (lane == 0) hs[wv * kHeadMaxK + k] = t;
+  }
+  __syncthreads();
+  if (tid < K) {
+    const float t = hs[tid] + hs[kHeadMaxK + tid] + hs[2 * kHeadMaxK + tid] + hs[3 * kHeadMaxK + tid];
+    logits[(size_t)n * K + tid] = t + (b ? b[tid] : 0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dl,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ pooled, int N,
+                                                       int HW, int C, int K,
+                                                       bf16* __restrict__ dx,
+                                                       float* __restrict__ dw,
+                                                       float* __restrict__ db) {
+  extern __shared__ float hs[];
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x < N) {
+    const int n = blockIdx.x;
+    const float inv = 1.f / HW;
+    float d[kHeadMaxK];
+#pragma unroll
+    for (int k = 0; k < kHeadMaxK; ++k) {
+      const float v = dl[(size_t)n * K + min(k, K - 1)];
+      d[k] = k < K ? v * inv : 0.f;
+    }
+    for (int c = tid; c < C; c += 256) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < kHeadMaxK; ++k) t += d[k] * w[(size_t)min(k, K - 1) * C + c];
+      hs[c] = t;
+    }
+    __syncthreads();
+    const int CG = C >> 3;
+    bf16* dxn = dx + (size_t)n * HW * C;
+    for (int i = tid; i < HW * CG; i += 256) {
+      const int g = i % CG;
+      *reinterpret_cast<uint4*>(dxn + (size_t)i * 8) = pack8(hs + g * 8);
+    }
+    return;
+  }
+  // weight / bias gradient: block (j, q) = 64 columns x kHeadSamples samples, 4 sample lanes
+  const int jq = blockIdx.x - N;
+  const int ncb = cdiv(C, 64);
+  const int j = jq % ncb, q = jq / ncb;
+  const int cl = tid & 63, nl = tid >> 6;
+  const int c = j * 64 + cl;
+  const int n0 = q * kHeadSamples, n1 = min(N, n0 + kHeadSamples);
+  float* red = hs;                                // [kHeadMaxK][4][64]
+  float acc[kHeadMaxK];
+#pragma unroll
+  for (int k = 0; k < kHeadMaxK; ++k) acc[k] = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int n = n0 + nl; n < n1; n += 4) {
+      const float p = pooled[(size_t)n * C + c];
+#pragma unroll
+      for (int k = 0; k < kHeadMaxK; ++k) acc[k] += dl[(size_t)n * K + min(k, K - 1)] * p;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kHeadMaxK; ++k) red[(k * 4 + nl) * 64 + cl] = acc[k];
+  __syncthreads();
+  if (nl == 0 && c < C) {
+    for (int k = 0; k < K; ++k) {
+      const float t = red[(k * 4 + 0) * 64 + cl] + red[(k * 4 + 1) * 64 + cl] +
+                      red[(k * 4 + 2) * 64 + cl] + red[(k * 4 + 3) * 64 + cl];
+      atomicAdd(dw + (size_t)k * C + c, t);
+    }
+  }
+  if (jq == 0 && db && nl == 1) {       // one wave: db[k] += sum_n dl[n][k]
+    for (int k = 0; k < K; ++k) {
+      float t = 0.f;
+      for (int n = cl; n < N; n += 64) t += dl[(size_t)n * K + k];
+      t = wave_sum(t);
+      if (cl == 0) db[k] += t;
+    }
+  }
+}
+
+bool head_supported(int C, int K) { return C % 8 == 0 && C <= 4096 && K >= 1 && K <= kHeadMaxK; }
+bool head_batch_supported(int N, int K) { return N >= 1 && K >= 1; }
+
+void head_fwd_launch(const bf16* x, int N, int HW, int C, const float* w, const float* b, int K,
+                     float* pooled, float* logits, hipStream_t st) {
+  const int CG = C >> 3;
+  const int RL = CG >= 256 ? 1 : 256 / CG;
+  const size_t lds = std::max<size_t>((size_t)RL * C, 4 * kHeadMaxK) * sizeof(float);
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(N), dim3(256), lds, st, x, HW, C, w, b, K, pooled,
+                     logits);
+}
+
+void head_bwd_launch(const float* dl, const float* w, const float* pooled, int N, int HW, int C,
+                     int K, bf16* dx, float* dw, float* db, hipStream_t st) {
+  const size_t lds = std::max<size_t>((size_t)C, (size_t)kHeadMaxK * 4 * 64) * sizeof(float);
+  const int wblocks = cdiv(C, 64) * cdiv(N, kHeadSamples);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(N + wblocks), dim3(256), lds, st, dl, w, pooled, N,
+                     HW, C, K, dx, dw, db);
+}
 
 void gap_fwd_launch(const bf16* x, int N, int HW, int C, float* y, hipStream_t st) {
   if (vec8_ok(C)) {

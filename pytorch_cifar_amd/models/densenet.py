@@ -65,8 +65,7 @@ class DenseNet(tnn.Module):
         out = self.trans2(self.dense2(out))
         out = self.trans3(self.dense3(out))
         out = self.dense4(out)
-        out = F.avg_pool2d(self.bn(out, act="relu"), 4)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(self.bn(out, act="relu"), 4, self.linear)
 
 
 def DenseNet121():

@@ -57,5 +57,4 @@ class DLA(tnn.Module):
     def forward(self, x):
         out = self.layer2(self.layer1(self.base(x)))
         out = self.layer6(self.layer5(self.layer4(self.layer3(out))))
-        out = F.avg_pool2d(out, 4)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, 4, self.linear)

@@ -58,8 +58,7 @@ class DPN(tnn.Module):
     def forward(self, x):
         out = self.bn1(self.conv1(x), act="relu")
         out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
-        out = F.avg_pool2d(out, 4)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, 4, self.linear)
 
 
 def DPN26():

@@ -43,5 +43,4 @@ class MobileNet(tnn.Module):
 
     def forward(self, x):
         out = self.layers(self.bn1(self.conv1(x), act="relu"))
-        out = F.avg_pool2d(out, 2)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, 2, self.linear)

@@ -66,5 +66,4 @@ class MobileNetV2(tnn.Module):
     def forward(self, x):
         out = self.layers(self.bn1(self.conv1(x), act="relu"))
         out = self.bn2(self.conv2(out), act="relu")
-        out = F.avg_pool2d(out, 4)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, 4, self.linear)

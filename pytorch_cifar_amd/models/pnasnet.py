@@ -96,8 +96,7 @@ class PNASNet(tnn.Module):
         out = self.bn1(self.conv1(x), act="relu")
         for m in (self.layer1, self.layer2, self.layer3, self.layer4, self.layer5):
             out = m(out)
-        out = F.avg_pool2d(out, 8)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, 8, self.linear)
 
 
 def PNASNetA():

@@ -73,8 +73,7 @@ class PreActResNet(tnn.Module):
     def forward(self, x):
         out = self.conv1(x)
         out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
-        out = F.avg_pool2d(out, 4)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, 4, self.linear)
 
 
 def PreActResNet18():

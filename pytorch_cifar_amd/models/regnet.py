@@ -75,8 +75,7 @@ class RegNet(tnn.Module):
     def forward(self, x):
         out = self.bn1(self.conv1(x), act="relu")
         out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
-        out = F.adaptive_avg_pool2d(out, (1, 1))
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, None, self.linear)
 
 
 def RegNetX_200MF():

@@ -85,9 +85,7 @@ class ResNet(tnn.Module):
         out = self.layer2(out)
         out = self.layer3(out)
         out = self.layer4(out)
-        out = F.avg_pool2d(out, 4)
-        out = out.view(out.size(0), -1)
-        return self.linear(out)
+        return F.pool_linear(out, 4, self.linear)
 
 
 def ResNet18(amp=False):

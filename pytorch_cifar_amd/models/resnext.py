@@ -58,8 +58,7 @@ class ResNeXt(tnn.Module):
     def forward(self, x):
         out = self.bn1(self.conv1(x), act="relu")
         out = self.layer3(self.layer2(self.layer1(out)))
-        out = F.avg_pool2d(out, 8)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, 8, self.linear)
 
 
 def ResNeXt29_2x64d():

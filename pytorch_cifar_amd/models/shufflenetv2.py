@@ -106,8 +106,7 @@ class ShuffleNetV2(tnn.Module):
         out = self.bn1(self.conv1(x), act="relu")
         out = self.layer3(self.layer2(self.layer1(out)))
         out = self.bn2(self.conv2(out), act="relu")
-        out = F.avg_pool2d(out, 4)
-        return self.linear(out.reshape(out.size(0), -1))
+        return F.pool_linear(out, 4, self.linear)
 
 
 configs = {

@@ -17,6 +17,7 @@ from ..ops.functional import (  # noqa: F401
     dropout,
     global_avg_pool,
     max_pool2d,
+    pool_linear,
     relu,
     se_excite,
     split_channels,

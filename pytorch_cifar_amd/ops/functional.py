@@ -1054,6 +1054,63 @@ def global_avg_pool(x):
     return _GAP.apply(to_nhwc(x)).view(x.shape[0], x.shape[1], 1, 1)
 
 
+class _PoolLinear(torch.autograd.Function):
+    """Global average pool + Linear in one kernel each way (csrc/misc.hip head_*_kernel)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        logits, pooled = _C().head_fwd(x, weight, bias)
+        ctx.save_for_backward(weight, pooled)
+        ctx.hw = (x.shape[1], x.shape[2])
+        ctx.params = (weight, bias)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dl):
+        weight, pooled = ctx.saved_tensors
+        w, b = ctx.params
+        ctx.params = None
+        wbuf = G.grad_buffer(w) if (w.requires_grad and w.is_leaf) else None
+        bbuf = G.grad_buffer(b) if (b is not None and b.requires_grad and b.is_leaf) else None
+        dx, dw, db = _C().head_bwd(dl.float().contiguous(), weight, pooled, ctx.hw[0], ctx.hw[1],
+                                   wbuf, bbuf, b is not None)
+        dw_ret = db_ret = None
+        if w.requires_grad:
+            if wbuf is not None:
+                G.fire(w)
+            elif w.is_leaf:
+                G.accumulate(w, dw)
+            else:
+                dw_ret = dw
+        if b is not None and b.requires_grad:
+            if bbuf is not None:
+                G.fire(b)
+            elif b.is_leaf:
+                G.accumulate(b, db)
+            else:
+                db_ret = db
+        return dx, dw_ret, db_ret
+
+
+def pool_linear(x, kernel_size, linear):
+    """``linear(avg_pool2d(x, kernel_size).flatten(1))`` — the classifier head of the zoo.
+
+    ``kernel_size=None`` means a global (adaptive 1x1) pool. When the pool is global and the
+    shapes allow (C % 8 == 0, <= 16 classes, fp32 weights), the pool and the Linear run as one
+    fused kernel forward and one backward (its weight gradient is added with fp32 atomics);
+    otherwise (CPU reference path, non-global pools, deterministic mode) it is exactly the
+    unfused composition.
+    """
+    N, C, H, W = x.shape
+    glob = kernel_size is None or (_pair1(kernel_size) == H == W)
+    w, b = linear.weight, linear.bias
+    if (_ref(x) or not glob or w.dtype != torch.float32 or torch.is_autocast_enabled()
+            or not _C().head_supported(N, C, w.shape[0]) or _C().deterministic()):
+        out = adaptive_avg_pool2d(x, 1) if kernel_size is None else avg_pool2d(x, kernel_size)
+        return linear(out.reshape(N, -1))
+    return _PoolLinear.apply(to_nhwc(x), w, b)
+
+
 class _AvgPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, s, p):

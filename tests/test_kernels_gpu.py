@@ -433,3 +433,33 @@ def test_debug_sync_proxy_runs_ops():
         assert y.shape[-1] == 16 and C.last_error() == ""
     finally:
         _native.set_debug_sync(False)
+
+
+@pytest.mark.parametrize("N,H,C,K", [(128, 4, 512, 10), (7, 2, 1280, 10), (33, 8, 96, 16),
+                                     (16, 1, 2048, 10), (5, 4, 4096, 3)])
+def test_fused_head_matches_fp32(N, H, C, K, C_=None):
+    """Fused global-average-pool + Linear (forward and backward, gradients accumulated into the
+    given buffers) against the fp32 torch composition."""
+    from pytorch_cifar_amd import _native
+
+    C_ = _native.lib()
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
+    w = torch.randn(K, C, device="cuda") * 0.05
+    b = torch.randn(K, device="cuda")
+    logits, pooled = C_.head_fwd(x, w, b)
+    xr = x.float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = torch.nn.functional.linear(xr.mean((1, 2)), wr, br)
+    assert rel_err(logits, ref) < 1e-4
+    assert rel_err(pooled, xr.detach().mean((1, 2))) < 1e-5
+    dl = torch.randn(N, K, device="cuda")
+    ref.backward(dl)
+    dw0 = torch.randn(K, C, device="cuda")
+    db0 = torch.randn(K, device="cuda")
+    dwa, dba = dw0.clone(), db0.clone()
+    dx, dw, db = C_.head_bwd(dl, w, pooled, H, H, dwa, dba, True)
+    assert dw.data_ptr() == dwa.data_ptr() and db.data_ptr() == dba.data_ptr()
+    assert rel_err(dx, xr.grad) < 1e-2
+    assert rel_err(dw - dw0, wr.grad) < 1e-4
+    assert rel_err(db - db0, br.grad) < 1e-5
