@@ -68,27 +68,41 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
   }
 }
 
-// Compile-time stage geometry for a square W x W image (W | 32): a stage is 32 output pixels =
+// Compile-time stage geometry for a square W x W image (W | KP): a stage is KP output pixels =
 // RS rows of IMGS images; the halo is IMGS x (RS+2) x W2P rows (row pitch W2P = W+2 rounded up to
-// a multiple of 8 so that a kh*W2P row shift only flips bit 3 of the XOR swizzle key).
-template <int W>
+// a multiple of 8 so that a kh*W2P row shift only flips bit 3 of the XOR swizzle key). A stage
+// is KP / 32 MFMA K-steps deep: KP = 64 / 128 amortise the per-stage barrier, counted wait and
+// DMA issue over 2 / 4 steps (KP = 32 left one 16x16x32 MFMA row per wave between barriers, the
+// reason the bs128 shapes ran at 15 % of a CU's matrix rate).
+template <int W, int KP = 32>
 struct HaloShape {
-  static constexpr int RS = (32 / W) <= W ? 32 / W : W;
-  static constexpr int IMGS = (32 / W) <= W ? 1 : (32 / W) / W;
+  static constexpr int RS = (KP / W) <= W ? KP / W : W;
+  static constexpr int IMGS = (KP / W) <= W ? 1 : (KP / W) / W;
   static constexpr int W2P = ((W + 2) + 7) / 8 * 8;
   static constexpr int HR = IMGS * (RS + 2) * W2P;
   static constexpr int HI = (HR + 7) / 8;        // halo DMA instructions per stage
   static constexpr int HBYTES = HI * 1024;
+  static_assert(IMGS * RS * W == KP, "a stage must be whole rows / whole images");
 };
 
-template <int W, int MB, int WM, int WN>
+template <int W, int MB, int KP>
+constexpr int halo_stage_bytes() {
+  return HaloShape<W, KP>::HBYTES + MB * KP * 128 + 1024;
+}
+template <int W, int MB, int KP>
+constexpr bool halo_fits() {
+  return 3 * halo_stage_bytes<W, MB, KP>() <= 160 * 1024;
+}
+
+template <int W, int MB, int WM, int WN, int KP>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wgrad_halo_kernel(const bf16* __restrict__ X,
                                                                   const bf16* __restrict__ DY,
                                                                   float* __restrict__ out,
                                                                   const HaloGeom g) {
-  using SH = HaloShape<W>;
+  using SH = HaloShape<W, KP>;
   constexpr int NW = WM * WN;
-  constexpr int KP = 32;
+  constexpr int KS = KP / 32;                    // MFMA K-steps per stage
+  constexpr int DYI = KP / 8;                    // DMA instructions per 64-channel dY block
   constexpr int STAGES = 3;
   constexpr int A_OFF = SH::HBYTES;              // dY blocks follow the halo image
   constexpr int J_OFF = A_OFF + MB * KP * 128;   // junk KiB for the padding DMA slots
@@ -96,7 +110,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   constexpr int BM = MB * 64, BN = 9 * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int T = SH::HI + 4 * MB;             // real DMA instructions per stage
+  constexpr int T = SH::HI + DYI * MB;           // real DMA instructions per stage
   constexpr int SLOTS = (T + NW - 1) / NW;       // every wave issues exactly SLOTS per stage
   constexpr int W2P = SH::W2P;
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
@@ -134,9 +148,9 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
       s_b[j] = (((lane & 7) ^ tr_swz<128>(hr)) << 4) + (grp * g.cin_g + cib * 64) * 2;
     } else if (t < T) {
       const int q = t - SH::HI;
-      const int r = 8 * (q & 3) + row8;
+      const int r = 8 * (q % DYI) + row8;
       s_a[j] = r;
-      s_b[j] = (((lane & 7) ^ tr_swz<128>(r)) << 4) + (grp * g.cout_g + m0 + 64 * (q >> 2)) * 2;
+      s_b[j] = (((lane & 7) ^ tr_swz<128>(r)) << 4) + (grp * g.cout_g + m0 + 64 * (q / DYI)) * 2;
     } else {
       s_a[j] = 0;
       s_b[j] = 0;
@@ -166,7 +180,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
         const int q = t - SH::HI;
         const int p = pbase + s_a[j];
         if (live && p < p_end) off = (uint32_t)(p * g.Cy * 2 + s_b[j]);
-        dma16(rsD, S + A_OFF + (q >> 2) * KP * 128 + (q & 3) * 1024, off);
+        dma16(rsD, S + A_OFF + (q / DYI) * KP * 128 + (q % DYI) * 1024, off);
       } else {
         dma16(rsD, S + J_OFF, kOOB);              // keeps vmcnt per wave uniform
       }
@@ -176,21 +190,24 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   // ---- per-lane B-fragment addressing: halo rows of this lane's two pixel rows ----
   // B frag (tap kh,kw; columns c0..c0+15 of the 64-channel block) for the lane lives at
   //   row R = prow + kh*W2P + kw,  byte = R*128 + ((c0/8 ^ swz(R)) << 4) + L
-  // and swz(R) = swz(prow + kw) ^ (kh*W2P/8 odd ? 4 : 0) because W2P % 8 == 0.
-  int rbase[2], swk[2][3];
+  // and swz(R) = swz(prow + kw) ^ (kh*W2P/8 odd ? 4 : 0) because W2P % 8 == 0. K-step ks of a
+  // stage covers the stage pixels 32*ks .. 32*ks + 31.
+  int rbase[KS][2], swk[KS][2][3];
   {
     const int q = (lane & 15) >> 2, pq = lane & 3;
     const int L = ((pq >> 1) << 4) + ((pq & 1) << 3);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int r = 8 * (lane >> 4) + q + 4 * h;
-      const int img = r / (SH::RS * W), rr = r - img * (SH::RS * W);
-      const int jj = rr / W, ow = rr - jj * W;
-      const int prow = img * (SH::RS + 2) * W2P + jj * W2P + ow;
-      rbase[h] = prow * 128 + L;
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) swk[h][kw] = tr_swz<128>(prow + kw) << 4;
-    }
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * ks + 8 * (lane >> 4) + q + 4 * h;
+        const int img = r / (SH::RS * W), rr = r - img * (SH::RS * W);
+        const int jj = rr / W, ow = rr - jj * W;
+        const int prow = img * (SH::RS + 2) * W2P + jj * W2P + ow;
+        rbase[ks][h] = prow * 128 + L;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) swk[ks][h][kw] = tr_swz<128>(prow + kw) << 4;
+      }
   }
 
   f32x4 acc[TM][TN];
@@ -210,30 +227,33 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
     issue(p_begin + (kt + 2) * KP, (kt + 2) % STAGES);
     if (g.ablate & 2) continue;
     const char* S = smem + (kt % STAGES) * STAGE;
-    bf16x8 af[TM];
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi) {
-      const int m = wm * WTM + mi * 16;
-      af[mi] = tr_frag<64>(S + A_OFF + (m >> 6) * KP * 128, 0, m & 63, lane);
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 af[TM];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        const int m = wm * WTM + mi * 16;
+        af[mi] = tr_frag<64>(S + A_OFF + (m >> 6) * KP * 128, 32 * ks, m & 63, lane);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int n = wn * WTN + ni * 16;
+        const int tap = n >> 6, kh = tap / 3, kw = tap % 3;
+        const int c0 = n & 63;
+        const int cx = ((c0 >> 3) ^ (((kh * W2P / 8) & 1) ? 4 : 0)) << 4;
+        const int rsh = (kh * W2P + kw) * 128;
+        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_i16x4*)(S + rbase[ks][0] + rsh + (cx ^ swk[ks][0][kw])));
+        const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_i16x4*)(S + rbase[ks][1] + rsh + (cx ^ swk[ks][1][kw])));
+        const bf16x8 bfv = __builtin_bit_cast(bf16x8, (i16x8)__builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfv, acc[mi][ni], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
     }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni) {
-      const int n = wn * WTN + ni * 16;
-      const int tap = n >> 6, kh = tap / 3, kw = tap % 3;
-      const int c0 = n & 63;
-      const int cx = ((c0 >> 3) ^ (((kh * W2P / 8) & 1) ? 4 : 0)) << 4;
-      const int rsh = (kh * W2P + kw) * 128;
-      const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (lds_i16x4*)(S + rbase[0] + rsh + (cx ^ swk[0][kw])));
-      const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (lds_i16x4*)(S + rbase[1] + rsh + (cx ^ swk[1][kw])));
-      const bf16x8 bfv = __builtin_bit_cast(bf16x8, (i16x8)__builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi)
-        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfv, acc[mi][ni], 0, 0, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
   }
   wait_vmcnt<0>();
 
@@ -303,17 +323,22 @@ static int halo_cus() {
   return n;
 }
 
-// X(cfg, MB, WM, WN)
+// X(cfg, MB, WM, WN, KP)
 #define PCA_HALO_CFGS(X) \
-  X(0, 1, 1, 4)          \
-  X(1, 2, 2, 4)          \
-  X(2, 1, 2, 4)
+  X(0, 1, 1, 4, 32)      \
+  X(1, 2, 2, 4, 32)      \
+  X(2, 1, 2, 4, 32)      \
+  X(3, 1, 2, 4, 64)      \
+  X(4, 2, 2, 4, 64)      \
+  X(5, 1, 2, 4, 128)     \
+  X(6, 1, 1, 4, 64)
+constexpr int kHaloCfgs = 7;
 
-template <int W, int MB, int WM, int WN>
+template <int W, int MB, int WM, int WN, int KP>
 static int halo_occupancy() {
   static int occ = 0;
   if (occ == 0) {
-occ = blocks_per_cu((const void*)wgrad_halo_kernel<W, MB, WM, WN>, WM * WN * 64, "wgrad_halo");
+occ = blocks_per_cu((const void*)wgrad_halo_kernel<W, MB, WM, WN, KP>, WM * WN * 64, "wgrad_halo");
   }
   return occ;
 }
@@ -370,16 +395,16 @@ static int halo_select(const HaloGeom& g) {
   return g.cout_g <= 64 ? 0 : 1;
 }
 
-template <int W, int MB, int WM, int WN>
+template <int W, int MB, int WM, int WN, int KP>
 static int64_t halo_plan(HaloGeom& g) {
   const int tiles = cdiv(g.cout_g, 64 * MB) * (g.cin_g / 64) * g.groups;
-  const int slots = halo_occupancy<W, MB, WM, WN>() * halo_cus();
+  const int slots = halo_occupancy<W, MB, WM, WN, KP>() * halo_cus();
   int splits = std::max(1, slots / tiles);
   splits = std::min(splits, std::max(1, cdiv(g.P, 256)));
   const int forced = wgrad_split_force();
   if (forced >= 1) splits = std::min(forced, std::max(1, cdiv(g.P, 32)));
   if (forced <= -2) splits = std::min(-forced, std::max(1, cdiv(g.P, 32)));   // slab, fixed count
-  int chunk = cdiv(cdiv(g.P, splits), 32) * 32;
+  int chunk = cdiv(cdiv(g.P, splits), KP) * KP;
   splits = cdiv(g.P, chunk);
   g.chunk = chunk;
   g.splits = splits;
@@ -387,19 +412,20 @@ static int64_t halo_plan(HaloGeom& g) {
               (!g_deterministic && forced == -1 && splits <= 4)) ? 1 : 0;
   static const bool verbose = getenv("PCA_CONV_VERBOSE") != nullptr;
   if (verbose)
-    fprintf(stderr, "[pca] halo wgrad W=%d MB=%d waves=%d: occ=%d cus=%d tiles=%d splits=%d chunk=%d atomic=%d\n",
-            W, MB, WM * WN, halo_occupancy<W, MB, WM, WN>(), halo_cus(), tiles, splits, chunk, g.atomic);
+    fprintf(stderr, "[pca] halo wgrad W=%d MB=%d waves=%d KP=%d: occ=%d cus=%d tiles=%d splits=%d chunk=%d atomic=%d\n",
+            W, MB, WM * WN, KP, halo_occupancy<W, MB, WM, WN, KP>(), halo_cus(), tiles, splits, chunk,
+            g.atomic);
   if (g.atomic) return 0;
   return slab_ws_floats(splits, (int64_t)g.groups * g.cout_g * g.Ktot);
 }
 
-template <int W, int MB, int WM, int WN>
+template <int W, int MB, int WM, int WN, int KP>
 static void launch_halo(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom g,
                         hipStream_t st) {
-  halo_plan<W, MB, WM, WN>(g);
+  halo_plan<W, MB, WM, WN, KP>(g);
   dim3 grid(cdiv(g.cout_g, 64 * MB), g.cin_g / 64, g.splits * g.groups);
-  hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN>), grid, dim3(WM * WN * 64), 0, st, x, dy,
-                     g.atomic ? dw : ws, g);
+  hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP>), grid, dim3(WM * WN * 64), 0, st, x,
+                     dy, g.atomic ? dw : ws, g);
   if (!g.atomic) slab_reduce_launch(ws, dw, g.splits, (int64_t)g.groups * g.cout_g * g.Ktot, st);
 }
 
@@ -408,18 +434,23 @@ template <int W>
 static int64_t halo_dispatch_w(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom& g,
                                hipStream_t st, bool plan_only) {
   switch (halo_select(g)) {
-#define PCA_CASE(C, MB, WM, WN)                                        \
+#define PCA_CASE(C, MB, WM, WN, KP)                                    \
     case C:                                                            \
-      if (plan_only) return halo_plan<W, MB, WM, WN>(g);               \
-      launch_halo<W, MB, WM, WN>(x, dy, dw, ws, g, st);                \
-      return 0;
+      if constexpr (halo_fits<W, MB, KP>()) {                          \
+        if (plan_only) return halo_plan<W, MB, WM, WN, KP>(g);         \
+        launch_halo<W, MB, WM, WN, KP>(x, dy, dw, ws, g, st);          \
+        return 0;                                                      \
+      }                                                                \
+      break;
     PCA_HALO_CFGS(PCA_CASE)
 #undef PCA_CASE
     default:
-      if (plan_only) return halo_plan<W, 1, 1, 4>(g);
-      launch_halo<W, 1, 1, 4>(x, dy, dw, ws, g, st);
-      return 0;
+      break;
   }
+  // (a configuration whose LDS stages do not fit this image width falls back to cfg 0)
+  if (plan_only) return halo_plan<W, 1, 1, 4, 32>(g);
+  launch_halo<W, 1, 1, 4, 32>(x, dy, dw, ws, g, st);
+  return 0;
 }
 
 static int64_t halo_dispatch(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom& g,

@@ -2061,7 +2061,7 @@ std::vector<std::pair<int, int>> wgrad_tune_candidates(int N, int H, int W, int 
                                                        int groups) {
   std::vector<int> cfgs;
   const bool halo = wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) >= 0;
-  if (halo) cfgs.insert(cfgs.end(), {32, 33, 34});
+  if (halo) cfgs.insert(cfgs.end(), {32, 33, 34, 35, 36, 37, 38});
   const int cin_g = Cin / groups, cout_g = Cout / groups;
   if (cin_g % 64 == 0 && cout_g % 64 == 0) cfgs.insert(cfgs.end(), {16, 17, 18, 19, 20, 21});
   cfgs.insert(cfgs.end(), {0, 1, 2, 3, 6, 7});
