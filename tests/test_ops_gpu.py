@@ -146,6 +146,7 @@ def reproducible_convs():
     C = _native.lib()
     at, det = C.conv_autotune_enabled(), C.deterministic()
     C.conv_autotune(False)
+    C.conv_clear_tuned()         # choices tuned by earlier tests would override the heuristic
     C.set_deterministic(True)
     yield
     C.conv_autotune(at)
