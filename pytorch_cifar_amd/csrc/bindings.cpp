@@ -96,6 +96,14 @@ void augment_launch(const uint8_t*, const int64_t*, const int32_t*, int, int, in
 void gap_fwd_launch(const bf16*, int, int, int, float*, hipStream_t);
 void gap_bwd_launch(const float*, int, int, int, bf16*, hipStream_t);
 bool head_supported(int C, int K);
+bool se_mlp_supported(int C, int R);
+void se_mlp_fwd_launch(const float*, int, int, int, const float*, const float*, const float*,
+                       const float*, int, float*, float*, hipStream_t);
+void se_mlp_bwd_launch(const float*, const float*, const float*, int, int, int, const float*,
+                       const float*, int, float*, float*, float*, float*, float*, float*,
+                       hipStream_t);
+void se_ds_launch(const bf16*, const bf16*, const float*, int, int, int, float*, hipStream_t);
+void se_dx_launch(const bf16*, const float*, const float*, int, int, int, bf16*, hipStream_t);
 bool head_batch_supported(int N, int K);
 void head_fwd_launch(const bf16*, int, int, int, const float*, const float*, int, float*, float*,
                      hipStream_t);
@@ -481,6 +489,38 @@ Tensor bn_stats(const Tensor& x) {
   return partial;
 }
 
+// Reduce-kernel grid when it adds into an R-row sharded accumulator: at most kAccDepth
+// workgroups per shard row, so the same-address fp32 atomics stay shallow (deeper queues — 1024
+// blocks into 16 rows — cost more than the finalize launch they remove).
+constexpr int kAccDepth = 16;
+static int acc_reduce_blocks(int M, int C, int R) {
+  return std::max(1, std::min(pca::bn_row_blocks(M, C), kAccDepth * R));
+}
+// tensors up to this size use the accumulator form for a separate statistics / backward-reduce
+// pass (small per-GPU batches: EfficientNet-B0 at bs128), larger ones keep slab rows + finalize
+// largest tensor (elements) whose statistics / backward sums a separate pass adds into an
+// accumulator (PCA_BN_ACC_MAX_ELEMS; larger ones take the slab + finalize path)
+static int64_t acc_max_elems() {
+  static const int64_t v = [] {
+    const char* e = getenv("PCA_BN_ACC_MAX_ELEMS");
+    return e ? (int64_t)atoll(e) : (int64_t)0;   // measured: the slab path is faster
+  }();
+  return v;
+}
+
+// per-channel (sum, sumsq) of a bare tensor added into a zeroed sharded accumulator [R][2][C];
+// returns false (nothing launched) when the tensor is too large for the accumulator form
+bool bn_stats_acc(const Tensor& x, const Tensor& acc, int R) {
+  check_bf16(x, "x");
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  check_acc(acc, R, 2, C);
+  if ((int64_t)M * C > acc_max_elems()) return false;
+  ShardScope shards(R);
+  pca::bn_stats_launch(ptr<bf16>(x), M, C, ptr<float>(acc), acc_reduce_blocks(M, C, R), cur_stream());
+  return true;
+}
+
 // conv bias gradient: per-channel sum of dY [.., C] (bf16), added into `accum` (fp32 [C], e.g.
 // the bias's gradient-arena view) when given, else returned as a new tensor
 Tensor bias_grad(const Tensor& dy, const optional<Tensor>& accum) {
@@ -668,11 +708,20 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
     float* zp1 = z1 ? ptr<float>(*zero1) : nullptr;
     float* zp2 = z2 ? ptr<float>(*zero2) : nullptr;
     const int zn1 = z1 ? (int)zero1->numel() : 0, zn2 = z2 ? (int)zero2->numel() : 0;
+    if (!acc_filled && (int64_t)M * C <= acc_max_elems()) {
+      // no dgrad epilogue delivered the sums: a separate reduce pass over dout, adding into the
+      // accumulator from a grid of at most kAccDepth blocks per shard row
+      ShardScope shards(acc_rows);
+      pca::bn_bwd_reduce_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
+                                optr<bf16>(y2), optr<float>(aux2), act, M, C, ptr<float>(acc),
+                                acc_reduce_blocks(M, C, acc_rows), st);
+      acc_filled = true;
+    }
     if (!acc_filled) {
-      // no dgrad epilogue delivered the sums: a separate reduce pass over dout. Its ~1024
-      // blocks would serialise on the accumulator's few shard rows (same-address atomics), so
-      // this case keeps ordered slab rows + the finalize kernel (whose block 0 clears the
-      // forward accumulators) and the accumulator stays untouched.
+      // large tensor, no dgrad epilogue delivered the sums: its ~1024 reduce blocks would
+      // serialise on the accumulator's few shard rows (same-address atomics), so this case keeps
+      // ordered slab rows + the finalize kernel (whose block 0 clears the forward accumulators)
+      // and the accumulator stays untouched.
       const int P = pca::bn_row_blocks(M, C);
       auto partial = at::empty({P, NS, C}, fopt);
       pca::bn_bwd_reduce_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
@@ -864,6 +913,82 @@ std::vector<Tensor> head_bwd(const Tensor& dl, const Tensor& w, const Tensor& po
                        ptr<bf16>(dx), ptr<float>(dw), db.defined() ? ptr<float>(db) : nullptr,
                        cur_stream());
   return {dx, dw, db};
+}
+
+// whole squeeze-excite block on NHWC x [N,H,W,C]: pool -> s = W2 act(W1 p + b1) + b2 ->
+// out = x * sigmoid(s). w1 [R, C(,1,1)], w2 [C, R(,1,1)] fp32. Returns {out, pooled, hpre, s}.
+static void check_se(const Tensor& x, const Tensor& w1, const Tensor& w2, int& R) {
+  const int C = x.size(3);
+  R = w1.size(0);
+  check_f32(w1, "w1");
+  check_f32(w2, "w2");
+  TORCH_CHECK(w1.is_contiguous() && w2.is_contiguous() && w1.numel() == (int64_t)R * C &&
+                  w2.numel() == (int64_t)R * C && w2.size(0) == C,
+              "squeeze-excite weights must be [R, C] and [C, R]");
+  TORCH_CHECK(pca::se_mlp_supported(C, R), "squeeze-excite MLP: C % 8 == 0, C <= 2048, R <= 192");
+}
+
+std::vector<Tensor> se_forward(const Tensor& x, const Tensor& w1, const optional<Tensor>& b1,
+                               const Tensor& w2, const optional<Tensor>& b2, int act) {
+  check_bf16(x, "x");
+  int R;
+  check_se(x, w1, w2, R);
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  TORCH_CHECK(act == 1 || act == 2, "squeeze-excite act: relu (1) / swish (2)");
+  if (b1.has_value() && b1->defined()) TORCH_CHECK(b1->numel() == R, "b1");
+  if (b2.has_value() && b2->defined()) TORCH_CHECK(b2->numel() == C, "b2");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto pooled = at::empty({N, C}, fopt);
+  auto hpre = at::empty({N, R}, fopt);
+  auto s = at::empty({N, C}, fopt);
+  auto out = at::empty_like(x);
+  auto st = cur_stream();
+  pca::gap_fwd_launch(ptr<bf16>(x), N, HW, C, ptr<float>(pooled), st);
+  pca::se_mlp_fwd_launch(ptr<float>(pooled), N, C, R, ptr<float>(w1), optr<float>(b1),
+                         ptr<float>(w2), optr<float>(b2), act, ptr<float>(hpre), ptr<float>(s), st);
+  pca::se_scale_fwd_launch(ptr<bf16>(x), ptr<float>(s), N, HW, C, ptr<bf16>(out), st);
+  return {out, pooled, hpre, s};
+}
+
+// backward of se_forward: returns {dx, dw1, db1, dw2, db2}; parameter gradients are added into
+// the given accumulators (gradient-arena views) when present, else into fresh zero tensors
+// (db* undefined when want_b* is false)
+std::vector<Tensor> se_backward(const Tensor& dout, const Tensor& x, const Tensor& pooled,
+                                const Tensor& hpre, const Tensor& s, const Tensor& w1,
+                                const Tensor& w2, int act, const optional<Tensor>& dw1_acc,
+                                const optional<Tensor>& db1_acc, const optional<Tensor>& dw2_acc,
+                                const optional<Tensor>& db2_acc, bool want_b1, bool want_b2) {
+  check_bf16(dout, "dout");
+  check_bf16(x, "x");
+  int R;
+  check_se(x, w1, w2, R);
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  TORCH_CHECK(dout.sizes() == x.sizes(), "dout shape");
+  TORCH_CHECK(pooled.numel() == (int64_t)N * C && s.numel() == (int64_t)N * C &&
+                  hpre.numel() == (int64_t)N * R,
+              "saved squeeze-excite tensors");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto pick = [&](const optional<Tensor>& a, int64_t n, bool want) {
+    if (!want) return Tensor();
+    Tensor t = (a.has_value() && a->defined()) ? *a : at::zeros({n}, fopt);
+    TORCH_CHECK(t.is_contiguous() && t.numel() == n && t.scalar_type() == at::kFloat,
+                "squeeze-excite gradient accumulator");
+    return t;
+  };
+  Tensor dw1 = pick(dw1_acc, (int64_t)R * C, true), dw2 = pick(dw2_acc, (int64_t)R * C, true);
+  Tensor db1 = pick(db1_acc, R, want_b1), db2 = pick(db2_acc, C, want_b2);
+  auto ds = at::empty({N, C}, fopt);
+  auto dp = at::empty({N, C}, fopt);
+  auto dz = at::empty({N, R}, fopt);
+  auto dx = at::empty_like(x);
+  auto st = cur_stream();
+  pca::se_ds_launch(ptr<bf16>(dout), ptr<bf16>(x), ptr<float>(s), N, HW, C, ptr<float>(ds), st);
+  pca::se_mlp_bwd_launch(ptr<float>(ds), ptr<float>(hpre), ptr<float>(pooled), N, C, R,
+                         ptr<float>(w1), ptr<float>(w2), act, ptr<float>(dz), ptr<float>(dp),
+                         ptr<float>(dw1), db1.defined() ? ptr<float>(db1) : nullptr,
+                         ptr<float>(dw2), db2.defined() ? ptr<float>(db2) : nullptr, st);
+  pca::se_dx_launch(ptr<bf16>(dout), ptr<float>(s), ptr<float>(dp), N, HW, C, ptr<bf16>(dx), st);
+  return {dx, dw1, db1, dw2, db2};
 }
 
 Tensor gap_fwd(const Tensor& x) {
@@ -1232,6 +1357,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weight_prep", &weight_prep);
   m.def("weight_prep_multi", &weight_prep_multi);
   m.def("bn_stats", &bn_stats);
+  m.def("bn_acc_max_elems", &acc_max_elems,
+        "largest tensor whose BN sums a separate pass adds into an accumulator");
+  m.def("bn_stats_acc", &bn_stats_acc, "BN sums of a bare tensor into a sharded accumulator");
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("accum") = py::none());
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply);
@@ -1253,6 +1381,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nhwc_to_nchw", &nhwc_to_nchw);
   m.def("augment", &augment);
   m.def("gap_fwd", &gap_fwd);
+  m.def("se_supported", &pca::se_mlp_supported, "fused squeeze-excite path for (C, R)?");
+  m.def("se_forward", &se_forward, "squeeze-excite: pool + MLP + sigmoid scale (NHWC bf16)");
+  m.def("se_backward", &se_backward);
   m.def("head_fwd", &head_fwd, "fused global-average-pool + Linear -> (logits, pooled)");
   m.def("head_bwd", &head_bwd, py::arg("dl"), py::arg("w"), py::arg("pooled"), py::arg("H"),
         py::arg("W"), py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none(),

@@ -742,7 +742,9 @@ __global__ __launch_bounds__(256) void se_scale_fwd8_kernel(const bf16* __restri
   }
 }
 
-// dx = dout * sig(s); ds[n,c] = sum_hw dout*x * sig'(s); one block per image
+// dx = dout * sig(s); ds[n,c] = sum_hw dout*x * sig'(s); one block per image (DX = false: ds
+// only, dx is written later by se_dx8_kernel together with the squeeze path's gradient)
+template <bool DX>
 __global__ __launch_bounds__(256) void se_scale_bwd8_kernel(const bf16* __restrict__ dout,
                                                             const bf16* __restrict__ x,
                                                             const float* __restrict__ s, int HW,
@@ -769,7 +771,7 @@ __global__ __launch_bounds__(256) void se_scale_bwd8_kernel(const bf16* __restri
         o[v] = d[v] * sg[v];
         a[v] += d[v] * xv[v];
       }
-      *reinterpret_cast<uint4*>(dx + e) = pack8(o);
+      if (DX) *reinterpret_cast<uint4*>(dx + e) = pack8(o);
     }
   }
 #pragma unroll
@@ -782,6 +784,215 @@ __global__ __launch_bounds__(256) void se_scale_bwd8_kernel(const bf16* __restri
       for (int j = 0; j < RW; ++j) acc += red[(j * G + t) * 8 + v];
       ds[(size_t)n * C + t * 8 + v] = acc * sg[v] * (1.f - sg[v]);
     }
+  }
+}
+
+// ---- squeeze-excite MLP on the pooled [N, C] fp32 vector (efficientnet.py:26-36, senet.py:
+// 59-66, regnet.py:15-24): s = W2 act(W1 p + b1) + b2, W1 [R][C], W2 [C][R] (the 1x1 convs'
+// fp32 masters). Four small kernels replace the library GEMM / GEMV / elementwise chain (5
+// launches forward, 8 backward): two "row" dot kernels (a wave per 8 samples x 4 outputs, lanes
+// across the C reduction) and two "column" kernels (a thread per channel x 8 samples, the short
+// R reduction serial), so even a 128-sample batch spreads over many waves with short
+// dependency chains — a staged-tile variant with one block per 8 samples ran 10-200 us per call.
+constexpr int kSeNB = 8;        // samples per wave / thread
+constexpr int kSeRC = 4;        // row outputs per wave
+
+__device__ __forceinline__ float se_act(float v, int act) {
+  return act == ACT_RELU ? fmaxf(v, 0.f) : v * sigmoidf_(v);
+}
+__device__ __forceinline__ float se_act_grad(float v, int act) {
+  return act == ACT_RELU ? (v > 0.f ? 1.f : 0.f) : act_grad(v, ACT_SWISH);
+}
+
+// out[n][r] = sum_c a[n][c] W(r, c) with W(r, c) = w[r*C + c] (WT = false, W1) or w[c*R + r]
+// (WT = true, W2).  Forward (BWD = false): out = hpre = sum + b1[r].  Backward: out = dz =
+// sum * act'(hpre[n][r]).  One block per (8-sample group, 4 outputs): its 4 waves split the C
+// reduction (two channels per lane in flight), then combine through LDS.
+template <bool WT, bool BWD>
+__global__ __launch_bounds__(256) void se_rowdot_kernel(const float* __restrict__ a, int N, int C,
+                                                        int R, const float* __restrict__ w,
+                                                        const float* __restrict__ b1,
+                                                        const float* __restrict__ hpre, int act,
+                                                        float* __restrict__ out) {
+  __shared__ float part[4][kSeNB * kSeRC];
+  const int lane = threadIdx.x & 63, wv_id = threadIdx.x >> 6;
+  const int rgroups = cdiv(R, kSeRC);
+  const int n0 = (blockIdx.x / rgroups) * kSeNB, r0 = (blockIdx.x % rgroups) * kSeRC;
+  float acc[kSeNB][kSeRC];
+#pragma unroll
+  for (int i = 0; i < kSeNB; ++i)
+#pragma unroll
+    for (int j = 0; j < kSeRC; ++j) acc[i][j] = 0.f;
+  int rr[kSeRC], nn[kSeNB];
+#pragma unroll
+  for (int j = 0; j < kSeRC; ++j) rr[j] = min(r0 + j, R - 1);   // clamped: computed, not stored
+#pragma unroll
+  for (int i = 0; i < kSeNB; ++i) nn[i] = min(n0 + i, N - 1);
+  for (int c0 = wv_id * 64 + lane; c0 < C; c0 += 512) {
+    const int c1 = min(c0 + 256, C - 1);
+    const float keep = c0 + 256 < C ? 1.f : 0.f;       // second channel of the pair, if any
+    float wv[2][kSeRC], av[2][kSeNB];
+#pragma unroll
+    for (int j = 0; j < kSeRC; ++j) {
+      wv[0][j] = WT ? w[(size_t)c0 * R + rr[j]] : w[(size_t)rr[j] * C + c0];
+      wv[1][j] = (WT ? w[(size_t)c1 * R + rr[j]] : w[(size_t)rr[j] * C + c1]) * keep;
+    }
+#pragma unroll
+    for (int i = 0; i < kSeNB; ++i) {
+      av[0][i] = a[(size_t)nn[i] * C + c0];
+      av[1][i] = a[(size_t)nn[i] * C + c1];
+    }
+#pragma unroll
+    for (int i = 0; i < kSeNB; ++i)
+#pragma unroll
+      for (int j = 0; j < kSeRC; ++j) acc[i][j] += av[0][i] * wv[0][j] + av[1][i] * wv[1][j];
+  }
+#pragma unroll
+  for (int i = 0; i < kSeNB; ++i)
+#pragma unroll
+    for (int j = 0; j < kSeRC; ++j) {
+      const float v = wave_sum(acc[i][j]);
+      if (lane == 0) part[wv_id][i * kSeRC + j] = v;
+    }
+  __syncthreads();
+  if (threadIdx.x < kSeNB * kSeRC) {
+    const int i = threadIdx.x / kSeRC, j = threadIdx.x % kSeRC, n = n0 + i, r = r0 + j;
+    const float v = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] +
+                    part[3][threadIdx.x];
+    if (n < N && r < R) {
+      const size_t o = (size_t)n * R + r;
+      out[o] = BWD ? v * se_act_grad(hpre[o], act) : v + (b1 ? b1[r] : 0.f);
+    }
+  }
+}
+
+// out[n][c] = bias[c] + sum_r h(n, r) W(r, c), h = act(hin) (ACTIN) or hin; W(r, c) =
+// w[c*R + r] (WT = true, W2) or w[r*C + c] (WT = false, W1).  Thread -> (channel, 8 samples);
+// the block's 8 x R input rows are staged in LDS (R <= 256).
+template <bool WT, bool ACTIN>
+__global__ __launch_bounds__(256) void se_coldot_kernel(const float* __restrict__ hin, int N, int C,
+                                                        int R, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, int act,
+                                                        float* __restrict__ out) {
+  __shared__ float hs[kSeNB * 256];
+  const int n0 = blockIdx.y * kSeNB, c = blockIdx.x * 256 + threadIdx.x;
+  for (int i = threadIdx.x; i < kSeNB * R; i += 256) {
+    const int n = n0 + i / R;
+    const float v = n < N ? hin[(size_t)n0 * R + i] : 0.f;
+    hs[i] = ACTIN ? se_act(v, act) : v;
+  }
+  __syncthreads();
+  if (c >= C) return;
+  float acc[kSeNB];
+  const float b = bias ? bias[c] : 0.f;
+#pragma unroll
+  for (int i = 0; i < kSeNB; ++i) acc[i] = b;
+  for (int r = 0; r < R; ++r) {
+    const float wv = WT ? w[(size_t)c * R + r] : w[(size_t)r * C + c];
+#pragma unroll
+    for (int i = 0; i < kSeNB; ++i) acc[i] += hs[i * R + r] * wv;
+  }
+#pragma unroll
+  for (int i = 0; i < kSeNB; ++i)
+    if (n0 + i < N) out[(size_t)(n0 + i) * C + c] = acc[i];
+}
+
+// backward, parameter part, added into the gradient buffers with fp32 atomics:
+//   dW2[c][r] += sum_n ds[n][c] h[n][r], db2[c] += sum_n ds[n][c],
+//   dW1[r][c] += sum_n dz[n][r] p[n][c], db1[r] += sum_n dz[n][r].
+// Grid (C / 32 channel tiles, sample chunks); each block walks its chunk 32 samples at a time.
+// LDS: dsT[32][32] | pT[32][32] | hs[32][R] | dzs[32][R]
+constexpr int kSeWC = 32, kSeWN = 32;
+template <int J>   // J >= outputs per thread = 2 * 32 * R / 256
+__global__ __launch_bounds__(256) void se_mlp_bwd_param_kernel(
+    const float* __restrict__ ds, const float* __restrict__ dz, const float* __restrict__ hpre,
+    const float* __restrict__ pooled, int N, int C, int R, int act, int chunk,
+    float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dw2,
+    float* __restrict__ db2) {
+  extern __shared__ float sm[];
+  float* dsT = sm;
+  float* pT = dsT + kSeWN * kSeWC;
+  float* hs = pT + kSeWN * kSeWC;
+  float* dzs = hs + kSeWN * R;
+  const int t = threadIdx.x, c0 = blockIdx.x * kSeWC;
+  const int tc = min(kSeWC, C - c0);
+  const int nbeg = blockIdx.y * chunk, nend = min(N, nbeg + chunk);
+  const int nout = 2 * kSeWC * R;
+  const bool do_b1 = blockIdx.x == 0 && db1 != nullptr;
+  float acc[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) acc[j] = 0.f;
+  float bacc = 0.f;
+  for (int nb0 = nbeg; nb0 < nend; nb0 += kSeWN) {
+    const int nn = min(kSeWN, nend - nb0);
+    __syncthreads();
+    for (int i = t; i < kSeWN * kSeWC; i += 256) {
+      const int n = i / kSeWC, cc = i % kSeWC;
+      const bool ok = n < nn && cc < tc;
+      dsT[i] = ok ? ds[(size_t)(nb0 + n) * C + c0 + cc] : 0.f;
+      pT[i] = ok ? pooled[(size_t)(nb0 + n) * C + c0 + cc] : 0.f;
+    }
+    for (int i = t; i < kSeWN * R; i += 256) {
+      const int n = i / R;
+      const bool ok = n < nn;
+      hs[i] = ok ? se_act(hpre[(size_t)nb0 * R + i], act) : 0.f;
+      dzs[i] = ok ? dz[(size_t)nb0 * R + i] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int o = t + 256 * j;
+      if (o < nout) {
+        float a = 0.f;
+        if (o < kSeWC * R) {            // dW2[c0 + cc][r]
+          const int cc = o / R, r = o % R;
+          for (int n = 0; n < kSeWN; ++n) a += dsT[n * kSeWC + cc] * hs[n * R + r];
+        } else {                        // dW1[r][c0 + cc]
+          const int o2 = o - kSeWC * R, r = o2 / kSeWC, cc = o2 % kSeWC;
+          for (int n = 0; n < kSeWN; ++n) a += dzs[n * R + r] * pT[n * kSeWC + cc];
+        }
+        acc[j] += a;
+      }
+    }
+    if (t < kSeWC) {
+      for (int n = 0; n < kSeWN; ++n) bacc += dsT[n * kSeWC + t];
+    } else if (do_b1 && t - kSeWC < R) {
+      for (int n = 0; n < kSeWN; ++n) bacc += dzs[n * R + t - kSeWC];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int o = t + 256 * j;
+    if (o < nout) {
+      if (o < kSeWC * R) {
+        const int cc = o / R, r = o % R;
+        if (cc < tc) atomicAdd(dw2 + (size_t)(c0 + cc) * R + r, acc[j]);
+      } else {
+        const int o2 = o - kSeWC * R, r = o2 / kSeWC, cc = o2 % kSeWC;
+        if (cc < tc) atomicAdd(dw1 + (size_t)r * C + c0 + cc, acc[j]);
+      }
+    }
+  }
+  if (t < tc && db2) atomicAdd(db2 + c0 + t, bacc);
+  else if (do_b1 && t >= kSeWC && t - kSeWC < R) atomicAdd(db1 + t - kSeWC, bacc);
+}
+
+// dx = dout * sig(s) + dp / HW   (excitation path + broadcast squeeze-path gradient)
+__global__ __launch_bounds__(256) void se_dx8_kernel(const bf16* __restrict__ dout,
+                                                     const float* __restrict__ s,
+                                                     const float* __restrict__ dp, int N, int HW,
+                                                     int C, bf16* __restrict__ dx) {
+  const int G = C >> 3;
+  const int total = N * HW * G;
+  const float inv = 1.f / HW;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int gi = i % G, n = i / (HW * G);
+    const size_t sc = (size_t)n * C + gi * 8;
+    float d[8];
+    unpack8(*reinterpret_cast<const uint4*>(dout + (size_t)i * 8), d);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) d[v] = d[v] * sigmoidf_(s[sc + v]) + dp[sc + v] * inv;
+    *reinterpret_cast<uint4*>(dx + (size_t)i * 8) = pack8(d);
   }
 }
 
@@ -841,7 +1052,9 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, int G, int Cn, i
 // Cr, numel}; chunks[b] = {t, a, b, pass}:
 //   pass 0: elements [a, b) of the forward layout, 8 per thread (16-byte stores);
 //   pass 1: 64x64 (co, ci) transpose tile number a of one (group, tap), staged through LDS so
-//           both the fp32 reads (along ci) and the bf16 writes (along co) are coalesced.
+//           both the fp32 reads (along ci) and the bf16 writes (along co) are coalesced;
+//   pass 2: depthwise weight [Cn][T] -> fp32 tap-major copy [T][Cn] (desc wb = the copy) for
+//           output channels [a, b), the layout the depthwise kernels read 8 channels at a time.
 // All index math is 32-bit and per block / per 8 elements (64-bit div/mod per element made the
 // first version of this kernel 10x slower than its bandwidth).
 __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* __restrict__ desc,
@@ -852,6 +1065,15 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* _
   const float* w = reinterpret_cast<const float*>(d[0]);
   const int Cn = (int)d[4], T = (int)d[5], Cr = (int)d[6];
   const int tid = threadIdx.x;
+  if (ch[3] == 2) {
+    float* wtf = reinterpret_cast<float*>(d[1]);
+    const int c0 = (int)ch[1], nc = (int)ch[2] - c0;
+    for (int k = tid; k < nc * T; k += 256) {
+      const int co = c0 + k / T, tap = k % T;
+      wtf[tap * Cn + co] = w[co * T + tap];
+    }
+    return;
+  }
   if (ch[3] == 0) {
     bf16* wb = reinterpret_cast<bf16*>(d[1]);
     const int s0 = (int)ch[1], s1 = (int)ch[2];
@@ -1158,11 +1380,63 @@ void se_scale_fwd_launch(const bf16* x, const float* s, int N, int HW, int C, bf
 void se_scale_bwd_launch(const bf16* dout, const bf16* x, const float* s, int N, int HW, int C,
                          bf16* dx, float* ds, hipStream_t st) {
   if (vec8_ok(C)) {
-    hipLaunchKernelGGL(se_scale_bwd8_kernel, dim3(N), dim3(256), 0, st, dout, x, s, HW, C, dx, ds);
+    hipLaunchKernelGGL(se_scale_bwd8_kernel<true>, dim3(N), dim3(256), 0, st, dout, x, s, HW, C, dx, ds);
     return;
   }
   hipLaunchKernelGGL(se_scale_bwd_kernel, dim3(cdiv(C, 64), N), dim3(256), 0, st, dout, x, s, N, HW,
                      C, dx, ds);
+}
+static size_t se_param_lds_bytes(int R) {
+  return sizeof(float) * (2 * kSeWN * kSeWC + 2 * (size_t)kSeWN * R);
+}
+// (64 KB of static LDS per block for the parameter kernel; R <= 192 keeps its per-thread
+// outputs within 64 registers and the column kernels' staged rows within 8 x 256 floats)
+bool se_mlp_supported(int C, int R) {
+  return C % 8 == 0 && C <= 2048 && R >= 1 && R <= 192 && se_param_lds_bytes(R) <= 65536;
+}
+static dim3 se_row_grid(int N, int R) { return dim3(cdiv(N, kSeNB) * cdiv(R, kSeRC)); }
+static dim3 se_col_grid(int N, int C) { return dim3(cdiv(C, 256), cdiv(N, kSeNB)); }
+void se_mlp_fwd_launch(const float* pooled, int N, int C, int R, const float* w1, const float* b1,
+                       const float* w2, const float* b2, int act, float* hpre, float* s,
+                       hipStream_t st) {
+  hipLaunchKernelGGL((se_rowdot_kernel<false, false>), se_row_grid(N, R), dim3(256), 0, st, pooled,
+                     N, C, R, w1, b1, nullptr, act, hpre);
+  hipLaunchKernelGGL((se_coldot_kernel<true, true>), se_col_grid(N, C), dim3(256), 0, st, hpre, N,
+                     C, R, w2, b2, act, s);
+}
+void se_mlp_bwd_launch(const float* ds, const float* hpre, const float* pooled, int N, int C,
+                       int R, const float* w1, const float* w2, int act, float* dz, float* dp,
+                       float* dw1, float* db1, float* dw2, float* db2, hipStream_t st) {
+  hipLaunchKernelGGL((se_rowdot_kernel<true, true>), se_row_grid(N, R), dim3(256), 0, st, ds, N, C,
+                     R, w2, nullptr, hpre, act, dz);
+  hipLaunchKernelGGL((se_coldot_kernel<false, false>), se_col_grid(N, C), dim3(256), 0, st, dz, N,
+                     C, R, w1, nullptr, act, dp);
+  // ~2 blocks per CU: split the samples into chunks over the channel tiles
+  const int ct = cdiv(C, kSeWC);
+  const int nchunks = std::max(1, std::min(cdiv(N, kSeWN), 512 / ct));
+  const int chunk = cdiv(cdiv(N, nchunks), kSeWN) * kSeWN;
+  const size_t lds = se_param_lds_bytes(R);
+  const dim3 grid(ct, cdiv(N, chunk));
+  const int need = cdiv(2 * kSeWC * R, 256);
+#define PCA_SE_PARAM(J)                                                                        \
+  hipLaunchKernelGGL(se_mlp_bwd_param_kernel<J>, grid, dim3(256), lds, st, ds, dz, hpre, pooled, \
+                     N, C, R, act, chunk, dw1, db1, dw2, db2)
+  if (need <= 4) PCA_SE_PARAM(4);
+  else if (need <= 8) PCA_SE_PARAM(8);
+  else if (need <= 16) PCA_SE_PARAM(16);
+  else if (need <= 32) PCA_SE_PARAM(32);
+  else PCA_SE_PARAM(64);
+#undef PCA_SE_PARAM
+}
+void se_ds_launch(const bf16* dout, const bf16* x, const float* s, int N, int HW, int C, float* ds,
+                  hipStream_t st) {
+  hipLaunchKernelGGL(se_scale_bwd8_kernel<false>, dim3(N), dim3(256), 0, st, dout, x, s, HW, C,
+                     nullptr, ds);
+}
+void se_dx_launch(const bf16* dout, const float* s, const float* dp, int N, int HW, int C, bf16* dx,
+                  hipStream_t st) {
+  hipLaunchKernelGGL(se_dx8_kernel, dim3(grid_cap((size_t)N * HW * C / 8)), dim3(256), 0, st, dout,
+                     s, dp, N, HW, C, dx);
 }
 void act_fwd_launch(const bf16* x, size_t n, int act, bf16* y, hipStream_t st) {
   hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_cap(n)), dim3(256), 0, st, x, n, act, y);

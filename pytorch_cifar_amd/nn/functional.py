@@ -21,6 +21,7 @@ from ..ops.functional import (  # noqa: F401
     relu,
     se_excite,
     split_channels,
+    squeeze_excite,
 )
 
 
@@ -108,10 +109,14 @@ def se_gate(x, fc1, fc2, act="relu"):
 
     ``fc1``/``fc2`` are the reference's 1x1 ``Conv2d`` modules with bias (efficientnet.py:28-31,
     regnet.py:15-18, senet.py:59-60); on the pooled [N, C] vector they are plain GEMMs, so the
-    squeeze runs on the native global-pool kernel, the two tiny FCs as library GEMMs in fp32
-    (:class:`_SEMLP` on the GPU, plain autograd on the CPU reference path) and the excitation
-    (sigmoid + broadcast scale, and its backward) on the native SE kernel.
+    whole block normally runs as the native squeeze-excite kernels (pool, fp32 MLP, sigmoid scale;
+    ``ops.functional.squeeze_excite``). Otherwise the squeeze runs on the native global-pool
+    kernel, the two tiny FCs as library GEMMs in fp32 (:class:`_SEMLP` on the GPU, plain autograd
+    on the CPU reference path) and the excitation on the native SE-scale kernel.
     """
+    y = squeeze_excite(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, act)
+    if y is not None:
+        return y
     n, c = x.shape[0], x.shape[1]
     pooled = global_avg_pool(x).reshape(n, c).to(fc1.weight.dtype)
     if (not _ref(x) and act in ("relu", "swish", "silu") and pooled.dtype == torch.float32

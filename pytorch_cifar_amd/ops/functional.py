@@ -233,7 +233,13 @@ class WeightPrepPlan:
         return None
 
     def register(self, w, groups, w_phys):
-        wb, wt = _C().weight_prep(w_phys, groups, True)
+        if groups == DW_PREP:
+            # depthwise: fp32 tap-major copy [KH*KW][Co] (valid for this forward already)
+            co = w.shape[0]
+            wb = w.detach().reshape(co, -1).t().contiguous()
+            wt = None
+        else:
+            wb, wt = _C().weight_prep(w_phys, groups, True)
         e = _PrepEntry(w, groups, wb, wt)
         self.entries.append(e)
         self.by_id[id(w)] = e
@@ -246,6 +252,10 @@ class WeightPrepPlan:
             wp = G.physical(e.w)
             Cout, KH, KW, Cg = wp.shape
             n = wp.numel()
+            if e.groups == DW_PREP:
+                desc.append([wp.data_ptr(), e.wb.data_ptr(), 0, 1, Cout, KH * KW, 1, n])
+                chunks += [[t, c0, min(Cout, c0 + 64), 2] for c0 in range(0, Cout, 64)]
+                continue
             desc.append([wp.data_ptr(), e.wb.data_ptr(), e.wt.data_ptr(), e.groups,
                          Cout // e.groups, KH * KW, Cg, n])
             chunks += [[t, s0, min(n, s0 + _PREP_CHUNK), 0] for s0 in range(0, n, _PREP_CHUNK)]
@@ -287,6 +297,23 @@ def enable_batched_weight_prep(model):
         model.register_forward_pre_hook(_plan_pre_hook)
         model.register_forward_hook(_plan_post_hook)
     return model
+
+
+DW_PREP = -1      # WeightPrepPlan "groups" key of a depthwise weight's tap-major fp32 copy
+
+
+def _dw_weight(weight):
+    """Depthwise weight [Co,1,KH,KW] as the fp32 tap-major [KH*KW][Co] operand of the kernels:
+    from the active plan (refreshed by its one batched launch per forward) when there is one."""
+    plan = _PLAN["cur"]
+    if plan is not None and weight.is_leaf and weight.dtype == torch.float32 and \
+            weight.permute(0, 2, 3, 1).is_contiguous():
+        e = plan.lookup(weight, DW_PREP)
+        if e is None:
+            e = plan.register(weight, DW_PREP, None)
+        return e.wb
+    Co = weight.shape[0]
+    return weight.detach().reshape(Co, -1).t().contiguous()
 
 
 def _prepped_weight(weight, groups, w_phys, need_dx):
@@ -340,6 +367,9 @@ class _BNSrc:
 # (clean -> filled -> used) falls back to a memset only when a pass is skipped (a forward without
 # backward). Deterministic mode (ordered slab rows + finalize kernel) and PCA_BN_ACC=0 turn it off.
 _BN_ACC = os.environ.get("PCA_BN_ACC", "1") != "0"
+# BNs whose input comes with no conv statistics get their own statistics pass into an accumulator
+# (off by default: measured slower, its reduction runs on few blocks to bound atomic contention)
+_BN_OWN_STATS = os.environ.get("PCA_BN_OWN_STATS", "0") != "0"
 _DETERMINISTIC = False
 
 
@@ -406,6 +436,26 @@ def _bn_fusable(C, act, has_res, dual, bn, bn2=None):
             and not (has_res and dual)):
         return False
     return bn.running_mean is not None and (bn2 is None or bn2.running_mean is not None)
+
+
+_ACC_MAX = []
+
+
+def _acc_max_elems():
+    if not _ACC_MAX:
+        _ACC_MAX.append(_C().bn_acc_max_elems())
+    return _ACC_MAX[0]
+
+
+def _own_stats(bn, role, y_nhwc, stats):
+    if stats is not None:
+        return stats
+    a = stat_acc(bn, role, y_nhwc.shape[-1], 2, y_nhwc.device)
+    a.begin()
+    if _C().bn_stats_acc(y_nhwc, a.buf, a.R):
+        return a
+    a.state = "clean"             # too large for the accumulator form: nothing was added
+    return None
 
 
 def _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add):
@@ -573,7 +623,7 @@ class _ConvDepthwise(torch.autograd.Function):
     def forward(ctx, x, weight, stride, padding):
         C = _C()
         Co, _, KH, KW = weight.shape
-        wT = weight.detach().reshape(Co, KH * KW).t().contiguous()
+        wT = _dw_weight(weight)
         y = C.dw_fwd(x, wT, KH, KW, stride, padding)
         ctx.save_for_backward(x, wT)
         ctx.geom = (stride, padding, KH, KW)
@@ -848,8 +898,13 @@ class _BatchNormAct(torch.autograd.Function):
             else:
                 acc.ensure_clean()        # filled by a dgrad whose output is not dout: discard
             part = None
-            # unfilled: the backward takes its slab-reduce path and leaves the accumulator clean
-            acc.state = "used" if filled else "clean"
+            # unfilled: tensors up to bn_acc_max_elems() are reduced into the accumulator by a
+            # separate pass (then consumed: "used"), larger ones take the slab path and leave it
+            # untouched ("clean": no memset before the next forward)
+            if filled or y.numel() <= _acc_max_elems():
+                acc.state = "used"
+            else:
+                acc.state = "clean"
             # the forward accumulators this BN consumed are cleared by the backward kernel
             for i, fa in enumerate(cfg.faccs):
                 if fa.state == "used":
@@ -942,6 +997,13 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
             _bn_fusable(Cc, act, residual is not None, bn2 is not None, bn, bn2):
         # (also without grad: the forward kernel then just keeps it clear)
         cfg.bacc = stat_acc(bn, "bwd", Cc, 3 if bn2 is not None else 2, y.device)
+        # no producing conv delivered statistics (depthwise / concat / pooled inputs): a
+        # separate statistics pass adds them into this BN's own accumulator (small tensors), so
+        # the fused finalize+apply kernel still serves it
+        if _BN_OWN_STATS:
+            stats = _own_stats(bn, "fwdstat", y, stats)
+            if bn2 is not None:
+                st2 = _own_stats(bn2, "fwdstat", y2, st2)
         # the producing conv(s) may deliver their statistics through accumulators from now on
         p1 = getattr(x, "_pca_stats_src", None)
         p2 = getattr(residual_bn[1], "_pca_stats_src", None) if residual_bn is not None else None
@@ -1195,6 +1257,60 @@ def se_excite(x, s_logits):
         return x * torch.sigmoid(s_logits).view(x.shape[0], x.shape[1], 1, 1)
     s = s_logits.reshape(x.shape[0], x.shape[1]).float().contiguous()
     return to_nchw(_SEScale.apply(to_nhwc(x), s))
+
+
+class _SqueezeExcite(torch.autograd.Function):
+    """The whole squeeze-excite block on NHWC bf16 x (csrc/misc.hip se_*): 3 launches forward
+    (pool, MLP, scale) and 4 backward (excitation reduce, MLP data, MLP parameters with fp32
+    atomics into the gradient arena, combined dx) instead of the 5 + 10 of the library-GEMM
+    composition."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, act):
+        out, pooled, hpre, s = _C().se_forward(x, w1, b1, w2, b2, act)
+        ctx.save_for_backward(x, pooled, hpre, s, w1, w2)
+        ctx.act = act
+        ctx.params = (w1, b1, w2, b2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, pooled, hpre, s, w1s, w2s = ctx.saved_tensors
+        params = ctx.params
+        ctx.params = None
+
+        def buf(p):
+            return G.grad_buffer(p) if (p is not None and p.requires_grad and p.is_leaf) else None
+
+        bufs = [buf(p) for p in params]
+        dx, dw1, db1, dw2, db2 = _C().se_backward(
+            dout.contiguous(), x, pooled, hpre, s, w1s, w2s, ctx.act,
+            *[b.view(-1) if b is not None else None for b in bufs],
+            params[1] is not None, params[3] is not None)
+        ret = []
+        for p, b, g in zip(params, bufs, (dw1, db1, dw2, db2)):
+            r = None
+            if p is not None and p.requires_grad:
+                if b is not None:
+                    G.fire(p)
+                elif p.is_leaf:
+                    G.accumulate(p, g.view(p.shape))
+                else:
+                    r = g.view(p.shape)
+            ret.append(r)
+        return (dx, *ret, None)
+
+
+def squeeze_excite(x, w1, b1, w2, b2, act):
+    """x * sigmoid(W2 act(W1 mean_hw(x) + b1) + b2) as one native block, or None when the
+    shapes / mode need the composed path (CPU reference, deterministic mode: the parameter
+    gradients are fp32 atomics)."""
+    if (_ref(x) or act not in ("relu", "swish", "silu") or w1.dtype != torch.float32
+            or w2.dtype != torch.float32 or torch.is_autocast_enabled()
+            or _DETERMINISTIC or _C().deterministic()
+            or not _C().se_supported(x.shape[1], w1.shape[0])):
+        return None
+    return to_nchw(_SqueezeExcite.apply(to_nhwc(x), w1, b1, w2, b2, ACT[act]))
 
 
 # ------------------------------------------------------------------------ cross-entropy

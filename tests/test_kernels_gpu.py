@@ -463,3 +463,58 @@ def test_fused_head_matches_fp32(N, H, C, K, C_=None):
     assert rel_err(dx, xr.grad) < 1e-2
     assert rel_err(dw - dw0, wr.grad) < 1e-4
     assert rel_err(db - db0, br.grad) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,C,R,act,bias", [
+    (128, 16, 96, 4, 2, True),       # EfficientNet-B0 stage-2 shapes
+    (7, 2, 1152, 48, 2, True),       # last stage, ragged batch (< 8 samples per block)
+    (33, 8, 512, 32, 1, True),       # SENet18 (ReLU)
+    (70, 4, 440, 26, 1, False),      # RegNet-like, no bias, ragged tiles (C % 64, R odd)
+    (1024, 4, 1152, 48, 2, True),    # bs1024: several sample chunks per channel tile
+])
+def test_squeeze_excite_matches_fp32(N, H, C, R, act, bias):
+    """Native squeeze-excite block (pool + fp32 MLP + sigmoid scale, and its backward with the
+    parameter gradients added into given buffers) against the fp32 torch composition."""
+    from pytorch_cifar_amd import _native
+
+    L = _native.lib()
+    assert L.se_supported(C, R)
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
+    w1 = torch.randn(R, C, 1, 1, device="cuda") * 0.1
+    w2 = torch.randn(C, R, 1, 1, device="cuda") * 0.1
+    b1 = torch.randn(R, device="cuda") if bias else None
+    b2 = torch.randn(C, device="cuda") if bias else None
+    out, pooled, hpre, s = L.se_forward(x, w1, b1, w2, b2, act)
+
+    xr = x.float().requires_grad_(True)
+    w1r, w2r = w1.clone().requires_grad_(True), w2.clone().requires_grad_(True)
+    b1r = b1.clone().requires_grad_(True) if bias else None
+    b2r = b2.clone().requires_grad_(True) if bias else None
+    p = xr.mean((1, 2))
+    h = torch.nn.functional.linear(p, w1r.view(R, C), b1r)
+    h = torch.relu(h) if act == 1 else torch.nn.functional.silu(h)
+    sr = torch.nn.functional.linear(h, w2r.view(C, R), b2r)
+    ref = xr * torch.sigmoid(sr)[:, None, None, :]
+    assert rel_err(pooled, p.detach()) < 1e-5
+    assert rel_err(s, sr.detach()) < 1e-4
+    assert rel_err(out, ref.detach()) < 1e-2
+
+    dout = torch.randn_like(x)
+    ref.backward(dout.float())
+    dw10, dw20 = torch.randn(R * C, device="cuda"), torch.randn(R * C, device="cuda")
+    db10, db20 = torch.randn(R, device="cuda"), torch.randn(C, device="cuda")
+    acc = [t.clone() for t in (dw10, db10, dw20, db20)]
+    dx, dw1, db1, dw2, db2 = L.se_backward(dout, x, pooled, hpre, s, w1, w2, act,
+                                           acc[0], acc[1] if bias else None, acc[2],
+                                           acc[3] if bias else None, bias, bias)
+    assert dw1.data_ptr() == acc[0].data_ptr() and dw2.data_ptr() == acc[2].data_ptr()
+    assert rel_err(dx, xr.grad) < 1e-2
+    assert rel_err(dw1 - dw10, w1r.grad.view(-1)) < 1e-3
+    assert rel_err(dw2 - dw20, w2r.grad.view(-1)) < 1e-3
+    if bias:
+        assert rel_err(db1 - db10, b1r.grad) < 1e-3
+        assert rel_err(db2 - db20, b2r.grad) < 1e-3
+    else:
+        assert db1 is None and db2 is None

@@ -183,7 +183,8 @@ def static_tiles():
 
 
 @pytest.mark.parametrize("name", ["ResNet18", "ResNet50", "PreActResNet18", "MobileNetV2",
-                                  "EfficientNetB0", "RegNetY_400MF", "densenet_cifar", "DLA"])
+                                  "EfficientNetB0", "RegNetY_400MF", "densenet_cifar", "DLA",
+                                  "SENet18"])
 def test_bn_accumulators_match_reference(name, static_tiles):
     """Steps after the first route every conv->BN statistic and every BN-backward sum through the
     sharded accumulators (fused finalize in the BN kernels): still as close to fp32 as stock
@@ -205,7 +206,7 @@ def test_bn_accumulators_match_reference(name, static_tiles):
     torch.cuda.synchronize()
     for k, a in items:
         assert isinstance(a, StatAcc)
-        if k[0] == "fwd":
+        if k[0] in ("fwd", "fwdstat"):
             assert a.state == "clean", (k, a.state)
         if a.state == "clean":
             assert a.buf.abs().max().item() == 0, f"{k}: accumulator marked clean is not zero"
@@ -223,23 +224,28 @@ def test_bn_accumulators_match_reference(name, static_tiles):
         assert len(fwd) >= 19 and len(bwd) >= 17, (len(fwd), len(bwd))
 
 
-def test_batched_weight_prep_matches_per_conv(reproducible_convs):
-    """The one-launch weight conversion (forward pre-hook) produces the same forward/backward as
-    per-conv conversion, and follows in-place weight updates (it re-converts every forward).
+@pytest.mark.parametrize("name", ["ResNet18", "MobileNetV2"])
+def test_batched_weight_prep_matches_per_conv(name, reproducible_convs):
+    """The one-launch weight conversion (forward pre-hook; MFMA conv operands and the depthwise
+    tap-major copies) produces the same forward/backward as per-conv conversion, and follows
+    in-place weight updates (it re-converts every forward).
     Deterministic mode: with fp32-atomic BatchNorm sums the backward chain of two identical
     models differs in bf16 rounding, so it would not isolate the weight conversion."""
     from pytorch_cifar_amd import models
     from pytorch_cifar_amd.engine.arena import ParamArena
-    from pytorch_cifar_amd.ops.functional import cross_entropy, enable_batched_weight_prep
+    from pytorch_cifar_amd.ops.functional import DW_PREP, cross_entropy, enable_batched_weight_prep
 
     torch.manual_seed(0)
-    a = models.ResNet18().cuda()
+    a = models.MODEL_REGISTRY[name]().cuda()
     b = copy.deepcopy(a)
     ParamArena(a.parameters())
     ParamArena(b.parameters())
     enable_batched_weight_prep(b)
     x = torch.randn(16, 3, 32, 32, device="cuda")
     y = torch.randint(0, 10, (16,), device="cuda")
+    convs = [n for n, m in a.named_modules()
+             if isinstance(getattr(m, "weight", None), torch.Tensor) and m.weight.dim() == 4]
+    dw = [n for n, m in a.named_modules() if getattr(m, "groups", 1) > 1]
     for it in range(2):
         outs = []
         for m in (a, b):
@@ -255,9 +261,15 @@ def test_batched_weight_prep_matches_per_conv(reproducible_convs):
             torch.testing.assert_close(p.grad, ga[n].grad, rtol=1e-2, atol=1e-4)
         with torch.no_grad():   # an in-place update that does not go through the optimizer
             for m in (a, b):
-                m.conv1.weight.mul_(0.5)
-                m.layer2[0].conv1.weight.add_(0.01)
-    assert len(b.__dict__["_pca_wplan"].entries) >= 19
+                mods = dict(m.named_modules())
+                mods[convs[0]].weight.mul_(0.5)
+                mods[convs[5]].weight.add_(0.01)
+                if dw:
+                    mods[dw[1]].weight.mul_(-0.7)
+    entries = b.__dict__["_pca_wplan"].entries
+    assert len(entries) >= 19
+    if dw:
+        assert sum(e.groups == DW_PREP for e in entries) >= len(dw) - 1
 
 
 def test_bn_backward_reduce_fusion_matches_separate_pass():

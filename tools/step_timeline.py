@@ -22,7 +22,8 @@ CATEGORIES = [
     ("batchnorm fwd", r"bn_apply|bn_finalize|bn_stats|colsum"),
     ("batchnorm bwd", r"bn_bwd"),
     ("optimizer / weight prep", r"sgd_kernel|weight_prep"),
-    ("head (pool, linear, CE)", r"gap_|Cijk|ce_fused|scale_by_scalar|reduce_kernel"),
+    ("squeeze-excite", r"se_scale|se_"),
+    ("head (pool, linear, CE)", r"head_|gap_|Cijk|ce_fused|scale_by_scalar|reduce_kernel"),
     ("data (augment, gather)", r"augment|scatter_gather|copyBuffer"),
 ]
 
