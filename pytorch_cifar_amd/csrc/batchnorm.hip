@@ -289,6 +289,61 @@ __device__ __forceinline__ void compute_dz(const bf16* dout, const bf16* out, co
 }
 
 // ---- backward reduce: partial[P][NS][C] with sums of dz, dz*xhat, (dz*xhat2) ----
+// Fast path body (8 channels, single BN; masked ReLU / swish / no act): kBwdRows rows of one
+// thread from clamped (unconditional) loads issued before the per-channel constants, rows past
+// r1 weighted 0. Straight-line loads matter on the small late-stage tensors, where each thread
+// sees only a few rows: a guarded / loop-carried chain of them (and branchy per-element loads
+// of the constants) left the kernel latency-bound at ~10 us whatever the size.
+constexpr int kBwdRows = 4;
+template <bool MASK, bool SWISH>
+__device__ __forceinline__ void bwd_reduce_rows(const bf16* __restrict__ dout,
+                                                const bf16* __restrict__ y,
+                                                const uint8_t* __restrict__ mask,
+                                                const float* __restrict__ aux, int C, int c0, int r,
+                                                int r1, int rpp, float (&acc)[2][8]) {
+  uint4 dr[kBwdRows], yr[kBwdRows];
+  uint32_t mr[kBwdRows];
+  float wgt[kBwdRows];
+#pragma unroll
+  for (int k = 0; k < kBwdRows; ++k) {
+    const int rk = r + k * rpp;
+    wgt[k] = rk < r1 ? 1.f : 0.f;
+    const size_t e = (size_t)min(rk, r1 - 1) * C + c0;
+    dr[k] = *reinterpret_cast<const uint4*>(dout + e);
+    yr[k] = *reinterpret_cast<const uint4*>(y + e);
+    mr[k] = MASK ? mask[e >> 3] : 0xffu;
+  }
+  // aux = [mean | istd | scale | shift] x C (scale / shift: the BN affine as used by the act)
+  float mean[8], istd[8], sc[8], sh[8];
+  const float4* a4 = reinterpret_cast<const float4*>(aux + c0);
+  const int q = C >> 2;
+  const float4 m0 = a4[0], m1 = a4[1], i0 = a4[q], i1 = a4[q + 1];
+  mean[0] = m0.x; mean[1] = m0.y; mean[2] = m0.z; mean[3] = m0.w;
+  mean[4] = m1.x; mean[5] = m1.y; mean[6] = m1.z; mean[7] = m1.w;
+  istd[0] = i0.x; istd[1] = i0.y; istd[2] = i0.z; istd[3] = i0.w;
+  istd[4] = i1.x; istd[5] = i1.y; istd[6] = i1.z; istd[7] = i1.w;
+  if constexpr (SWISH) {
+    const float4 s0 = a4[2 * q], s1 = a4[2 * q + 1], h0 = a4[3 * q], h1 = a4[3 * q + 1];
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
+    sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+  }
+#pragma unroll
+  for (int k = 0; k < kBwdRows; ++k) {
+    float dz[8], yy[8];
+    unpack8(dr[k], dz);
+    unpack8(yr[k], yy);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      float a = ((mr[k] >> v) & 1u) ? dz[v] * wgt[k] : 0.f;
+      if constexpr (SWISH) a *= act_grad(yy[v] * sc[v] + sh[v], ACT_SWISH);
+      acc[0][v] += a;
+      acc[1][v] += a * (yy[v] - mean[v]) * istd[v];
+    }
+  }
+}
+
 template <int VEC, int NS>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16* __restrict__ dout, const bf16* __restrict__ out, const uint8_t* __restrict__ mask,
@@ -322,36 +377,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
       }
       int r = r0 + ry;
       if constexpr (VEC == 8 && NS == 2) {
-        // masked-ReLU / no-act / swish fast path: two rows in flight per thread
-        const bool swish = act == ACT_SWISH;
-        if (mask || act == ACT_NONE || swish) {
-          float sc[8], sh[8];
-#pragma unroll
-          for (int v = 0; v < 8; ++v) {
-            sc[v] = swish ? aux[2 * C + c0 + v] : 0.f;
-            sh[v] = swish ? aux[3 * C + c0 + v] : 0.f;
-          }
-          for (; r + rp.RPP < r1; r += 2 * rp.RPP) {
-            const size_t e = (size_t)r * C + c0, e2 = e + (size_t)rp.RPP * C;
-            float dz[8], dz2[8], yy[8], yy2[8];
-            unpack8(*reinterpret_cast<const uint4*>(dout + e), dz);
-            unpack8(*reinterpret_cast<const uint4*>(dout + e2), dz2);
-            unpack8(*reinterpret_cast<const uint4*>(y + e), yy);
-            unpack8(*reinterpret_cast<const uint4*>(y + e2), yy2);
-            const uint32_t m = mask ? mask[e >> 3] : 0xffu, m2 = mask ? mask[e2 >> 3] : 0xffu;
-#pragma unroll
-            for (int v = 0; v < 8; ++v) {
-              float a = ((m >> v) & 1u) ? dz[v] : 0.f;
-              float b = ((m2 >> v) & 1u) ? dz2[v] : 0.f;
-              if (swish) {   // swish'(z), z recomputed from y (the BN output before the act)
-                a *= act_grad(yy[v] * sc[v] + sh[v], ACT_SWISH);
-                b *= act_grad(yy2[v] * sc[v] + sh[v], ACT_SWISH);
-              }
-              acc[0][v] += a + b;
-              acc[1][v] += (a * (yy[v] - mean[v]) + b * (yy2[v] - mean[v])) * istd[v];
-            }
-          }
-        }
+        // masked-ReLU / no-act / swish fast path (bwd_reduce_rows)
+        if (mask)
+          for (; r < r1; r += kBwdRows * rp.RPP)
+            bwd_reduce_rows<true, false>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+        else if (act == ACT_SWISH)
+          for (; r < r1; r += kBwdRows * rp.RPP)
+            bwd_reduce_rows<false, true>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+        else if (act == ACT_NONE)
+          for (; r < r1; r += kBwdRows * rp.RPP)
+            bwd_reduce_rows<false, false>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
       }
       for (; r < r1; r += rp.RPP) {
         const size_t e = (size_t)r * C + c0;
