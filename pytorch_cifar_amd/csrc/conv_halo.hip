@@ -33,7 +33,7 @@ struct HaloGeom {
   int HR;                 // halo rows per stage = IMGS * (RS+2) * (W+2)
   int HI;                 // halo DMA instructions per stage = ceil(HR / 8)
   int chunk, splits, atomic;
-  int ablate;             // diagnostics (PCA_HALO_ABLATE): 1 = no DMA, 2 = no MFMA phase
+  int ablate;             // diagnostics (PCA_HALO_ABLATE): 1 = no DMA, 2 = no MFMA phase, 4 = no epilogue
   uint32_t x_bytes, dy_bytes;
   FastDiv fd_hw, fd_w;
 };
@@ -256,8 +256,24 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
     }
   }
   wait_vmcnt<0>();
+  if (g.ablate & 4) return;
 
-  float* dst = g.atomic ? out : out + (size_t)split * g.groups * g.cout_g * g.Ktot;
+  if (!g.atomic) {
+    // slab row in accumulator order: each (wave, mi, ni) fragment is one 1 KiB dwordx4 store of
+    // 64 lanes x float4, instead of 4 dword stores of 4 x 64-byte row pieces each (the scattered
+    // store tail alone took ~18 us of the ~25 us kernel on the bs128 shard: 256 blocks x 147 KB).
+    // halo_slab_reduce_kernel maps the order back to dW[co][tap][ci].
+    const int tiles = gridDim.x * gridDim.y * g.groups;
+    const int tile = (grp * gridDim.x + blockIdx.x) * gridDim.y + blockIdx.y;
+    float4* dst4 = reinterpret_cast<float4*>(out) + (size_t)(split * tiles + tile) * (BM * BN / 4);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+        dst4[((wid * TM + mi) * TN + ni) * 64 + lane] =
+            make_float4(acc[mi][ni][0], acc[mi][ni][1], acc[mi][ni][2], acc[mi][ni][3]);
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -269,30 +285,101 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
         const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + j;
         if (m < g.cout_g) {
           const size_t idx = ((size_t)grp * g.cout_g + m) * g.Ktot + col;
-          if (g.atomic) {
-            if (g.splits == 1) dst[idx] += acc[mi][ni][j];   // sole writer
-            else atomicAdd(dst + idx, acc[mi][ni][j]);
-          } else {
-            dst[idx] = acc[mi][ni][j];
-          }
+          if (g.splits == 1) out[idx] += acc[mi][ni][j];   // sole writer
+          else atomicAdd(out + idx, acc[mi][ni][j]);
         }
       }
     }
 }
 
-// Slab reduction in a fixed order, one kernel: a block owns 64 float4 columns; its 4 thread
-// lanes per column sum the slab rows s = l, l+4, ... and the 4 lane partials are added in lane
-// order (deterministic) before dW += sum.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float4* __restrict__ slab,
-                                                          float4* __restrict__ dw, int splits,
-                                                          int64_t n4) {
-  __shared__ float4 red[4][64];
-  const int c = threadIdx.x & 63, l = threadIdx.x >> 6;
+// Geometry of the accumulator-order slab rows written by wgrad_halo_kernel (per tile:
+// [wave][mi][ni][lane] float4 = rows m..m+3 of one column).
+struct HaloSlabMap {
+  int TM, TN, WN, WTM, WTN, BM, BN;
+  int tiles_x, tiles_y;   // grid.x (output-channel tiles), grid.y (64-channel input blocks)
+  int cout_g, cin_g, Ktot;
+};
+
+// dW += sum_s slab[s] in a fixed order: a block owns 64 float4 slots; its L = blockDim/64 split
+// lanes sum slab rows s = l, l+L, ... (4 loads in flight), the L partials are added in lane order,
+// and the slot is scattered back to dW[co][tap][ci] (its 4 rows).
+__global__ __launch_bounds__(1024) void halo_slab_reduce_kernel(const float4* __restrict__ slab,
+                                                                float* __restrict__ dw, int splits,
+                                                                int64_t n4, HaloSlabMap mp) {
+  __shared__ float4 red[16][64];
+  const int c = threadIdx.x & 63, l = threadIdx.x >> 6, L = blockDim.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * 64 + c;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q < n4) {
+    int s = l;
+    for (; s + 3 * L < splits; s += 4 * L) {
+      const float4 v0 = slab[(int64_t)s * n4 + q];
+      const float4 v1 = slab[(int64_t)(s + L) * n4 + q];
+      const float4 v2 = slab[(int64_t)(s + 2 * L) * n4 + q];
+      const float4 v3 = slab[(int64_t)(s + 3 * L) * n4 + q];
+      a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+      a.x += v1.x; a.y += v1.y; a.z += v1.z; a.w += v1.w;
+      a.x += v2.x; a.y += v2.y; a.z += v2.z; a.w += v2.w;
+      a.x += v3.x; a.y += v3.y; a.z += v3.z; a.w += v3.w;
+    }
+    for (; s < splits; s += L) {
+      const float4 v = slab[(int64_t)s * n4 + q];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[l][c] = a;
+  __syncthreads();
+  if (l != 0 || q >= n4) return;
+  for (int k = 1; k < L; ++k) {
+    const float4 v = red[k][c];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  const int per_tile = mp.BM * mp.BN / 4;
+  const int tile = (int)(q / per_tile);
+  int r = (int)(q - (int64_t)tile * per_tile);
+  const int lane = r & 63;
+  r >>= 6;
+  const int ni = r % mp.TN;
+  r /= mp.TN;
+  const int mi = r % mp.TM;
+  const int wid = r / mp.TM;
+  const int wm = wid / mp.WN, wn = wid - wm * mp.WN;
+  const int by = tile % mp.tiles_y;
+  const int bx = (tile / mp.tiles_y) % mp.tiles_x;
+  const int grp = tile / (mp.tiles_y * mp.tiles_x);
+  const int n = wn * mp.WTN + ni * 16 + (lane & 15);
+  const int col = (n >> 6) * mp.cin_g + by * 64 + (n & 63);
+  const int mb = bx * mp.BM + wm * mp.WTM + mi * 16 + (lane >> 4) * 4;
+  const float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (mb + j < mp.cout_g) dw[((size_t)grp * mp.cout_g + mb + j) * mp.Ktot + col] += v[j];
+}
+
+// Slab reduction in a fixed order, one kernel: a block owns 64 float4 columns; its L =
+// blockDim/64 thread lanes per column sum the slab rows s = l, l+L, ... (4 loads in flight) and
+// the L lane partials are added in lane order (deterministic) before dW += sum.
+__global__ __launch_bounds__(1024) void slab_reduce_kernel(const float4* __restrict__ slab,
+                                                           float4* __restrict__ dw, int splits,
+                                                           int64_t n4) {
+  __shared__ float4 red[16][64];
+  const int c = threadIdx.x & 63, l = threadIdx.x >> 6, L = blockDim.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + c;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < n4) {
-    for (int sidx = l; sidx < splits; sidx += 4) {
-      const float4 v = slab[(int64_t)sidx * n4 + i];
+    int s = l;
+    for (; s + 3 * L < splits; s += 4 * L) {
+      const float4 v0 = slab[(int64_t)s * n4 + i];
+      const float4 v1 = slab[(int64_t)(s + L) * n4 + i];
+      const float4 v2 = slab[(int64_t)(s + 2 * L) * n4 + i];
+      const float4 v3 = slab[(int64_t)(s + 3 * L) * n4 + i];
+      a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+      a.x += v1.x; a.y += v1.y; a.z += v1.z; a.w += v1.w;
+      a.x += v2.x; a.y += v2.y; a.z += v2.z; a.w += v2.w;
+      a.x += v3.x; a.y += v3.y; a.z += v3.z; a.w += v3.w;
+    }
+    for (; s < splits; s += L) {
+      const float4 v = slab[(int64_t)s * n4 + i];
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
   }
@@ -300,8 +387,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float4* __restri
   __syncthreads();
   if (l == 0 && i < n4) {
     float4 o = dw[i];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < L; ++k) {
       const float4 v = red[k][c];
       o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
     }
@@ -364,7 +450,9 @@ int wgrad_split_force() { return g_deterministic ? -1 : g_wsplit; }
 // hold slab_ws_floats(splits, n) floats.
 void slab_reduce_launch(float* ws, float* dw, int splits, int64_t n, hipStream_t st) {
   const int64_t n4 = n / 4;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv64(n4, 64)), dim3(256), 0, st,
+  int L = 1;   // split lanes per column: a power of two <= min(16, splits)
+  while (L < 16 && 2 * L <= splits) L *= 2;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)cdiv64(n4, 64)), dim3(64 * L), 0, st,
                      reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(dw), splits, n4);
 }
 
@@ -416,7 +504,7 @@ static int64_t halo_plan(HaloGeom& g) {
             W, MB, WM * WN, KP, halo_occupancy<W, MB, WM, WN, KP>(), halo_cus(), tiles, splits, chunk,
             g.atomic);
   if (g.atomic) return 0;
-  return slab_ws_floats(splits, (int64_t)g.groups * g.cout_g * g.Ktot);
+  return slab_ws_floats(splits, (int64_t)tiles * (64 * MB) * (9 * 64));
 }
 
 template <int W, int MB, int WM, int WN, int KP>
@@ -426,7 +514,26 @@ static void launch_halo(const bf16* x, const bf16* dy, float* dw, float* ws, Hal
   dim3 grid(cdiv(g.cout_g, 64 * MB), g.cin_g / 64, g.splits * g.groups);
   hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP>), grid, dim3(WM * WN * 64), 0, st, x,
                      dy, g.atomic ? dw : ws, g);
-  if (!g.atomic) slab_reduce_launch(ws, dw, g.splits, (int64_t)g.groups * g.cout_g * g.Ktot, st);
+  if (g.atomic) return;
+  constexpr int BM = 64 * MB, BN = 9 * 64;
+  HaloSlabMap mp;
+  mp.BM = BM;
+  mp.BN = BN;
+  mp.WN = WN;
+  mp.WTM = BM / WM;
+  mp.WTN = BN / WN;
+  mp.TM = mp.WTM / 16;
+  mp.TN = mp.WTN / 16;
+  mp.tiles_x = (int)grid.x;
+  mp.tiles_y = (int)grid.y;
+  mp.cout_g = g.cout_g;
+  mp.cin_g = g.cin_g;
+  mp.Ktot = g.Ktot;
+  const int64_t n4 = (int64_t)grid.x * grid.y * g.groups * (BM * BN / 4);
+  int L = 1;   // split lanes per slot: a power of two <= min(16, splits)
+  while (L < 16 && 2 * L <= g.splits) L *= 2;
+  hipLaunchKernelGGL(halo_slab_reduce_kernel, dim3((unsigned)cdiv64(n4, 64)), dim3(64 * L), 0, st,
+                     reinterpret_cast<const float4*>(ws), dw, g.splits, n4, mp);
 }
 
 // One dispatcher for planning (ws == nullptr && plan_only) and launching.

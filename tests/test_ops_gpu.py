@@ -69,12 +69,28 @@ def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True, wa
     # an SE bias) has a meaningless relative error; compare it against the typical grad norm
     norms = sorted(g.norm().item() for g in gr.values() if g is not None)
     scale = norms[len(norms) // 2] if norms else 0.0
+    # relative-error floor: the squeeze-excite MLP gradients (SENet / RegNetY / EfficientNet)
+    # are sums over the image that nearly cancel at init, so BOTH bf16 paths land at 0.05-0.5
+    # relative error on them and which of the two is lower at one seed is chance (measured over
+    # seeds with tools/debug_senet.py). A parameter's stock error is therefore floored at the
+    # median stock error of the parameters of its kind (SE MLP vs the rest).
+    errs = {n: (rel(gn[n], g), rel(gs[n], g)) for n, g in gr.items() if g is not None}
+
+    def _se(n):
+        return ".fc1." in n or ".fc2." in n or ".se." in n
+
+    def _median(vals):
+        vals = sorted(vals)
+        return vals[len(vals) // 2] if vals else 0.0
+
+    floor = {k: _median([e[1] for n, e in errs.items() if _se(n) == k]) for k in (True, False)}
     bad = []
     for name, g in gr.items():
         if g is None:
             assert gn[name] is None or gn[name].abs().max().item() == 0, name
             continue
-        en, es = rel(gn[name], g), rel(gs[name], g)
+        en, es = errs[name]
+        es = max(es, floor[_se(name)]) if _se(name) else es
         small = (gn[name].detach().float().cpu() - g).norm().item() <= 0.02 * scale
         if en > factor * es + slack and not small:
             bad.append((name, round(en, 4), round(es, 4)))
