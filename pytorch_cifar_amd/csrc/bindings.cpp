@@ -88,11 +88,16 @@ bool bn_bwd_apply_acc_launch(const bf16* dout, const uint8_t* mask, const bf16* 
                              float* dgamma2, float* dbeta2, int act, bf16* dy, bf16* dres,
                              const bf16* y2, bf16* dy2, float* zero, int zero_n, float* zero2,
                              int zero2_n, hipStream_t st);
+// stem.hip
+bool stem_wgrad_supported(int N, int H, int W, int Cs, int Ci, int Co);
+int stem_wgrad_slab_rows(int N, int H);
+void stem_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int Co, float* slab, float* out,
+                       hipStream_t st);
 // misc.hip
 void nchw_to_nhwc_launch(const float*, int, int, int, int, bf16*, hipStream_t);
 void nhwc_to_nchw_launch(const bf16*, int, int, int, int, float*, hipStream_t);
 void augment_launch(const uint8_t*, const int64_t*, const int32_t*, int, int, int, int,
-                    const float*, const float*, bf16*, hipStream_t);
+                    const float*, const float*, bf16*, const int64_t*, int64_t*, hipStream_t);
 void gap_fwd_launch(const bf16*, int, int, int, float*, hipStream_t);
 void gap_bwd_launch(const float*, int, int, int, bf16*, hipStream_t);
 bool head_supported(int C, int K);
@@ -867,8 +872,50 @@ Tensor augment(const Tensor& data, const Tensor& idx, const Tensor& rnd, int pad
   float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   float s[3] = {(float)std[0], (float)std[1], (float)std[2]};
   pca::augment_launch(ptr<uint8_t>(data), ptr<int64_t>(idx), ptr<int32_t>(rnd), B, H, W, pad, m, s,
-                      ptr<bf16>(out), cur_stream());
+                      ptr<bf16>(out), nullptr, nullptr, cur_stream());
   return out;
+}
+
+// stem 3x3 conv weight gradient added into `out` (the fp32 gradient, physical [Co][3][3][3]) from
+// the 8-channel padded input x [N,H,W,8] and dy [N,H,W,Co]; False when the shape is not the
+// stem's (the caller then takes the generic padded wgrad)
+bool stem_wgrad(const Tensor& x, const Tensor& dy, int64_t stride, int64_t padding, Tensor out) {
+  if (!(x.is_cuda() && dy.is_cuda() && out.is_cuda() && x.dim() == 4 && dy.dim() == 4 &&
+        out.dim() == 4 && x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 &&
+        out.scalar_type() == at::kFloat && x.is_contiguous() && dy.is_contiguous() &&
+        out.is_contiguous() && stride == 1 && padding == 1))
+    return false;
+  const int N = x.size(0), H = x.size(1), W = x.size(2), Cs = x.size(3), Co = dy.size(3);
+  if (dy.size(0) != N || dy.size(1) != H || dy.size(2) != W) return false;
+  if (out.size(0) != Co || out.size(1) != 3 || out.size(2) != 3) return false;
+  if (!pca::stem_wgrad_supported(N, H, W, Cs, (int)out.size(3), Co)) return false;
+  auto slab = at::empty({pca::stem_wgrad_slab_rows(N, H), Co * 27}, out.options());
+  pca::stem_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), N, H, Co, ptr<float>(slab), ptr<float>(out),
+                         cur_stream());
+  return true;
+}
+
+// packed[b] = sample | word << 32 (word: the augmentation draw, see augment_kernel) ->
+// (NHWC8 bf16 images, int64 targets gathered from labels) in one launch
+std::vector<Tensor> augment_packed(const Tensor& data, const Tensor& labels, const Tensor& packed,
+                                   int pad, std::vector<double> mean, std::vector<double> std) {
+  TORCH_CHECK(data.is_cuda() && data.scalar_type() == at::kByte && data.dim() == 4 &&
+                  data.size(3) == 3 && data.is_contiguous(),
+              "data must be uint8 [N,H,W,3] on GPU");
+  TORCH_CHECK(packed.scalar_type() == at::kLong && packed.is_contiguous() && packed.is_cuda(),
+              "packed must be contiguous int64 on GPU");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() &&
+                  labels.numel() == data.size(0),
+              "labels must be int64 [N]");
+  TORCH_CHECK(mean.size() == 3 && std.size() == 3, "mean/std");
+  const int B = packed.numel(), H = data.size(1), W = data.size(2);
+  auto out = at::empty({B, H, W, 8}, data.options().dtype(at::kBFloat16));
+  auto targets = at::empty({B}, labels.options());
+  float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  float s[3] = {(float)std[0], (float)std[1], (float)std[2]};
+  pca::augment_launch(ptr<uint8_t>(data), ptr<int64_t>(packed), nullptr, B, H, W, pad, m, s,
+                      ptr<bf16>(out), ptr<int64_t>(labels), ptr<int64_t>(targets), cur_stream());
+  return {out, targets};
 }
 
 // fused classifier head: x [N,H,W,C] bf16 -> (logits [N,K] fp32, pooled [N,C] fp32)
@@ -1380,6 +1427,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("nhwc_to_nchw", &nhwc_to_nchw);
   m.def("augment", &augment);
+  m.def("augment_packed", &augment_packed);
+  m.def("stem_wgrad", &stem_wgrad);
   m.def("gap_fwd", &gap_fwd);
   m.def("se_supported", &pca::se_mlp_supported, "fused squeeze-excite path for (C, R)?");
   m.def("se_forward", &se_forward, "squeeze-excite: pool + MLP + sigmoid scale (NHWC bf16)");

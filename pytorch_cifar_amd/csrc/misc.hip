@@ -54,10 +54,13 @@ __global__ void nhwc_to_nchw_kernel(const bf16* __restrict__ y, int N, int C, in
 
 // ----------------------------------------------------------------------------- augment
 // One thread per output pixel: gathers 3 uint8 channels, writes 8 bf16 (16 B, C padded to 8).
+// Packed form (rnd == nullptr): idx[b] = sample | word << 32, drawn once per epoch by the loader,
+// so a training step needs no RNG launches; the thread of pixel 0 also gathers targets[b].
 __global__ void augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx,
                                const int32_t* __restrict__ rnd, int B, int H, int W, int pad,
                                float m0, float m1, float m2, float is0, float is1, float is2,
-                               bf16* __restrict__ out) {
+                               bf16* __restrict__ out, const int64_t* __restrict__ labels,
+                               int64_t* __restrict__ targets) {
   const int total = B * H * W;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int b = i / (H * W);
@@ -65,7 +68,10 @@ __global__ void augment_kernel(const uint8_t* __restrict__ data, const int64_t* 
     const int h = hw / W, w = hw % W;
     // augmentation word k drawn uniformly in [0, span^2 * 2): dy = k % span,
     // dx = (k / span) % span, flip = k / span^2 (span = 2 * pad + 1) -> exactly uniform offsets
-    const int r = rnd[b];
+    const int64_t e = idx[b];
+    const int r = rnd ? rnd[b] : (int)(e >> 32);
+    const int64_t sample = rnd ? e : (e & 0xffffffffll);
+    if (targets && hw == 0) targets[b] = labels[sample];
     const int span = 2 * pad + 1;
     const int dy = r % span;
     const int dx = (r / span) % span;
@@ -78,7 +84,7 @@ __global__ void augment_kernel(const uint8_t* __restrict__ data, const int64_t* 
     // ToTensor/Normalize: (0 - mean) / std.
     float px[3] = {0.f, 0.f, 0.f};
     if (sh >= 0 && sh < H && sw >= 0 && sw < W) {
-      const uint8_t* src = data + (((size_t)idx[b] * H + sh) * W + sw) * 3;
+      const uint8_t* src = data + (((size_t)sample * H + sh) * W + sw) * 3;
       px[0] = src[0] * (1.f / 255.f);
       px[1] = src[1] * (1.f / 255.f);
       px[2] = src[2] * (1.f / 255.f);
@@ -1054,7 +1060,8 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, int G, int Cn, i
 //   pass 1: 64x64 (co, ci) transpose tile number a of one (group, tap), staged through LDS so
 //           both the fp32 reads (along ci) and the bf16 writes (along co) are coalesced;
 //   pass 2: depthwise weight [Cn][T] -> fp32 tap-major copy [T][Cn] (desc wb = the copy) for
-//           output channels [a, b), the layout the depthwise kernels read 8 channels at a time.
+//           output channels [a, b), the layout the depthwise kernels read 8 channels at a time;
+//   pass 3: rows [a, b) of a channel-padded forward copy (desc numel slot = padded width).
 // All index math is 32-bit and per block / per 8 elements (64-bit div/mod per element made the
 // first version of this kernel 10x slower than its bandwidth).
 __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* __restrict__ desc,
@@ -1071,6 +1078,17 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* _
     for (int k = tid; k < nc * T; k += 256) {
       const int co = c0 + k / T, tap = k % T;
       wtf[tap * Cn + co] = w[co * T + tap];
+    }
+    return;
+  }
+  if (ch[3] == 3) {
+    // channel-padded bf16 copy (stem convs on 8-channel padded RGB): rows [r0, r1) of
+    // [Cout*T][Cr] -> [Cout*T][Cp] with zeros in channels Cr..Cp-1 (Cp = desc[7])
+    bf16* wb = reinterpret_cast<bf16*>(d[1]);
+    const int Cp = (int)d[7], r0 = (int)ch[1], nr = (int)ch[2] - r0;
+    for (int k = tid; k < nr * Cp; k += 256) {
+      const int r = r0 + k / Cp, c = k % Cp;
+      wb[r * Cp + c] = f2bf(c < Cr ? w[r * Cr + c] : 0.f);
     }
     return;
   }
@@ -1124,10 +1142,10 @@ void nhwc_to_nchw_launch(const bf16* y, int N, int C, int HW, int Cp, float* x, 
 }
 void augment_launch(const uint8_t* data, const int64_t* idx, const int32_t* rnd, int B, int H,
                     int W, int pad, const float* mean, const float* std, bf16* out,
-                    hipStream_t st) {
+                    const int64_t* labels, int64_t* targets, hipStream_t st) {
   hipLaunchKernelGGL(augment_kernel, dim3(grid_cap((size_t)B * H * W)), dim3(256), 0, st, data, idx,
                      rnd, B, H, W, pad, mean[0], mean[1], mean[2], 1.f / std[0], 1.f / std[1],
-                     1.f / std[2], out);
+                     1.f / std[2], out, labels, targets);
 }
 static bool vec8_ok(int C) { return C % 8 == 0 && C <= 2048; }
 

@@ -1,0 +1,237 @@
+// Stem-conv weight gradient: 3x3, stride 1, pad 1, 3 input channels (RGB padded to 8 in the
+// NHWC input the augmentation kernel writes), 32-wide images — the first conv of every CIFAR
+// zoo model (resnet.py:102, vgg.py:33 first layer, mobilenetv2.py:58, efficientnet.py:136,
+// regnet.py:84, dla.py:91 ...; reference executes it as cuDNN wgrad).
+//
+// As a GEMM it is dW[co][tap*3+ci] = sum_p dy[p][co] * x[p + tap][ci]: M = Cout, N = 27,
+// K = N*H*W pixels (131072 at bs128, 1M at bs1024). The generic split-K wgrad spends most of its
+// time on the 8-wide padded channel dimension and a full-size fp32 output per split; here:
+//   * one workgroup walks 8-row image chunks (256 pixels = 8 MFMA K-steps of 32);
+//   * the dy chunk is staged TRANSPOSED in LDS ([co][pixel], pixel pairs written as dwords so a
+//     wave's stores hit 64 distinct banks), the x chunk as three column-shifted copies
+//     xs[dw][ci][row][col] = x[row-1][col+dw-1][ci] so every B fragment (8 consecutive pixels of
+//     one (tap, ci) column) is one aligned 16-byte LDS read;
+//   * v_mfma_f32_16x16x32_bf16 accumulates Cout x 32 (27 used) per wave over its rows; the four
+//     waves fold through LDS once per workgroup into one fp32 slab row of Cout*27 floats;
+//   * stem_wgrad_reduce_kernel sums the slab rows in a fixed order and ADDS the result into the
+//     fp32 gradient (physical [Cout][3][3][3]) — deterministic, no atomics, no padded copy.
+#include "common.h"
+
+#include <algorithm>
+
+namespace pca {
+namespace {
+constexpr int kSW = 32;            // image width
+constexpr int kSR = 8;             // output rows per chunk
+constexpr int kSP = kSR * kSW;     // pixels per chunk
+constexpr int kSPS = kSP + 8;      // bf16 row pitch of the transposed dy image (528 B: 16-lane
+                                   // ds_read_b128 row reads land 4 banks apart, conflict-free)
+constexpr int kSCI = 3;            // real input channels
+constexpr int kSCS = 8;            // channel pitch of the padded NHWC input
+constexpr int kSGrid = 512;        // workgroups (slab rows)
+}  // namespace
+
+template <int CO>
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const bf16* __restrict__ x,
+                                                         const bf16* __restrict__ dy, int N, int H,
+                                                         float* __restrict__ slab) {
+  constexpr int MT = CO / 16;
+  constexpr int NO = 9 * kSCI;               // outputs per output channel (27)
+  constexpr int NT = (NO + 15) / 16;         // N tiles (2)
+  constexpr int XR = kSR + 2;                // x rows incl. the halo
+  constexpr int DY_BYTES = CO * kSPS * 2;
+  constexpr int RED_BYTES = 4 * CO * NT * 16 * 4;
+  constexpr int U_BYTES = DY_BYTES > RED_BYTES ? DY_BYTES : RED_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[U_BYTES];
+  __shared__ __attribute__((aligned(16))) bf16 xs[3 * kSCI * XR * kSW];
+  bf16* dyT = reinterpret_cast<bf16*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cpi = H / kSR;                   // chunks per image
+  const int chunks = N * cpi;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // B-fragment column of this lane: n = nt*16 + (lane & 15) -> (tap, ci); n >= 27 reads zeros
+  int b_off[NT];
+  bool b_ok[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = nt * 16 + (lane & 15);
+    b_ok[nt] = n < NO;
+    const int tap = b_ok[nt] ? n / kSCI : 0, ci = b_ok[nt] ? n % kSCI : 0;
+    const int dh = tap / 3, dw = tap % 3;
+    b_off[nt] = ((dw * kSCI + ci) * XR + dh) * kSW + 8 * (lane >> 4);
+  }
+
+  // Global loads of the next chunk are issued into registers before the current chunk's MFMAs
+  // (software pipeline: with 2 workgroups per CU the loads would otherwise sit exposed between
+  // the two barriers of every chunk).
+  constexpr int CG = CO / 8;
+  constexpr int DY_IT = (kSP / 2) * CG / 256;             // dy pixel-pair items per thread
+  constexpr int X_ITEMS = 3 * XR * (kSW / 2);
+  constexpr int X_IT = (X_ITEMS + 255) / 256;             // x items per thread
+  static_assert((kSP / 2) * CG % 256 == 0, "dy items");
+  uint4 ra[DY_IT], rb[DY_IT], xa[X_IT], xb[X_IT];
+  auto load = [&](int ck) {
+    const int n = ck / cpi, h0 = (ck - n * cpi) * kSR;
+    const bf16* dyc = dy + (size_t)(n * H + h0) * kSW * CO;
+#pragma unroll
+    for (int i = 0; i < DY_IT; ++i) {
+      const int e = tid + 256 * i;
+      const int pp = e % (kSP / 2), cg = e / (kSP / 2);   // lanes take consecutive pixel pairs
+      ra[i] = *reinterpret_cast<const uint4*>(dyc + (size_t)(2 * pp) * CO + cg * 8);
+      rb[i] = *reinterpret_cast<const uint4*>(dyc + (size_t)(2 * pp + 1) * CO + cg * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < X_IT; ++i) {
+      const int e = tid + 256 * i;
+      const int cp = e % (kSW / 2);
+      const int t = e / (kSW / 2);
+      const int r = t % XR, dw = t / XR;
+      const int hh = h0 - 1 + r;
+      xa[i] = make_uint4(0, 0, 0, 0);
+      xb[i] = make_uint4(0, 0, 0, 0);
+      if (e < X_ITEMS && hh >= 0 && hh < H) {
+        const int s0 = 2 * cp + dw - 1, s1 = s0 + 1;
+        const bf16* row = x + (size_t)(n * H + hh) * kSW * kSCS;
+        if (s0 >= 0) xa[i] = *reinterpret_cast<const uint4*>(row + s0 * kSCS);
+        if (s1 < kSW) xb[i] = *reinterpret_cast<const uint4*>(row + s1 * kSCS);
+      }
+    }
+  };
+  if ((int)blockIdx.x < chunks) load(blockIdx.x);
+
+  for (int ck = blockIdx.x; ck < chunks; ck += gridDim.x) {
+    // dy chunk -> dyT[co][pixel] (pixel pairs as dwords)
+#pragma unroll
+    for (int i = 0; i < DY_IT; ++i) {
+      const int e = tid + 256 * i;
+      const int pp = e % (kSP / 2), cg = e / (kSP / 2);
+      const uint32_t aw[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+      const uint32_t bw[4] = {rb[i].x, rb[i].y, rb[i].z, rb[i].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t lo = (aw[q] & 0xffffu) | (bw[q] << 16);
+        const uint32_t hi = (aw[q] >> 16) | (bw[q] & 0xffff0000u);
+        *reinterpret_cast<uint32_t*>(dyT + (cg * 8 + 2 * q) * kSPS + 2 * pp) = lo;
+        *reinterpret_cast<uint32_t*>(dyT + (cg * 8 + 2 * q + 1) * kSPS + 2 * pp) = hi;
+      }
+    }
+    // x rows h0-1 .. h0+kSR, three column shifts xs[dw][ci][r][c] = x[h0-1+r][c+dw-1][ci]
+#pragma unroll
+    for (int i = 0; i < X_IT; ++i) {
+      const int e = tid + 256 * i;
+      if (e < X_ITEMS) {
+        const int cp = e % (kSW / 2);
+        const int t = e / (kSW / 2);
+        const int r = t % XR, dw = t / XR;
+        const uint32_t aw[2] = {xa[i].x, xa[i].y}, bw[2] = {xb[i].x, xb[i].y};
+#pragma unroll
+        for (int ci = 0; ci < kSCI; ++ci) {
+          const uint32_t av = (ci & 1) ? (aw[ci >> 1] >> 16) : (aw[ci >> 1] & 0xffffu);
+          const uint32_t bv = (ci & 1) ? (bw[ci >> 1] & 0xffff0000u) : (bw[ci >> 1] << 16);
+          *reinterpret_cast<uint32_t*>(xs + ((dw * kSCI + ci) * XR + r) * kSW + 2 * cp) = av | bv;
+        }
+      }
+    }
+    __syncthreads();
+    if (ck + (int)gridDim.x < chunks) load(ck + gridDim.x);
+    // wave wid: chunk rows wid and wid + 4 (one 32-pixel K-step each)
+#pragma unroll
+    for (int r = wid; r < kSR; r += 4) {
+      bf16x8 bfr[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(xs + b_off[nt] + r * kSW);
+        bfr[nt] = b_ok[nt] ? v : bf16x8{};
+      }
+      const int k0 = r * kSW + 8 * (lane >> 4);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(dyT + (mt * 16 + (lane & 15)) * kSPS + k0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[nt], acc[mt][nt], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // fold the four waves, one slab row per workgroup
+  float* red = reinterpret_cast<float*>(smem);   // [4][CO][NT*16]
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = mt * 16 + 4 * (lane >> 4) + j, nn = nt * 16 + (lane & 15);
+        red[(wid * CO + co) * (NT * 16) + nn] = acc[mt][nt][j];
+      }
+  __syncthreads();
+  float* row = slab + (size_t)blockIdx.x * CO * NO;
+  for (int e = tid; e < CO * NO; e += 256) {
+    const int co = e / NO, nn = e - co * NO;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s += red[(w * CO + co) * (NT * 16) + nn];
+    row[e] = s;
+  }
+}
+
+// out[o] += sum_b slab[b][o], b in a fixed order: 8 outputs x 32 partial lanes per workgroup,
+// each lane with 4 independent partial sums (loads in flight instead of one dependent chain).
+__global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ slab,
+                                                                int nb, int total,
+                                                                float* __restrict__ out) {
+  __shared__ float part[32][9];
+  const int c = threadIdx.x & 7, s = threadIdx.x >> 3;
+  const int o = blockIdx.x * 8 + c;
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  if (o < total) {
+    int b = s;
+    for (; b + 96 < nb; b += 128) {
+      v0 += slab[(size_t)b * total + o];
+      v1 += slab[(size_t)(b + 32) * total + o];
+      v2 += slab[(size_t)(b + 64) * total + o];
+      v3 += slab[(size_t)(b + 96) * total + o];
+    }
+    for (; b < nb; b += 32) v0 += slab[(size_t)b * total + o];
+  }
+  part[s][c] = (v0 + v1) + (v2 + v3);
+  __syncthreads();
+  if (threadIdx.x < 8 && o < total) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) t += part[q][c];
+    out[o] += t;
+  }
+}
+
+bool stem_wgrad_supported(int N, int H, int W, int Cs, int Ci, int Co) {
+  return N > 0 && W == kSW && H % kSR == 0 && Cs == kSCS && Ci == kSCI &&
+         (Co == 16 || Co == 32 || Co == 64);
+}
+
+int stem_wgrad_slab_rows(int N, int H) { return std::min(kSGrid, N * (H / kSR)); }
+
+// x [N][H][32][8] bf16, dy [N][H][32][Co] bf16, slab [rows][Co*27] fp32, out [Co][3][3][3] fp32
+void stem_wgrad_launch(const bf16* x, const bf16* dy, int N, int H, int Co, float* slab,
+                       float* out, hipStream_t st) {
+  const int rows = stem_wgrad_slab_rows(N, H);
+  switch (Co) {
+    case 16: hipLaunchKernelGGL(stem_wgrad_kernel<16>, dim3(rows), dim3(256), 0, st, x, dy, N, H, slab); break;
+    case 32: hipLaunchKernelGGL(stem_wgrad_kernel<32>, dim3(rows), dim3(256), 0, st, x, dy, N, H, slab); break;
+    default: hipLaunchKernelGGL(stem_wgrad_kernel<64>, dim3(rows), dim3(256), 0, st, x, dy, N, H, slab); break;
+  }
+  const int total = Co * 9 * kSCI;
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(cdiv(total, 8)), dim3(256), 0, st, slab, rows,
+                     total, out);
+}
+
+}  // namespace pca

@@ -104,10 +104,25 @@ class DeviceLoader:
     def epoch_indices(self) -> torch.Tensor:
         return self.sampler.indices().to(self.device)
 
+    @property
+    def packed(self) -> bool:
+        """GPU loaders hand out packed batch entries ``sample | word << 32``: the epoch's
+        augmentation words are drawn in one launch at epoch start, so a (graph-captured) training
+        step needs no RNG or label-gather launches — one augment kernel makes images + targets."""
+        return self.device.type == "cuda"
+
     def batch_indices(self):
+        """Per-batch device tensors of the epoch (packed entries on GPU, see :attr:`packed`)."""
         idx = self.epoch_indices()
+        if self.packed:
+            idx = idx | (self.random_words(idx.numel()).to(torch.int64) << 32)
         for b in range(len(self)):
             yield idx[b * self.batch_size: (b + 1) * self.batch_size]
+
+    @staticmethod
+    def sample_ids(batch: torch.Tensor) -> torch.Tensor:
+        """Dataset indices of a batch from :meth:`batch_indices` (packed or not)."""
+        return batch & 0xFFFFFFFF
 
     def random_words(self, n: int) -> torch.Tensor:
         """Per-sample augmentation word k (int32), uniform over every (dy, dx, flip) triple:
@@ -117,13 +132,22 @@ class DeviceLoader:
         span = 2 * p + 1
         if not self.train or (p == 0 and not self.flip):
             return torch.full((n,), p + p * span, dtype=torch.int32, device=self.device)
-        # GPU: the default (graph-safe, philox) generator so the draw is captured into hipGraphs
+        # GPU: the default generator (seeded by torch.manual_seed), drawn once per epoch
         gen = None if self.device.type == "cuda" else self.gen
         hi = span * span * (2 if self.flip else 1)
         return torch.randint(0, hi, (n,), generator=gen, device=self.device, dtype=torch.int32)
 
     def make_batch(self, idx: torch.Tensor, rnd: torch.Tensor | None = None):
-        """Gather + augment the samples ``idx`` -> (NCHW-shaped inputs, int64 targets)."""
+        """Gather + augment the samples ``idx`` -> (NCHW-shaped inputs, int64 targets).
+
+        On GPU ``idx`` holds packed entries from :meth:`batch_indices` (unless ``rnd`` is given)."""
+        if self.device.type == "cuda" and rnd is None:
+            out, targets = _native.lib().augment_packed(self.images, self.labels, idx, self.crop_pad,
+                                                        list(self.mean), list(self.std))
+            x = padded_input(out, 3)
+            if self.fp32:
+                x = x.float()
+            return x, targets
         if rnd is None:
             rnd = self.random_words(idx.numel())
         targets = self.labels.index_select(0, idx)

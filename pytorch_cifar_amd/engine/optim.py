@@ -32,6 +32,7 @@ class SGD(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self.grad_scale = grad_scale
         self._lr_dev = {}
+        self._lr_host = {}
         self._tables = {}
         self.capturing = False
 
@@ -39,17 +40,25 @@ class SGD(torch.optim.Optimizer):
     def sync_lr(self):
         """Copy every group's python lr into its device scalar (call outside graph capture)."""
         for i, g in enumerate(self.param_groups):
-            t = self._lr_dev.get(i)
-            if t is not None:
-                t.fill_(float(g["lr"]))
+            self._set_lr(i, g)
+
+    def _set_lr(self, i, group):
+        # the device scalar is rewritten only when the schedule moved (one fill per epoch, not per
+        # step: a captured step's replay otherwise pays a launch for an unchanged value)
+        t = self._lr_dev.get(i)
+        lr = float(group["lr"])
+        if t is not None and self._lr_host.get(i) != lr:
+            t.fill_(lr)
+            self._lr_host[i] = lr
 
     def _lr_tensor(self, i, group, device):
         t = self._lr_dev.get(i)
         if t is None or t.device != device:
             t = torch.full((1,), float(group["lr"]), dtype=torch.float32, device=device)
             self._lr_dev[i] = t
+            self._lr_host[i] = float(group["lr"])
         elif not self.capturing:
-            t.fill_(float(group["lr"]))
+            self._set_lr(i, group)
         return t
 
     def _table(self, i, params, grads, bufs):

@@ -18,7 +18,7 @@ import time
 
 import torch
 
-from ..ops.functional import cross_entropy
+from ..ops.functional import cross_entropy, unit_grad
 from ..utils.profiling import trace_range
 
 
@@ -55,7 +55,7 @@ class TrainStep:
             out = self.net(x)
             loss = cross_entropy(out, y, self.metrics)
         with trace_range("backward"):
-            loss.backward()
+            loss.backward(unit_grad(loss))
             if self.ddp is not None:
                 self.ddp.finish()
         with trace_range("optimizer"):
@@ -117,7 +117,6 @@ class TrainStep:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         self.opt.capturing = True
-        self.loader.graph_safe_rng = True
         try:
             with torch.cuda.graph(g):
                 self.static_loss = self._body(self.static_idx)

@@ -207,7 +207,7 @@ def join_wgrad_streams():
 # pre-hook, into persistent buffers (stable addresses for hipGraph replay). The conversion runs
 # every forward from the current masters, so it can never serve a stale weight.
 _PLAN = {"cur": None}
-_PREP_CHUNK = 4096
+_PREP_CHUNK = int(os.environ.get("PCA_PREP_CHUNK", "4096"))   # fp32 elements per convert block
 
 
 class _PrepEntry:
@@ -233,7 +233,12 @@ class WeightPrepPlan:
         return None
 
     def register(self, w, groups, w_phys):
-        if groups == DW_PREP:
+        if isinstance(groups, tuple):
+            # ("pad", Cp): forward-only bf16 copy with channels zero-padded to Cp (stem convs)
+            co, cg, kh, kw = w.shape
+            wb = torch.empty((co, kh, kw, groups[1]), dtype=COMPUTE_DTYPE, device=w.device)
+            wt = None
+        elif groups == DW_PREP:
             # depthwise: fp32 tap-major copy [KH*KW][Co] (valid for this forward already)
             co = w.shape[0]
             wb = w.detach().reshape(co, -1).t().contiguous()
@@ -252,6 +257,13 @@ class WeightPrepPlan:
             wp = G.physical(e.w)
             Cout, KH, KW, Cg = wp.shape
             n = wp.numel()
+            if isinstance(e.groups, tuple):
+                cp = e.groups[1]
+                rows = Cout * KH * KW
+                desc.append([wp.data_ptr(), e.wb.data_ptr(), 0, 1, Cout, KH * KW, Cg, cp])
+                step = max(1, 2048 // cp)
+                chunks += [[t, r0, min(rows, r0 + step), 3] for r0 in range(0, rows, step)]
+                continue
             if e.groups == DW_PREP:
                 desc.append([wp.data_ptr(), e.wb.data_ptr(), 0, 1, Cout, KH * KW, 1, n])
                 chunks += [[t, c0, min(Cout, c0 + 64), 2] for c0 in range(0, Cout, 64)]
@@ -488,11 +500,21 @@ class _ConvMFMA(torch.autograd.Function):
         w_phys = G.physical(weight)
         if not w_phys.is_contiguous():
             w_phys = w_phys.contiguous()
-        if cin_pad:
-            w_phys = F.pad(w_phys, (0, cin_pad - w_phys.shape[-1]))
         need_dx = ctx.needs_input_grad[0]
         if cin_pad:
-            wb, wt = C.weight_prep(w_phys, groups, need_dx)
+            wb = None
+            plan = _PLAN["cur"]
+            if plan is not None and not need_dx and groups == 1 and weight.is_leaf and \
+                    weight.permute(0, 2, 3, 1).is_contiguous():
+                # zero-padded copy made by the plan's one batched launch (no pad + convert here)
+                key = ("pad", cin_pad)
+                e = plan.lookup(weight, key) or plan.register(weight, key, None)
+                wb, wt = e.wb, None
+                if plan.tables is None:          # first sight of this weight: fill it now
+                    wb.copy_(F.pad(w_phys, (0, cin_pad - w_phys.shape[-1])).to(COMPUTE_DTYPE))
+            if wb is None:
+                w_phys = F.pad(w_phys, (0, cin_pad - w_phys.shape[-1]))
+                wb, wt = C.weight_prep(w_phys, groups, need_dx)
         else:
             wb, wt = _prepped_weight(weight, groups, w_phys, need_dx)
         if acc is not None and want_stats:
@@ -538,7 +560,13 @@ class _ConvMFMA(torch.autograd.Function):
                     dx = None                # delivered through the owner's epilogue
         KH, KW = weight.shape[2], weight.shape[3]
         dw_ret = db_ret = None
-        if weight.requires_grad:
+        if weight.requires_grad and cin_pad and weight.is_leaf and KH == 3 and KW == 3:
+            # stem conv: dedicated small-Cin wgrad adds straight into the fp32 gradient
+            sbuf = G.grad_buffer(weight)
+            if sbuf is not None and C.stem_wgrad(x, dy, stride, padding, sbuf):
+                G.fire(weight)
+                weight = None
+        if weight is not None and weight.requires_grad:
             buf = None if (cin_pad or not weight.is_leaf) else G.grad_buffer(weight)
             side = wgrad_stream(x.device) if buf is not None else None
             if side is not None:
@@ -692,7 +720,11 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
     if groups == 1 and cout_g % 8 == 0 and Cin < 8 * 2 and Cout >= 16:
         # stem conv on 3-channel images: pad channels to 8 and run on MFMA
         cp = _round8(Cin)
-        y, stats = _ConvMFMA.apply(to_nhwc(x, pad_to=cp), weight, bias, stride, padding, groups, want_stats, cp)
+        # (BN partial sums into the accumulator as for every other MFMA conv: no finalize launch)
+        y, stats = _ConvMFMA.apply(to_nhwc(x, pad_to=cp), weight, bias, stride, padding, groups, want_stats, cp,
+                                   None, False, None, acc if want_stats else None)
+        if want_stats and acc is not None:
+            return to_nchw(y), acc
         return to_nchw(y), (stats if want_stats else None)
     if _GROUP_PAD:
         return _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats)
@@ -1314,6 +1346,29 @@ def squeeze_excite(x, w1, b1, w2, b2, act):
 
 
 # ------------------------------------------------------------------------ cross-entropy
+_UNIT = {}
+
+
+def unit_grad(loss: torch.Tensor) -> torch.Tensor:
+    """A persistent ones tensor shaped like ``loss`` for ``loss.backward(unit_grad(loss))``.
+
+    ``loss.backward()`` makes autograd launch a fill for the implicit 1.0 seed, and the CE
+    backward then scales dlogits by it (a second launch). Seeding with this never-written tensor
+    lets the CE backward recognise the unit seed by address and hand dlogits through as they are.
+    """
+    key = (loss.device, loss.dtype, tuple(loss.shape))
+    t = _UNIT.get(key)
+    if t is None:
+        t = torch.ones(loss.shape, dtype=loss.dtype, device=loss.device)
+        _UNIT[key] = t
+    return t
+
+
+def _is_unit(g: torch.Tensor) -> bool:
+    t = _UNIT.get((g.device, g.dtype, tuple(g.shape)))
+    return t is not None and t.data_ptr() == g.data_ptr()
+
+
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, metrics):
@@ -1324,6 +1379,8 @@ class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         (dl,) = ctx.saved_tensors
+        if _is_unit(dloss):
+            return dl, None, None
         return _C().scale_by_scalar(dl, dloss.float().reshape(1).contiguous()), None, None
 
 

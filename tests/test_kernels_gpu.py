@@ -381,6 +381,42 @@ def test_layout_and_augment(C):
     assert rel_err(out[2, ..., :3], ref2) < 1e-2
 
 
+def test_augment_packed_matches_unpacked(C):
+    """Packed batch entries (sample | word << 32) give the images of the (idx, rnd) form and the
+    gathered labels, in one launch."""
+    torch.manual_seed(11)
+    data = torch.randint(0, 256, (9, 32, 32, 3), dtype=torch.uint8, device="cuda")
+    labels = torch.randint(0, 10, (9,), device="cuda")
+    idx = torch.tensor([8, 0, 3, 3, 5], device="cuda")
+    rnd = torch.randint(0, 162, (5,), dtype=torch.int32, device="cuda")
+    mean, std = [0.4914, 0.4822, 0.4465], [0.2023, 0.1994, 0.2010]
+    ref = C.augment(data, idx, rnd, 4, mean, std)
+    packed = idx | (rnd.long() << 32)
+    out, tg = C.augment_packed(data, labels, packed, 4, mean, std)
+    assert torch.equal(out, ref)
+    assert torch.equal(tg, labels[idx])
+
+
+@pytest.mark.parametrize("N,Co", [(2, 64), (5, 32), (3, 16), (130, 64)])
+def test_stem_wgrad_matches_fp32(C, N, Co):
+    """Stem 3x3 wgrad (3 channels padded to 8, stride 1, pad 1) vs torch's fp32 weight gradient
+    of the same bf16 operands; the result is ADDED to the existing gradient."""
+    torch.manual_seed(N * 100 + Co)
+    x = torch.zeros(N, 32, 32, 8, device="cuda", dtype=torch.bfloat16)
+    x[..., :3] = torch.randn(N, 32, 32, 3, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(N, 32, 32, Co, device="cuda").to(torch.bfloat16)
+    base = torch.randn(Co, 3, 3, 3, device="cuda")
+    out = base.clone()
+    assert C.stem_wgrad(x, dy, 1, 1, out)
+    ref = torch.nn.grad.conv2d_weight(nchw(x[..., :3].float()), (Co, 3, 3, 3), nchw(dy.float()),
+                                      stride=1, padding=1)
+    assert rel_err(out - base, nhwc(ref)) < 2e-3
+    # not the stem's shape -> declined (caller falls back)
+    assert not C.stem_wgrad(x, dy, 2, 1, out)
+    assert not C.stem_wgrad(x[:, :16].contiguous(), dy[:, :16].contiguous(), 1, 1,
+                            torch.zeros(Co, 3, 3, 5, device="cuda"))
+
+
 def test_sgd_multi_tensor(C):
     from pytorch_cifar_amd.engine.optim import SGD
 
