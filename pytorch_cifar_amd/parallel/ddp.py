@@ -15,8 +15,14 @@ Re-implements what main_dist.py:140-144 gets from ``torch.nn.parallel.Distribute
   that got no gradient — EfficientNet-B0's unused ``layers.0.conv1`` / ``bn1``, efficientnet.py:
   61-67, 96) are reduced as zeros, which is what ``find_unused_parameters=True`` yields, and
   the compute stream waits for the communication stream before the optimizer runs;
-* ``broadcast_buffers=True`` (DDP default): rank 0's BN running statistics are broadcast before
-  every forward that follows a grad-enabled forward (C4) — one collective per dtype arena;
+* ``broadcast_buffers=True`` (DDP default): rank 0's BN running statistics reach every rank
+  before any forward that follows a grad-enabled forward (C4) — one collective per dtype arena.
+  DDP issues it at the start of that next forward, where it sits on the critical path; nothing
+  touches the buffers between the end of a forward and the next one (backward never does), so
+  with ``overlap_buffer_broadcast`` (default) it is issued right after the grad-enabled forward
+  on the communication stream and runs under the backward (joined with the gradient buckets).
+  Every forward then sees exactly the buffers DDP would give it; only the non-zero ranks' own
+  copies between a step's forward and the next forward differ (they already hold rank 0's);
 * the initial rank-0 parameters and buffers are broadcast at construction (C3).
 
 xGMI is point-to-point (7 links/GPU); RCCL's ring/tree channels stripe a large message over the
@@ -63,7 +69,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, ctx, bucket_cap_mb: float = 25.0,
                  first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  find_unused_parameters: bool = True, arena: ParamArena | None = None,
-                 force_collectives: bool = False):
+                 force_collectives: bool = False, overlap_buffer_broadcast: bool = True):
         super().__init__()
         self.module = module
         self.ctx = ctx
@@ -72,6 +78,7 @@ class DistributedDataParallel(nn.Module):
         # path on a single-GPU box this way; a world-1 RCCL all-reduce is a device copy)
         self._collectives = self.world > 1 or force_collectives
         self.broadcast_buffers = broadcast_buffers
+        self.overlap_buffer_broadcast = overlap_buffer_broadcast
         self.find_unused_parameters = find_unused_parameters
         params = [p for p in module.parameters() if p.requires_grad]
         self.arena = arena if arena is not None else ParamArena(params)
@@ -85,6 +92,7 @@ class DistributedDataParallel(nn.Module):
             self.comm_stream = None
         self._build_buckets(bucket_cap_mb, first_bucket_mb)
         self._require_forward_param_sync = True
+        self._bcast_pending = False
         self._pass_active = False
         self.last_unused = []
         for p in self.arena.params:
@@ -161,17 +169,31 @@ class DistributedDataParallel(nn.Module):
         self._join()
 
     # ------------------------------------------------------------------------ forward
-    def forward(self, *args, **kwargs):
-        if self.broadcast_buffers and self._collectives and self.buffers_arena is not None \
-                and self._require_forward_param_sync:
-            with torch.no_grad():
-                self._fork()
-                with self._stream_ctx():
-                    for t in self.buffers_arena.flat_tensors():
-                        self.comm.broadcast(t, 0, self._sid())
+    def _broadcast_buffers(self, join: bool):
+        with torch.no_grad():
+            self._fork()
+            with self._stream_ctx():
+                for t in self.buffers_arena.flat_tensors():
+                    self.comm.broadcast(t, 0, self._sid())
+            if join:
                 self._join()
+
+    def forward(self, *args, **kwargs):
+        if self._bcast_pending:          # previous grad-enabled forward had no backward
+            self._join()
+            self._bcast_pending = False
+        sync = self.broadcast_buffers and self._collectives and self.buffers_arena is not None
+        if sync and self._require_forward_param_sync:
+            self._broadcast_buffers(join=True)
         out = self.module(*args, **kwargs)
         self._require_forward_param_sync = torch.is_grad_enabled()
+        if sync and self._require_forward_param_sync and self.overlap_buffer_broadcast \
+                and self.comm_stream is not None:
+            # issued now on the communication stream (after this forward's kernels), overlapped
+            # with the backward; the pass-closing join orders it before the optimizer / next step
+            self._broadcast_buffers(join=False)
+            self._require_forward_param_sync = False
+            self._bcast_pending = True
         return out
 
     # ----------------------------------------------------------------------- backward
@@ -215,12 +237,16 @@ class DistributedDataParallel(nn.Module):
                 self._launch(b)
         self.last_unused = unused
         self._join()
+        self._bcast_pending = False
         self._pass_active = False
 
     def finish(self):
         """Explicitly close a pass (no-op if the autograd callback already ran)."""
         if self._pass_active:
             self._finish_pass()
+        elif self._bcast_pending:        # a grad-enabled forward without a backward
+            self._join()
+            self._bcast_pending = False
 
 
 class _Null:
