@@ -48,6 +48,11 @@ CONV_CASES = [
     (2, 32, 8, 32, 3, 2, 1, 4),
     (2, 96, 8, 576, 1, 1, 0, 1),
     (2, 24, 16, 16, 1, 1, 0, 1),
+    # 1x1 with reduction widths not a multiple of 64 (fast path, partial last K-step)
+    (3, 144, 16, 24, 1, 1, 0, 1),
+    (2, 160, 8, 320, 1, 2, 0, 1),
+    (2, 48, 8, 96, 1, 1, 0, 2),
+    (2, 40, 8, 200, 1, 1, 0, 1),
 ]
 
 
