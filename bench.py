@@ -59,14 +59,16 @@ def main():
     step, meta = build_bench_step(args.model, per_rank, device, ctx, graph=bool(args.graph),
                                   baseline=args.baseline, bucket_mb=args.bucket_mb)
 
+    # (CPU runs — the gloo contract test in tests/test_cli_cpu.py — have nothing to synchronize)
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
     for _ in range(args.warmup):
         step()
     ctx.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     ctx.barrier()
     t1 = time.perf_counter()
     dt = torch.tensor([t1 - t0], dtype=torch.float64, device=device)

@@ -114,6 +114,30 @@ def test_main_dist_torchrun_two_ranks_cpu(tmp_path):
     assert os.path.exists(tmp_path / "o" / "ckpt.pth")
 
 
+def test_bench_contract_two_ranks_cpu(tmp_path):
+    """The driver's multi-GPU invocation of bench.py (torchrun, one rank per device, env
+    rendezvous on 127.0.0.1) run with gloo on the CPU: rank 0 alone prints ONE JSON line with
+    the whole-job aggregate, n_gpus = WORLD_SIZE and the global batch split across ranks."""
+    import json
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = _run(["-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(port),
+                os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                "--model", "LeNet", "--batch", "64"], cwd=str(tmp_path))
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 64
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "strong"
+    assert abs(d["value"] - 64 * 1000.0 / d["ms_per_step"]) / d["value"] < 0.02
+
+
 def test_profiling_utils(tmp_path):
     from pytorch_cifar_amd.utils.profiling import StepTimer, range_pop, range_push, torch_profile, trace_range
 
