@@ -1654,6 +1654,13 @@ static int igemm_grid_x(const ConvGeom& g) {
 
 // number of BN-statistics slab rows the forward launch will write (= grid.x)
 // ResNet layer-1 specialisation (conv3x3_c64.hip)
+// stem.hip: 3x3 forward on the 8-channel padded RGB input
+bool conv_stem_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                          int pad, int groups);
+int conv_stem_stat_rows(int N, int H);
+void conv_stem_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, float* stats,
+                          int N, int H, int Cout, hipStream_t st);
+
 bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                          int pad, int groups);
 int conv_c64_stat_rows(int N, int H);
@@ -1667,6 +1674,8 @@ int64_t conv_fwd_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int K
                            int pad, int groups, int Ho, int Wo, bool has_bias) {
   if (g_igemm_override < 0 && !has_bias &&
       conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return 0;
+  if (g_igemm_override < 0 && conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
     return 0;
   ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
                          Cout / groups);
@@ -1749,7 +1758,7 @@ bool conv_needs_tune(int kind, int N, int H, int W, int Cin, int Cout, int KH, i
   if (kind == 0) {
     ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
                            Cout / groups);
-    return tunable(g, c64);
+    return tunable(g, c64 || conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups));
   }
   return tunable(dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo), c64);
 }
@@ -1807,6 +1816,8 @@ int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
                        int groups, int Ho, int Wo) {
   if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
     return conv_c64_stat_rows(N, H);
+  if (g_igemm_override < 0 && conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return conv_stem_stat_rows(N, H);
   ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
                          Cout / groups);
   return igemm_grid_x<0>(g);
@@ -1818,6 +1829,10 @@ void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, f
   if (g_igemm_override < 0 && bias == nullptr &&
       conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
     conv_c64_launch(x, w, y, stats, nullptr, N, H, false, st);
+    return;
+  }
+  if (g_igemm_override < 0 && conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
+    conv_stem_fwd_launch(x, w, bias, y, stats, N, H, Cout, st);
     return;
   }
   ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,

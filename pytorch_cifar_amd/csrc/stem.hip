@@ -18,6 +18,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace pca {
 namespace {
@@ -210,6 +211,168 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __r
 #pragma unroll
     for (int q = 0; q < 32; ++q) t += part[q][c];
     out[o] += t;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Stem forward: y[p][co] = sum_{tap, ci < 8} x[p + tap][ci] * W[co][tap][ci] on the 8-channel
+// padded NHWC input (the batched weight prep pads W's channels with zeros). The generic igemm
+// runs this as K = 72 over two 64-wide K-steps with a per-granule gather. Here:
+//   * a workgroup walks 8-row chunks (256 pixels); the chunk's halo (10 x 34 pixels x 16 B)
+//     is staged once in LDS with zero borders;
+//   * the MFMA K axis is (tap, 8 channels): one K-step of v_mfma_f32_16x16x32_bf16 covers four
+//     taps, so every A fragment is ONE aligned 16-byte LDS read (the lane's pixel shifted by its
+//     tap) and every B fragment one 16-byte weight row; three K-steps cover the nine taps
+//     (slots 9-11 are zero), the weight fragments stay in registers for the whole kernel;
+//   * wave w owns chunk rows 2w, 2w+1 (64 pixels x Cout); the bf16 tile goes out through LDS as
+//     16-byte coalesced row stores; the BatchNorm partial sums (sum, sumsq of the fp32 outputs)
+//     accumulate over all the workgroup's chunks and leave once (stat_out: slab row or sharded
+//     accumulator, like every conv epilogue).
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int kFW2 = kSW + 2;            // halo row pitch (pixels)
+constexpr int kFHP = (kSR + 2) * kFW2;   // halo pixels per chunk (340)
+constexpr int kFGrid = 512;
+}  // namespace
+
+template <int CO>
+__global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ x,
+                                                       const bf16* __restrict__ w,
+                                                       const float* __restrict__ bias,
+                                                       bf16* __restrict__ y, int N, int H,
+                                                       float* __restrict__ stats, int shards) {
+  constexpr int NT = CO / 16;
+  constexpr int CST = CO + 8;                      // staged C row pitch (bf16)
+  __shared__ __attribute__((aligned(16))) bf16 halo[kFHP * kSCS];
+  __shared__ __attribute__((aligned(16))) bf16 ct[kSP * CST];
+  __shared__ float red[4][2][CO];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cpi = H / kSR, chunks = N * cpi;
+
+  // weight fragments: B[k = (tap, ci)][n = co]; lane: co = nt*16 + lane%16, tap = 4*ks + lane/16
+  bf16x8 bw[3][NT];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tap = 4 * ks + (lane >> 4), co = nt * 16 + (lane & 15);
+      bw[ks][nt] = tap < 9 ? *reinterpret_cast<const bf16x8*>(w + ((size_t)co * 9 + tap) * kSCS)
+                           : bf16x8{};
+    }
+  float bb[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) bb[nt] = bias ? bias[nt * 16 + (lane & 15)] : 0.f;
+  // A-fragment tap offsets (halo pixels) of this lane for the three K-steps
+  int toff[3];
+  bool tok[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int tap = 4 * ks + (lane >> 4);
+    tok[ks] = tap < 9;
+    toff[ks] = tok[ks] ? (tap / 3) * kFW2 + tap % 3 : 0;
+  }
+  float st_s[NT], st_q[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) st_s[nt] = st_q[nt] = 0.f;
+
+  for (int ck = blockIdx.x; ck < chunks; ck += gridDim.x) {
+    const int n = ck / cpi, h0 = (ck - n * cpi) * kSR;
+    // halo: rows h0-1 .. h0+8, cols -1 .. 32, zeros outside the image
+    for (int e = tid; e < kFHP; e += 256) {
+      const int r = e / kFW2, c = e - r * kFW2;
+      const int hh = h0 - 1 + r, ww = c - 1;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (hh >= 0 && hh < H && ww >= 0 && ww < kSW)
+        v = *reinterpret_cast<const uint4*>(x + ((size_t)(n * H + hh) * kSW + ww) * kSCS);
+      *reinterpret_cast<uint4*>(halo + e * kSCS) = v;
+    }
+    __syncthreads();
+    f32x4 acc[4][NT];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int p = wid * 64 + mt * 16 + (lane & 15);          // chunk pixel of the A row
+      const int base = (p >> 5) * kFW2 + (p & 31);             // its halo pixel at tap (0, 0)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(halo + (base + toff[ks]) * kSCS);
+        const bf16x8 av = tok[ks] ? a : bf16x8{};
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bw[ks][nt], acc[mt][nt], 0, 0, 0);
+      }
+    }
+    // epilogue: bias, statistics, bf16 tile through LDS
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = acc[mt][nt][j] + bb[nt];
+          st_s[nt] += v;
+          st_q[nt] += v * v;
+          const int p = wid * 64 + mt * 16 + 4 * (lane >> 4) + j;
+          ct[p * CST + nt * 16 + (lane & 15)] = f2bf(v);
+        }
+    __syncthreads();
+    bf16* yc = y + (size_t)(n * H + h0) * kSW * CO;
+    constexpr int CG = CO / 8;
+    for (int e = tid; e < kSP * CG; e += 256) {
+      const int p = e / CG, c8 = e - p * CG;
+      *reinterpret_cast<uint4*>(yc + (size_t)p * CO + c8 * 8) =
+          *reinterpret_cast<const uint4*>(ct + p * CST + c8 * 8);
+    }
+    // (the next chunk's halo writes do not touch ct; its barrier orders these reads before the
+    // next epilogue's ct writes)
+  }
+  if (stats) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      float s1 = st_s[nt], s2 = st_q[nt];
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 16) {
+        red[wid][0][nt * 16 + lane] = s1;
+        red[wid][1][nt * 16 + lane] = s2;
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * CO) {
+      const int k = tid / CO, c = tid - k * CO;
+      const float v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+      stat_out(stats, blockIdx.x, shards, 2 * CO, k * CO + c, v);
+    }
+  }
+}
+
+bool conv_stem_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                          int pad, int groups) {
+  static const bool on = [] {
+    const char* e = getenv("PCA_STEM_FWD");
+    return !(e && e[0] == '0');
+  }();
+  return on && N > 0 && Cin == kSCS && KH == 3 && KW == 3 && stride == 1 && pad == 1 &&
+         groups == 1 && W == kSW && H % kSR == 0 && (Cout == 16 || Cout == 32 || Cout == 64);
+}
+
+int conv_stem_stat_rows(int N, int H) { return std::min(kFGrid, N * (H / kSR)); }
+
+// x [N][H][32][8] bf16, w [Cout][3][3][8] bf16, y [N][H][32][Cout] bf16; stats: slab rows
+// [conv_stem_stat_rows][2][Cout] (shards 0) or the sharded accumulator (stat_shards() > 0)
+void conv_stem_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, float* stats,
+                          int N, int H, int Cout, hipStream_t st) {
+  const int grid = conv_stem_stat_rows(N, H), sh = stat_shards();
+  switch (Cout) {
+    case 16: hipLaunchKernelGGL(stem_fwd_kernel<16>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh); break;
+    case 32: hipLaunchKernelGGL(stem_fwd_kernel<32>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh); break;
+    default: hipLaunchKernelGGL(stem_fwd_kernel<64>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh); break;
   }
 }
 

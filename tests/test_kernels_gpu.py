@@ -41,6 +41,8 @@ CONV_CASES = [
     (2, 64, 32, 128, 3, 2, 1, 1),
     (2, 64, 32, 128, 1, 2, 0, 1),
     (3, 8, 32, 64, 3, 1, 1, 1),
+    (2, 8, 32, 32, 3, 1, 1, 1),     # stem forward kernel (stem.hip), Cout 32 / 16
+    (5, 8, 32, 16, 3, 1, 1, 1),
     (3, 32, 16, 96, 3, 1, 1, 1),
     (2, 128, 8, 256, 3, 1, 1, 1),
     (5, 256, 4, 512, 3, 1, 1, 1),
