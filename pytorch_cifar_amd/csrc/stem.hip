@@ -276,18 +276,33 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) st_s[nt] = st_q[nt] = 0.f;
 
-  for (int ck = blockIdx.x; ck < chunks; ck += gridDim.x) {
+  // halo of a chunk: rows h0-1 .. h0+8, cols -1 .. 32, zeros outside the image; loaded into
+  // registers one chunk ahead (issued before the current chunk's MFMAs and epilogue)
+  constexpr int HI = (kFHP + 255) / 256;
+  uint4 hv[HI];
+  auto load = [&](int ck) {
     const int n = ck / cpi, h0 = (ck - n * cpi) * kSR;
-    // halo: rows h0-1 .. h0+8, cols -1 .. 32, zeros outside the image
-    for (int e = tid; e < kFHP; e += 256) {
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int e = tid + 256 * i;
       const int r = e / kFW2, c = e - r * kFW2;
       const int hh = h0 - 1 + r, ww = c - 1;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (hh >= 0 && hh < H && ww >= 0 && ww < kSW)
-        v = *reinterpret_cast<const uint4*>(x + ((size_t)(n * H + hh) * kSW + ww) * kSCS);
-      *reinterpret_cast<uint4*>(halo + e * kSCS) = v;
+      hv[i] = make_uint4(0, 0, 0, 0);
+      if (e < kFHP && hh >= 0 && hh < H && ww >= 0 && ww < kSW)
+        hv[i] = *reinterpret_cast<const uint4*>(x + ((size_t)(n * H + hh) * kSW + ww) * kSCS);
+    }
+  };
+  if ((int)blockIdx.x < chunks) load(blockIdx.x);
+
+  for (int ck = blockIdx.x; ck < chunks; ck += gridDim.x) {
+    const int n = ck / cpi, h0 = (ck - n * cpi) * kSR;
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int e = tid + 256 * i;
+      if (e < kFHP) *reinterpret_cast<uint4*>(halo + e * kSCS) = hv[i];
     }
     __syncthreads();
+    if (ck + (int)gridDim.x < chunks) load(ck + gridDim.x);
     f32x4 acc[4][NT];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
