@@ -1061,7 +1061,9 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, int G, int Cn, i
 //           both the fp32 reads (along ci) and the bf16 writes (along co) are coalesced;
 //   pass 2: depthwise weight [Cn][T] -> fp32 tap-major copy [T][Cn] (desc wb = the copy) for
 //           output channels [a, b), the layout the depthwise kernels read 8 channels at a time;
-//   pass 3: rows [a, b) of a channel-padded forward copy (desc numel slot = padded width).
+//   pass 3: rows [a, b) of a channel-padded forward copy (desc numel slot = padded width);
+//   pass 4: pass 1 that also writes the forward copy of the tile's elements (one read of the
+//           master feeds both operands; the plan then issues no pass-0 chunks for the weight).
 // All index math is 32-bit and per block / per 8 elements (64-bit div/mod per element made the
 // first version of this kernel 10x slower than its bandwidth).
 __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* __restrict__ desc,
@@ -1104,6 +1106,7 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* _
     return;
   }
   bf16* wt = reinterpret_cast<bf16*>(d[2]);
+  bf16* wbt = ch[3] == 4 ? reinterpret_cast<bf16*>(d[1]) : nullptr;   // pass 4: + forward copy
   const int nco = (Cn + 63) >> 6, nci = (Cr + 63) >> 6;
   int q = (int)ch[1];
   const int ci_t = q % nci;
@@ -1119,6 +1122,31 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* _
     tile[r][c] = (co < Cn && ci < Cr) ? w[((g * Cn + co) * T + tap) * Cr + ci] : 0.f;
   }
   __syncthreads();
+  if (wbt) {   // forward copy of the tile: 8 consecutive ci per thread, 16-byte stores
+    for (int k = tid; k < 64 * 8; k += 256) {
+      const int r = k >> 3, c8 = (k & 7) * 8;
+      const int co = co0 + r, ci = ci0 + c8;
+      if (co < Cn && ci < Cr) {
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = tile[r][c8 + j];
+        *reinterpret_cast<uint4*>(wbt + ((g * Cn + co) * T + tap) * Cr + ci) = pack8(f);
+      }
+    }
+  }
+  if (Cn % 8 == 0) {   // transposed copy: 8 consecutive co per thread, 16-byte stores
+    for (int k = tid; k < 64 * 8; k += 256) {
+      const int r = k >> 3, c8 = (k & 7) * 8;       // r: ci, c8: first co (contiguous in wt)
+      const int ci = ci0 + r, co = co0 + c8;
+      if (ci < Cr && co < Cn) {
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = tile[c8 + j][r];
+        *reinterpret_cast<uint4*>(wt + ((g * Cr + ci) * T + tap) * Cn + co) = pack8(f);
+      }
+    }
+    return;
+  }
   for (int k = tid; k < 64 * 64; k += 256) {
     const int r = k >> 6, c = k & 63;               // r: ci, c: co (contiguous in wt)
     const int ci = ci0 + r, co = co0 + c;

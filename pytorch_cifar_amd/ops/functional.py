@@ -270,10 +270,11 @@ class WeightPrepPlan:
                 continue
             desc.append([wp.data_ptr(), e.wb.data_ptr(), e.wt.data_ptr(), e.groups,
                          Cout // e.groups, KH * KW, Cg, n])
-            chunks += [[t, s0, min(n, s0 + _PREP_CHUNK), 0] for s0 in range(0, n, _PREP_CHUNK)]
             cn, cr = Cout // e.groups, Cg
             tiles = e.groups * KH * KW * ((cn + 63) // 64) * ((cr + 63) // 64)
-            chunks += [[t, k, 0, 1] for k in range(tiles)]
+            # pass 4: each transpose tile also writes its elements' forward copy (one read of
+            # the fp32 master for both bf16 operands)
+            chunks += [[t, k, 0, 4] for k in range(tiles)]
         dev = self.entries[0].wb.device
         self.tables = (torch.tensor(desc, dtype=torch.int64).to(dev),
                        torch.tensor(chunks, dtype=torch.int64).to(dev),
