@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const bf16* __restrict_
 #pragma unroll
     for (int i = 0; i < DY_IT; ++i) {
       const int e = tid + 256 * i;
-      const int pp = e % (kSP / 2), cg = e / (kSP / 2);   // lanes take consecutive pixel pairs
+      const int cg = e % CG, pp = e / CG;   // CG lanes read one pixel's channels: coalesced
       ra[i] = *reinterpret_cast<const uint4*>(dyc + (size_t)(2 * pp) * CO + cg * 8);
       rb[i] = *reinterpret_cast<const uint4*>(dyc + (size_t)(2 * pp + 1) * CO + cg * 8);
     }
@@ -108,19 +108,23 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const bf16* __restrict_
   if ((int)blockIdx.x < chunks) load(blockIdx.x);
 
   for (int ck = blockIdx.x; ck < chunks; ck += gridDim.x) {
-    // dy chunk -> dyT[co][pixel] (pixel pairs as dwords)
+    // dy chunk -> dyT[co][pixel] (pixel pairs as dwords). The 16-byte chunk (8 pixels) of row co
+    // sits at chunk index (pixel / 8) ^ ((co / 8) & 7): the CG lanes of one pixel pair write 8
+    // rows 8 apart, which the swizzle spreads over distinct banks (a plain pitch cannot also keep
+    // the 16-row fragment reads conflict-free)
 #pragma unroll
     for (int i = 0; i < DY_IT; ++i) {
       const int e = tid + 256 * i;
-      const int pp = e % (kSP / 2), cg = e / (kSP / 2);
+      const int cg = e % CG, pp = e / CG;
+      const int col = ((((pp >> 2) ^ (cg & 7)) << 2) | (pp & 3)) * 2;   // swizzled pixel index
       const uint32_t aw[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
       const uint32_t bw[4] = {rb[i].x, rb[i].y, rb[i].z, rb[i].w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t lo = (aw[q] & 0xffffu) | (bw[q] << 16);
         const uint32_t hi = (aw[q] >> 16) | (bw[q] & 0xffff0000u);
-        *reinterpret_cast<uint32_t*>(dyT + (cg * 8 + 2 * q) * kSPS + 2 * pp) = lo;
-        *reinterpret_cast<uint32_t*>(dyT + (cg * 8 + 2 * q + 1) * kSPS + 2 * pp) = hi;
+        *reinterpret_cast<uint32_t*>(dyT + (cg * 8 + 2 * q) * kSPS + col) = lo;
+        *reinterpret_cast<uint32_t*>(dyT + (cg * 8 + 2 * q + 1) * kSPS + col) = hi;
       }
     }
     // x rows h0-1 .. h0+kSR, three column shifts xs[dw][ci][r][c] = x[h0-1+r][c+dw-1][ci]
@@ -151,10 +155,12 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const bf16* __restrict_
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(xs + b_off[nt] + r * kSW);
         bfr[nt] = b_ok[nt] ? v : bf16x8{};
       }
-      const int k0 = r * kSW + 8 * (lane >> 4);
+      const int kc = r * (kSW / 8) + (lane >> 4);   // 8-pixel chunk of this lane's K slice
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(dyT + (mt * 16 + (lane & 15)) * kSPS + k0);
+        const int co = mt * 16 + (lane & 15);
+        const bf16x8 a =
+            *reinterpret_cast<const bf16x8*>(dyT + co * kSPS + ((kc ^ ((co >> 3) & 7)) << 3));
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[nt], acc[mt][nt], 0, 0, 0);
