@@ -1315,12 +1315,19 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     }
   }
   if (jq == 0 && db && nl == 1) {       // one wave: db[k] += sum_n dl[n][k]
-    for (int k = 0; k < K; ++k) {
-      float t = 0.f;
-      for (int n = cl; n < N; n += 64) t += dl[(size_t)n * K + k];
-      t = wave_sum(t);
-      if (cl == 0) db[k] += t;
-    }
+    // all classes per sample at once (clamped loads, zero weight past K) and independent wave
+    // reductions: a per-class loop of load chains + reductions was the kernel's critical path
+    float t[kHeadMaxK];
+#pragma unroll
+    for (int k = 0; k < kHeadMaxK; ++k) t[k] = 0.f;
+#pragma unroll 2
+    for (int n = cl; n < N; n += 64)
+#pragma unroll
+      for (int k = 0; k < kHeadMaxK; ++k) t[k] += dl[(size_t)n * K + min(k, K - 1)];
+#pragma unroll
+    for (int k = 0; k < kHeadMaxK; ++k) t[k] = wave_sum(t[k]);
+    if (cl == 0)
+      for (int k = 0; k < K; ++k) db[k] += t[k];
   }
 }
 
