@@ -16,7 +16,7 @@ def main():
             for r in csv.DictReader(open(f)):
                 vals[r["Kernel_Name"][:90]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in vals.items():
-        if "conv" not in k and "wgrad" not in k:
+        if "conv" not in k and "wgrad" not in k and "stem" not in k:
             continue
         print(k)
         for c, v in sorted(cs.items()):
