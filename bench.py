@@ -11,6 +11,10 @@ The global batch is fixed at 1024 and split across ranks (main_dist.py:111: batc
 scaling is "strong". Prints exactly one JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--model ResNet18] [--batch 1024]
+
+--gpus N > 1 works both under torchrun (the driver's form) and stand-alone: without a WORLD_SIZE
+in the environment bench.py starts the N rank processes itself (parallel/launcher.py
+spawn_local_ranks, one fresh interpreter per GPU with the torchrun env on 127.0.0.1).
 """
 from __future__ import annotations
 
@@ -47,10 +51,20 @@ def main():
     args = parse()
     from pytorch_cifar_amd.parallel import launcher
 
+    if args.gpus > 1 and launcher.spawned_world() == 0:
+        # `python bench.py --gpus N` without torchrun: start the N rank processes ourselves (the
+        # reference's main_dist.py:51-60 mp.spawn), before anything here touches the GPU; rank 0
+        # of the children prints the JSON line.
+        ngpu = torch.cuda.device_count()      # counts devices without initialising HIP
+        if 0 < ngpu < args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but only {ngpu} GPU(s) visible")
+        sys.exit(launcher.spawn_local_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+
     ctx = launcher.init_from_env(backend="nccl")
     rank, world = ctx.rank, ctx.world
     if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        # n_gpus / parallelism below report the ranks actually timed (WORLD_SIZE)
+        print(f"bench.py: warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     device = ctx.device
     per_rank = args.batch // world
 

@@ -21,7 +21,9 @@ from pytorch_cifar_amd.engine.arena import ParamArena
 from pytorch_cifar_amd.engine.checkpoint import load_checkpoint, save_checkpoint
 from pytorch_cifar_amd.engine.optim import SGD
 from pytorch_cifar_amd.engine.trainer import Trainer
+from pytorch_cifar_amd.parallel import launcher
 from pytorch_cifar_amd.parallel.data_parallel import DataParallel
+from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
 from pytorch_cifar_amd.parallel.launcher import DistContext
 from utils import progress_bar
 
@@ -50,6 +52,10 @@ parser.add_argument('--profile', default=None, metavar='TRACE.json',
                     help='torch.profiler Chrome trace of the first training steps')
 parser.add_argument('--no_nan_guard', action='store_true', help='do not stop on a non-finite loss')
 parser.add_argument('--t_max', default=200, type=int, help='cosine schedule length (reference: 200)')
+parser.add_argument('--nproc', default=None, type=int,
+                    help='data-parallel ranks (default: every visible GPU, one process each; '
+                         'the reference main.py:74 DataParallel used all GPUs too)')
+parser.add_argument('--bucket_mb', default=4.0, type=float, help='gradient all-reduce bucket size (MiB)')
 
 
 
@@ -70,61 +76,100 @@ def _apply_runtime_flags(args, loaders):
         for ld in loaders:
             ld.fp32 = True
 
+def _data_parallel_ranks(args):
+    if args.nproc:
+        return args.nproc
+    if args.cpu or not torch.cuda.is_available():
+        return 1
+    return torch.cuda.device_count()
+
+
 def main(argv=None):
     args = parser.parse_args(argv)
-    device = 'cuda' if torch.cuda.is_available() and not args.cpu else 'cpu'
+    nranks = _data_parallel_ranks(args)
+    if nranks > 1 and launcher.spawned_world() == 0:
+        # Reference main.py:73-74 wraps the net in nn.DataParallel over every visible GPU. Here each
+        # GPU gets its own rank process (started fresh, the parent never touches the GPU) running
+        # the native RCCL bucket engine; the batch is split across ranks like DataParallel's
+        # scatter, and rank 0 writes the same module.-prefixed checkpoint.
+        argv = list(sys.argv[1:] if argv is None else argv)
+        rc = launcher.spawn_local_ranks(nranks, [os.path.abspath(__file__)] + argv)
+        if rc:
+            raise SystemExit(rc)
+        return 0.0
+    if launcher.spawned_world() > 1:
+        ctx = launcher.init_from_env(backend='gloo' if args.cpu else 'nccl')
+    else:
+        dev = torch.device('cuda', 0) if torch.cuda.is_available() and not args.cpu else torch.device('cpu')
+        if dev.type == 'cuda':
+            torch.cuda.set_device(dev)
+        ctx = DistContext(device=dev)
+    device = ctx.device
+    is_main = ctx.rank == 0
     torch.manual_seed(args.seed)
     best_acc = 0  # best test accuracy
     start_epoch = 0  # start from epoch 0 or last checkpoint epoch
 
-    print('==> Preparing data..')
-    trainloader, testloader = build_loaders(args.data_dir, args.synthetic, args.batch_size,
-                                            args.test_batch_size, device, seed=args.seed,
-                                            synthetic_size=args.synthetic_size,
+    say = print if is_main else (lambda *a, **k: None)
+    say('==> Preparing data..')
+    batch_size = max(1, args.batch_size // ctx.world)
+    test_batch_size = max(1, args.test_batch_size // ctx.world)
+    trainloader, testloader = build_loaders(args.data_dir, args.synthetic, batch_size,
+                                            test_batch_size, device, world=ctx.world, rank=ctx.rank,
+                                            seed=args.seed, synthetic_size=args.synthetic_size,
                                             test_synthetic_size=(args.synthetic_size // 5 if args.synthetic_size else None))
     _apply_runtime_flags(args, (trainloader, testloader))
 
-    print('==> Building model..')
+    say('==> Building model..')
     model = models.build_model(args.model).to(device)
     net = model
     arena = None
-    if device == 'cuda':
+    ddp = None
+    if ctx.world > 1:
         arena = ParamArena(model.parameters())
-        net = DataParallel(model)
+        ddp = net = DistributedDataParallel(model, ctx, bucket_cap_mb=args.bucket_mb, arena=arena)
+    elif device.type == 'cuda':
+        arena = ParamArena(model.parameters())
+        net = DataParallel(model, device_ids=[device.index])
 
     ckpt_path = os.path.join(args.checkpoint_dir, 'ckpt.pth')
     optimizer = SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-4)
-    if arena is not None and len(getattr(net, 'device_ids', [])) <= 1:
+    if arena is not None:
         optimizer.attach_arena(arena)
     scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=args.t_max)
     if args.resume:
-        print('==> Resuming from checkpoint..')
+        say('==> Resuming from checkpoint..')
         assert os.path.isdir(args.checkpoint_dir), 'Error: no checkpoint directory found!'
         best_acc, start_epoch = load_checkpoint(ckpt_path, net, optimizer, scheduler, map_location=device)
         start_epoch += 1
 
-    trainer = Trainer(net, optimizer, trainloader, testloader, DistContext(device=torch.device(device)),
-                      graph=bool(args.graph) and device == 'cuda', log_every=args.log_every,
-                      progress=progress_bar, max_steps=args.max_steps, nan_guard=not args.no_nan_guard)
-    if args.profile:
+    trainer = Trainer(net, optimizer, trainloader, testloader, ctx, ddp=ddp,
+                      graph=bool(args.graph) and device.type == 'cuda', log_every=args.log_every,
+                      progress=progress_bar if is_main else None, max_steps=args.max_steps,
+                      nan_guard=not args.no_nan_guard, is_main=is_main)
+    prof_cm = None
+    if args.profile and is_main:
         from pytorch_cifar_amd.utils.profiling import torch_profile
         prof_cm = torch_profile(args.profile)
         trainer.profiler = prof_cm.__enter__()
 
     for epoch in range(start_epoch, start_epoch + args.epochs):
-        print('\nEpoch: %d' % epoch)
+        say('\nEpoch: %d' % epoch)
         trainer.train_epoch(epoch)
         _, acc, _, _ = trainer.test_epoch(epoch)
         if trainer.images_per_sec:
-            print('Throughput: %.1f img/s' % trainer.images_per_sec)
+            say('Throughput: %.1f img/s' % trainer.images_per_sec)
         if acc > best_acc:
-            print('Saving..')
-            save_checkpoint(ckpt_path, net, acc, epoch, optimizer, scheduler)
+            say('Saving..')
+            if is_main:
+                save_checkpoint(ckpt_path, net, acc, epoch, optimizer, scheduler)
             best_acc = acc
         scheduler.step()
-    if args.profile:
+    if prof_cm is not None:
         prof_cm.__exit__(None, None, None)
         print('Profile trace written to %s' % args.profile)
+    ctx.barrier()
+    ctx.shutdown()
     return best_acc
 
 

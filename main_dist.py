@@ -11,7 +11,8 @@ Launch modes:
   python main_dist.py --dist ...                    spawns one process per visible GPU
                                                     (nodes = --world_size, node rank = --rank;
                                                     both default to 1/0 instead of -1)
-  python main_dist.py ...                           single process (reference: DataParallel)
+  python main_dist.py ...                           one rank per visible GPU, spawned here
+                                                    (reference: single-process DataParallel)
 
 Per-rank batch = batch_size / world_size (main_dist.py:111). Gradients are averaged with bucketed
 RCCL all-reduces overlapped with backward; BN buffers follow DDP's broadcast_buffers semantics;
@@ -64,6 +65,8 @@ parser.add_argument('--bucket_mb', default=4.0, type=float,
 parser.add_argument('--log_every', default=20, type=int)
 parser.add_argument('--no_broadcast_buffers', action='store_true')
 parser.add_argument('--cpu', action='store_true', help='gloo/CPU ranks (tests)')
+parser.add_argument('--nproc', default=None, type=int,
+                    help='ranks for the non---dist path (default: every visible GPU, one process each)')
 parser.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'],
                     help='bf16: native MI355X kernels; fp32: stock PyTorch fp32 kernels on the GPU')
 parser.add_argument('--deterministic', action='store_true', help='bitwise-reproducible weight gradients')
@@ -96,7 +99,7 @@ def _apply_runtime_flags(args, loaders):
 
 def main(argv=None):
     args = parser.parse_args(argv)
-    if 'WORLD_SIZE' in os.environ and int(os.environ['WORLD_SIZE']) > 1 and not args.dist:
+    if launcher.spawned_world() > 1 and not args.dist:
         ctx = launcher.init_from_env(backend='gloo' if args.cpu else 'nccl')
         return main_worker(ctx, args)
     if args.dist:
@@ -106,6 +109,16 @@ def main(argv=None):
         args.node_rank = args.rank if args.rank >= 0 else 0
         mp.spawn(_spawn_entry, nprocs=ngpus, args=(ngpus, args))
         return 0
+    nranks = args.nproc if args.nproc else (0 if args.cpu else torch.cuda.device_count())
+    if nranks > 1:
+        # reference non---dist path (README / train.sh): nn.DataParallel over every visible GPU
+        # (main_dist.py:145-147) with the global batch split across them. Here: one rank process
+        # per GPU on the native RCCL bucket engine, started fresh (never an exec of this process).
+        argv = list(sys.argv[1:] if argv is None else argv)
+        rc = launcher.spawn_local_ranks(nranks, [os.path.abspath(__file__)] + argv)
+        if rc:
+            raise SystemExit(rc)
+        return 0.0
     ctx = launcher.DistContext(device=torch.device('cuda' if torch.cuda.is_available() and not args.cpu else 'cpu'))
     if ctx.device.type == 'cuda':
         torch.cuda.set_device(0)

@@ -86,15 +86,26 @@ def digest_path() -> str:
     return ext_path() + ".srchash"
 
 
-def is_stale() -> bool:
-    """True when the in-tree .so is missing or was built from different csrc contents."""
+def is_stale():
+    """True when the in-tree .so is missing or was built from different csrc contents, False when
+    its recorded digest matches, None when unknown (the .so exists but its git-ignored ``.srchash``
+    does not, e.g. a fresh checkout next to a shipped .so): the loader then compares the digest the
+    .so carries itself (``_C.src_digest()``) after import."""
     if not os.path.exists(ext_path()):
         return True
     try:
         with open(digest_path()) as fh:
             return fh.read().strip() != source_digest()
     except OSError:
-        return True
+        return None
+
+
+def _digest_object(flags, verbose):
+    """A one-symbol object carrying the source digest, linked into the .so (see is_stale)."""
+    src = os.path.join(OBJ_DIR, "srcdigest.cpp")
+    with open(src, "w") as fh:
+        fh.write('extern "C" const char pca_src_digest[] = "%s";\n' % source_digest())
+    return _compile(src, src + ".o", flags, verbose)
 
 
 def _headers():
@@ -142,6 +153,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
             futs = [ex.submit(_compile, s, o, flags, verbose) for s, o in todo]
             for f in futs:
                 f.result()
+    objs.append(_digest_object(flags, verbose))
     out = ext_path()
     if todo or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out,
@@ -165,7 +177,7 @@ def build_locked(**kw) -> str:
     with open(os.path.join(os.path.dirname(OBJ_DIR), ".build.lock"), "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
         try:
-            if not is_stale() and not kw.get("force"):
+            if is_stale() is False and not kw.get("force"):
                 return ext_path()
             return build(**kw)
         finally:

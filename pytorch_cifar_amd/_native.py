@@ -64,10 +64,17 @@ def lib():
         return _wrap(_lib)
     from . import _build
 
-    if _build.is_stale():
+    # torch first: its libamdhip64 / librccl (SONAME .so.7 / .so.1) then satisfy _C's NEEDED
+    # entries. Loading _C first pulls /opt/rocm's copies in as well — two HIP runtimes and two
+    # RCCLs in one process, whose exit-time destructors corrupt the heap.
+    import torch  # noqa: F401
+
+    stale = _build.is_stale()
+    no_build = os.environ.get("PCA_NO_AUTOBUILD", "0") == "1"
+    if stale or (stale is None and not no_build):
         # the .so is missing or was built from other csrc contents: never run a stale kernel
         # library silently (a stale .so ships with the tree to the GPU box)
-        if os.environ.get("PCA_NO_AUTOBUILD", "0") == "1":
+        if no_build:
             raise RuntimeError(
                 "pytorch_cifar_amd native extension is missing or stale (csrc changed since it was "
                 "built); run `python -m pytorch_cifar_amd._build`")
@@ -75,6 +82,17 @@ def lib():
     try:
         from . import _C  # noqa: F401
 
+        if stale is None and no_build:
+            # no recorded digest next to the .so: trust the one it carries
+            want = _build.source_digest()
+            have = _C.src_digest() if hasattr(_C, "src_digest") else None
+            if have != want:
+                raise RuntimeError(
+                    "pytorch_cifar_amd native extension was built from other sources "
+                    f"(digest {have} != {want}); run `python -m pytorch_cifar_amd._build`")
+            import warnings
+
+            warnings.warn("pytorch_cifar_amd: .srchash missing; the .so's embedded source digest matches")
         _lib = _C
         return _wrap(_lib)
     except ImportError as e:  # not built yet

@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <vector>
 
+extern "C" const char pca_src_digest[];  // build/srcdigest.cpp, written by _build.py
+
 typedef __bf16 bf16;
 
 namespace pca {
@@ -1389,6 +1391,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
   m.def("conv_autotune_enabled", []() { return g_autotune; });
+  m.def("src_digest", []() { return std::string(pca_src_digest); },
+        "sha256 of the csrc sources this library was built from (_build.source_digest)");
   m.def("conv_trial", [](int kind, int cfg, int split) {
     if (kind == 0) pca::conv_set_trial(cfg, split);
     else pca::wgrad_set_trial(cfg, split);

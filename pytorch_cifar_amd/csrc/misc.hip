@@ -530,7 +530,18 @@ __global__ __launch_bounds__(1024) void ce_fused_kernel(const float* __restrict_
   const float invN = 1.f / N;
   for (int n = threadIdx.x; n < N; n += blockDim.x) {
     const float* row = logits + (size_t)n * K;
-    const int t = (int)tgt[n];
+    const int64_t t64 = tgt[n];
+    // a label outside [0, K) poisons this sample's loss and gradient with NaN (the trainer's
+    // non-finite-loss guard then stops the run, as F.cross_entropy would raise) instead of
+    // silently training on a wrong logit or reading past the row
+    const bool bad = t64 < 0 || t64 >= K;
+    const int t = bad ? 0 : (int)t64;
+    if (bad) {
+      lsum += __builtin_nanf("");
+      if (dlogits)
+        for (int k = 0; k < K; ++k) dlogits[(size_t)n * K + k] = __builtin_nanf("");
+      continue;
+    }
     if (K <= kCeRegK) {
       float v[kCeRegK];
 #pragma unroll

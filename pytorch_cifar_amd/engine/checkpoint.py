@@ -26,12 +26,19 @@ def _unwrap_keys(sd, want_prefix: bool):
     return sd
 
 
-def save_checkpoint(path, net, acc, epoch, optimizer=None, scheduler=None, extra=None):
+def save_checkpoint(path, net, acc, epoch, optimizer=None, scheduler=None, extra=None,
+                    scheduler_stepped=False):
+    """``scheduler_stepped``: whether ``scheduler.step()`` already ran for ``epoch`` when this was
+    saved (main.py / main_dist.py save inside the epoch, before stepping: False). Recorded in the
+    payload so a resume advances the schedule only when the saved state is one step behind."""
+    if hasattr(net, "finish"):
+        net.finish()       # DDP: join a buffer broadcast still in flight on the comm stream
     state = {"net": net.state_dict(), "acc": float(acc), "epoch": int(epoch)}
     if optimizer is not None:
         state["optimizer"] = optimizer.state_dict()
     if scheduler is not None:
         state["scheduler"] = scheduler.state_dict()
+        state["scheduler_stepped"] = bool(scheduler_stepped)
     if extra:
         state.update(extra)
     d = os.path.dirname(os.path.abspath(path))
@@ -52,9 +59,11 @@ def load_checkpoint(path, net, optimizer=None, scheduler=None, map_location="cpu
         optimizer.load_state_dict(ck["optimizer"])
     if scheduler is not None and "scheduler" in ck:
         scheduler.load_state_dict(ck["scheduler"])
-        # The entry points checkpoint inside epoch e, before that epoch's scheduler.step(); the
-        # resumed run starts at e + 1, so advance the schedule once to train e + 1 at lr(e + 1).
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore")   # "scheduler.step() before optimizer.step()"
-            scheduler.step()
+        # A resumed run starts at epoch e + 1. A checkpoint taken inside epoch e before that
+        # epoch's scheduler.step() (the entry points' order) is one step behind: advance it once
+        # so e + 1 trains at lr(e + 1). One saved after stepping is already there.
+        if not ck.get("scheduler_stepped", False):
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")   # "scheduler.step() before optimizer.step()"
+                scheduler.step()
     return float(ck.get("acc", 0.0)), int(ck.get("epoch", 0))

@@ -89,26 +89,39 @@ class TrainStep:
     def _capture(self):
         # The warm-up bodies below are real steps (SGD update, BN running stats, metrics). Snapshot
         # the state first and roll it back before capture, so the first captured replay is the
-        # first step this batch takes (N graph steps == N eager steps).
+        # first step this batch takes (N graph steps == N eager steps). Any failure on the way
+        # (a warm-up raising, capture unsupported) restores the snapshot and the optimizer's
+        # first-step flag before the caller falls back to eager, so the eager step that follows
+        # sees exactly the state it would have seen without the attempt.
         state = self._state_tensors()
         snap = [t.clone() for t in state]
         first = getattr(self.opt, "_arena_first", None)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(3):
-                self._body(self.static_idx)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        with torch.no_grad():
-            for t, v in zip(state, snap):
-                t.copy_(v)
-            known = {id(t) for t in state}
-            for st in self.opt.state.values():   # momenta created by the warm-ups start at zero
-                b = st.get("momentum_buffer")
-                if b is not None and id(b) not in known and getattr(self.opt, "arena", None) is None:
-                    b.zero_()
-        del snap
+        known = {id(t) for t in state}
+
+        def restore():
+            torch.cuda.synchronize()
+            with torch.no_grad():
+                for t, v in zip(state, snap):
+                    t.copy_(v)
+                for st in self.opt.state.values():   # momenta created by the warm-ups start at zero
+                    b = st.get("momentum_buffer")
+                    if b is not None and id(b) not in known and getattr(self.opt, "arena", None) is None:
+                        b.zero_()
+            if first is not None:
+                self.opt._arena_first = first
+
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    self._body(self.static_idx)
+            torch.cuda.current_stream().wait_stream(s)
+        except BaseException:
+            torch.cuda.current_stream().wait_stream(s)
+            restore()
+            raise
+        restore()
         # If this is the run's first step, the restored momenta are zero and the captured
         # steady-state rule buf = 0.9 * buf + d equals the first-step rule buf = d (dampening 0),
         # so the graph is exact from its first replay; keep recording the steady-state rule.
@@ -120,8 +133,15 @@ class TrainStep:
         try:
             with torch.cuda.graph(g):
                 self.static_loss = self._body(self.static_idx)
+        except BaseException:
+            self.opt.capturing = False
+            restore()
+            raise
         finally:
             self.opt.capturing = False
+        # (the captured step recorded the steady-state rule and left _arena_first False: the replay
+        # that follows is the first real step, exact on the restored zero momenta as noted above)
+        del snap
         self.graph = g
 
     def __call__(self, idx: torch.Tensor):

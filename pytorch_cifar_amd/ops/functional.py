@@ -1396,6 +1396,14 @@ def cross_entropy(logits, target, metrics=None):
                 metrics[2] += target.numel()
         return loss
     logits = logits.float().contiguous()
+    from .. import _native
+
+    if _native._debug:   # --debug_sync: name a bad label on the host (the kernel NaN-poisons it)
+        bad = (target < 0) | (target >= logits.shape[1])
+        if bool(bad.any()):
+            i = int(bad.nonzero()[0, 0])
+            raise IndexError(f"cross_entropy: target {int(target[i])} at position {i} is outside "
+                             f"[0, {logits.shape[1]})")
     if torch.is_grad_enabled() and logits.requires_grad:
         return _CrossEntropy.apply(logits, target, metrics)
     loss, _ = _C().ce_fused(logits, target, metrics, False)

@@ -1,16 +1,20 @@
-"""Single-process data parallelism for ``main.py`` (parity: main.py:73-74 ``nn.DataParallel``).
+"""Single-device module wrapper with ``nn.DataParallel``'s checkpoint layout (main.py:73-74).
 
-* One visible GPU (the common MI355X case): a thin wrapper whose only job is API/checkpoint
-  parity — the model lives in ``.module`` so ``state_dict`` keys carry the reference's
-  ``module.`` prefix — and the forward runs directly (no replicate/scatter/gather per step).
-* Several GPUs in one process: the replicate / scatter / parallel_apply / gather schedule of
-  ``torch.nn.DataParallel``, which works unchanged with the native ops
-  because their backward returns gradients of non-leaf (replicated) parameters through autograd.
-  For multi-GPU throughput use ``main_dist.py`` (one process per GPU, RCCL buckets).
+Multi-GPU data parallelism in this framework is one process per GPU on the native RCCL bucket
+engine (:mod:`.ddp`): ``main.py`` and the non-``--dist`` path of ``main_dist.py`` — the
+reference's ``nn.DataParallel`` workloads (main.py:74, main_dist.py:145-147) —
+start one rank per visible GPU themselves (:func:`.launcher.spawn_local_ranks`) and split the
+batch across them the way DataParallel's scatter did. Each rank's model lives in ``.module``, so
+checkpoints keep the reference's ``module.`` keys either way.
+
+This wrapper covers the remaining single-process case: the model on one device, forward called
+directly (no replicate / scatter / gather per step), ``module.`` prefixed ``state_dict``. Asking it
+for several devices in one process raises and points at the rank-per-GPU launch instead of
+silently falling back to stock single-process replication (broadcast_coalesced / reduce_add every
+step, no hipGraph, no native buckets).
 """
 from __future__ import annotations
 
-import torch
 import torch.nn as nn
 
 
@@ -19,13 +23,15 @@ class DataParallel(nn.Module):
         super().__init__()
         self.module = module
         if device_ids is None:
-            device_ids = list(range(torch.cuda.device_count())) if torch.cuda.is_available() else []
-        self.device_ids = device_ids
-        self._torch_dp = None
+            p = next(module.parameters(), None)
+            device_ids = [p.device.index] if p is not None and p.device.type == "cuda" else []
         if len(device_ids) > 1:
-            self._torch_dp = nn.DataParallel(module, device_ids=device_ids, output_device=output_device)
+            raise ValueError(
+                "pytorch_cifar_amd.DataParallel is single-device; for several GPUs run one rank per GPU "
+                "(main.py / main_dist.py do this by default, or parallel.launcher.spawn_local_ranks) "
+                "with parallel.ddp.DistributedDataParallel")
+        self.device_ids = device_ids
+        self.output_device = output_device
 
     def forward(self, *inputs, **kwargs):
-        if self._torch_dp is not None:
-            return self._torch_dp(*inputs, **kwargs)
         return self.module(*inputs, **kwargs)

@@ -240,6 +240,12 @@ class DistributedDataParallel(nn.Module):
         self._bcast_pending = False
         self._pass_active = False
 
+    def state_dict(self, *args, **kwargs):
+        # the overlapped BN-buffer broadcast of a grad-enabled forward may still be writing the
+        # buffers on the communication stream: order it before anyone reads them
+        self.finish()
+        return super().state_dict(*args, **kwargs)
+
     def finish(self):
         """Explicitly close a pass (no-op if the autograd callback already ran)."""
         if self._pass_active:

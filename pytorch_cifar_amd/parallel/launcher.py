@@ -104,6 +104,87 @@ def init_distributed(rank: int, world: int, local_rank: int, backend: str = "ncc
     return ctx
 
 
+def free_port(host: str = "127.0.0.1") -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+def spawned_world() -> int:
+    """WORLD_SIZE of the torchrun-style environment (0 when this process was not launched as a rank)."""
+    return int(os.environ.get("WORLD_SIZE", "0") or 0)
+
+
+def spawn_local_ranks(nprocs: int, argv: list[str], env_extra: dict | None = None,
+                      poll_s: float = 0.2) -> int:
+    """Run ``python argv...`` as ``nprocs`` rank processes of one node and wait for them.
+
+    The self-contained equivalent of ``torchrun --nnodes 1 --nproc-per-node N`` / the reference's
+    ``mp.spawn(main_worker, nprocs=ngpus)`` (main_dist.py:51-60): each child gets the torchrun env
+    (RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT) and
+    binds GPU LOCAL_RANK in :func:`init_from_env`. The parent never touches the GPU (it must not:
+    children are started as fresh interpreters, never by exec'ing a process that initialised HIP),
+    forwards SIGINT/SIGTERM, and if any rank fails it terminates the others (exact child PIDs)
+    so a collective blocked on the dead rank cannot hang the job. Returns the first non-zero exit
+    code (0 when every rank succeeded).
+    """
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    port = free_port()
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL peer buffers)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nprocs),
+                    "LOCAL_WORLD_SIZE": str(nprocs), "GROUP_RANK": "0",
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        env.update(env_extra or {})
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except ProcessLookupError:
+                    pass
+
+    prev = {}
+    for s in (signal.SIGINT, signal.SIGTERM):
+        try:
+            prev[s] = signal.signal(s, lambda sig, _f: stop_all(sig))
+        except ValueError:        # not the main thread
+            pass
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                stop_all()
+                deadline = time.time() + 30
+                for p in procs:
+                    try:
+                        p.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        p.wait()
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        for s, h in prev.items():
+            signal.signal(s, h)
+    return rc
+
+
 def init_from_env(backend: str = "nccl", native_comm: bool = True) -> DistContext:
     """Initialise from torchrun-style environment variables (single process if absent)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))

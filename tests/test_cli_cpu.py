@@ -13,6 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _run(args, cwd, timeout=300, env_extra=None):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     env.update(env_extra or {})
+    env = {k: v for k, v in env.items() if v is not None}
     r = subprocess.run([sys.executable] + args, cwd=cwd, env=env, capture_output=True, text=True,
                        timeout=timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -189,3 +190,83 @@ def test_main_py_aux_flags_cpu(tmp_path):
                 "--profile", str(tmp_path / "p.json"), "--checkpoint_dir", str(tmp_path / "ck")],
                cwd=str(tmp_path))
     assert "Profile trace written" in out
+
+
+def _clean_env():
+    # a stand-alone launch: no torchrun variables inherited from the test runner
+    return {k: None for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+
+
+def _reference_state_keys(module_file, ctor, wrap=True):
+    """state_dict keys of a reference model (imported read-only, no bytecode written)."""
+    import importlib.util
+
+    old = sys.dont_write_bytecode
+    sys.dont_write_bytecode = True
+    try:
+        spec = importlib.util.spec_from_file_location("_ref_" + ctor, module_file)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    finally:
+        sys.dont_write_bytecode = old
+    net = getattr(mod, ctor)()
+    return {("module." if wrap else "") + k for k in net.state_dict()}
+
+
+def test_bench_self_spawn_two_ranks_cpu(tmp_path):
+    """`python bench.py --gpus 2` with no torchrun around it starts its two rank processes itself
+    (reference main_dist.py:51-60 mp.spawn) and rank 0 prints ONE JSON line for the whole job."""
+    import json
+
+    out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                "--model", "LeNet", "--batch", "64"], cwd=str(tmp_path), env_extra=_clean_env())
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 64
+    assert d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+
+
+def test_spawn_local_ranks_failure_stops_peers(tmp_path):
+    """A rank that dies makes the launcher stop the others (a peer blocked in a collective on the
+    dead rank would otherwise hang) and return the failing exit code."""
+    import time
+
+    from pytorch_cifar_amd.parallel.launcher import spawn_local_ranks
+
+    script = tmp_path / "r.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "assert os.environ['WORLD_SIZE'] == '3' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "if r == 1:\n    sys.exit(7)\n"
+                      "time.sleep(120)\n")
+    t0 = time.time()
+    rc = spawn_local_ranks(3, [str(script)])
+    assert rc == 7 and time.time() - t0 < 60
+
+
+def test_main_py_data_parallel_ranks_cpu(tmp_path):
+    """main.py's DataParallel workload on several devices runs as one rank per device on the
+    native bucket engine (here: 2 gloo ranks); rank 0 writes the reference checkpoint layout with
+    exactly the keys nn.DataParallel(reference LeNet).state_dict() has."""
+    out = _run([os.path.join(ROOT, "main.py"), "--model", "LeNet", "--epochs", "1", "--synthetic",
+                "--synthetic_size", "512", "--max_steps", "3", "--cpu", "--nproc", "2",
+                "--batch_size", "64", "--checkpoint_dir", str(tmp_path / "ck")],
+               cwd=str(tmp_path), env_extra=_clean_env())
+    assert out.count("==> Building model..") == 1          # rank 0 prints, rank 1 is quiet
+    ck = torch.load(tmp_path / "ck" / "ckpt.pth", weights_only=True)
+    ref = _reference_state_keys("/root/reference/models/lenet.py", "LeNet")
+    assert set(ck["net"]) == ref
+    assert {"net", "acc", "epoch"} <= set(ck)
+
+
+def test_main_dist_default_path_spawns_ranks_cpu(tmp_path):
+    """main_dist.py without --dist (README / train.sh form, reference: DataParallel) uses every
+    device through spawned ranks; the global batch is split across them."""
+    out = _run([os.path.join(ROOT, "main_dist.py"), "--model", "LeNet", "--epochs", "1",
+                "--synthetic", "--synthetic_size", "1024", "--max_steps", "2", "--cpu", "--nproc", "2",
+                "--batch_size", "128", "--output_dir", str(tmp_path / "o")],
+               cwd=str(tmp_path), env_extra=_clean_env())
+    assert os.path.exists(tmp_path / "o" / "ckpt.pth"), out
+    ck = torch.load(tmp_path / "o" / "ckpt.pth", weights_only=True)
+    assert all(k.startswith("module.") for k in ck["net"])

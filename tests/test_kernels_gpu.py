@@ -280,6 +280,20 @@ def test_cross_entropy(C):
     assert metrics[1].item() == correct and metrics[2].item() == 300
 
 
+@pytest.mark.parametrize("K", [10, 40])
+def test_cross_entropy_bad_label_poisons(C, K):
+    """A label outside [0, K) must not train silently (F.cross_entropy raises): the fused kernel
+    NaN-poisons the loss and that sample's gradient row (register path K<=16 and row path)."""
+    logits = torch.randn(64, K, device="cuda")
+    tgt = torch.randint(0, K, (64,), device="cuda")
+    tgt[5] = K
+    tgt[9] = -1
+    loss, dl = C.ce_fused(logits, tgt, None, True)
+    assert torch.isnan(loss).all()
+    assert torch.isnan(dl[5]).all() and torch.isnan(dl[9]).all()
+    assert torch.isfinite(dl[0]).all()
+
+
 @pytest.mark.parametrize("Cc", [16, 12])
 def test_pools_and_gap(C, Cc):
     """Max/avg pools and global average pool; C % 8 == 0 takes the vectorized max-pool kernels."""
