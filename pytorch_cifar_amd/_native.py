@@ -94,6 +94,7 @@ def lib():
 
             warnings.warn("pytorch_cifar_amd: .srchash missing; the .so's embedded source digest matches")
         _lib = _C
+        _tune_cache(_lib)
         return _wrap(_lib)
     except ImportError as e:  # not built yet
         _err = e
@@ -102,10 +103,42 @@ def lib():
         from . import _C  # noqa: F811
 
         _lib = _C
+        _tune_cache(_lib)
         return _wrap(_lib)
     raise RuntimeError(
         "pytorch_cifar_amd native extension is not built; run `python -m pytorch_cifar_amd._build`"
     ) from _err
+
+
+def _tune_cache(mod):
+    """PCA_TUNE_CACHE=<file.json>: restore the conv autotuner's choices at load and save them at
+    exit (the reference's cudnn.benchmark re-times every run; here a cache skips the trials, and
+    profiled runs reuse the choices an un-profiled run made)."""
+    path = os.environ.get("PCA_TUNE_CACHE")
+    if not path or not hasattr(mod, "tune_import"):
+        return
+    import atexit
+    import json
+
+    try:
+        with open(path) as fh:
+            mod.tune_import(json.load(fh))
+    except (OSError, ValueError):
+        pass
+
+    def save():
+        try:
+            rows = mod.tune_export()
+            if not rows:
+                return
+            tmp = f"{path}.{os.getpid()}.tmp"
+            with open(tmp, "w") as fh:
+                json.dump(rows, fh)
+            os.replace(tmp, path)
+        except Exception:
+            pass
+
+    atexit.register(save)
 
 
 def available() -> bool:

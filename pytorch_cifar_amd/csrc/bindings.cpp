@@ -43,6 +43,8 @@ void wgrad_record_tuned(int N, int H, int W, int Cin, int Cout, int KH, int KW, 
                         int groups, int cfg, int split);
 int wgrad_tuned_count();
 void wgrad_clear_tuned();
+std::vector<std::vector<int>> tune_export();
+int tune_import(const std::vector<std::vector<int>>& rows);
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
 void set_conv_tile(int kind, int idx);
@@ -1391,6 +1393,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
   m.def("conv_autotune_enabled", []() { return g_autotune; });
+  m.def("tune_export", &pca::tune_export, "autotuned conv / wgrad choices as int rows");
+  m.def("tune_import", &pca::tune_import, "restore rows from tune_export (returns rows taken)");
   m.def("src_digest", []() { return std::string(pca_src_digest); },
         "sha256 of the csrc sources this library was built from (_build.source_digest)");
   m.def("conv_trial", [](int kind, int cfg, int split) {

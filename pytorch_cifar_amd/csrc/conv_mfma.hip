@@ -2104,4 +2104,33 @@ void wgrad_record_tuned(int N, int H, int W, int Cin, int Cout, int KH, int KW, 
 int wgrad_tuned_count() { return (int)g_wtuned.size(); }
 void wgrad_clear_tuned() { g_wtuned.clear(); }
 
+// ---- tuning cache (PCA_TUNE_CACHE, _native.py): rows {table, key[13], cfg, split} ----
+std::vector<std::vector<int>> tune_export() {
+  std::vector<std::vector<int>> rows;
+  int table = 0;
+  for (const auto* m : {&g_tuned, &g_wtuned}) {
+    for (const auto& kv : *m) {
+      std::vector<int> r{table};
+      r.insert(r.end(), kv.first.v, kv.first.v + 13);
+      r.push_back(kv.second.first);
+      r.push_back(kv.second.second);
+      rows.push_back(std::move(r));
+    }
+    ++table;
+  }
+  return rows;
+}
+
+int tune_import(const std::vector<std::vector<int>>& rows) {
+  int n = 0;
+  for (const auto& r : rows) {
+    if (r.size() != 16 || (r[0] != 0 && r[0] != 1)) continue;
+    TuneKey k;
+    std::copy(r.begin() + 1, r.begin() + 14, k.v);
+    (r[0] == 0 ? g_tuned : g_wtuned)[k] = {r[14], r[15]};
+    ++n;
+  }
+  return n;
+}
+
 }  // namespace pca

@@ -27,27 +27,53 @@ def short(name, n=70):
     return name[:n] + grid
 
 
+def _grid(r):
+    g = r.get("Grid_Size")
+    if g:
+        return int(g)
+    return int(r.get("Grid_Size_X", 1)) * int(r.get("Grid_Size_Y", 1)) * int(r.get("Grid_Size_Z", 1))
+
+
+def _window(rows):
+    """rows (dispatch_id, ...) sorted; keep the last complete step (after the second-to-last
+    sgd_kernel up to and including the last one)."""
+    sgd = [r[0] for r in rows if "sgd_kernel" in r[1]]
+    if len(sgd) >= 2:
+        lo, hi = sgd[-2], sgd[-1]
+        rows = [r for r in rows if lo < r[0] <= hi]
+    return rows
+
+
 def load_run(d):
-    trace = {}
+    """{key: [us, launches, Counter]} of one run's last step. Counters and durations are windowed
+    and keyed (kernel name @ grid) separately: the counter and trace CSVs number dispatches
+    independently."""
+    out = collections.defaultdict(lambda: [0.0, 0, collections.Counter()])
+    trace = []
     for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            g = r.get("Grid_Size") or (int(r.get("Grid_Size_X", 1)) * int(r.get("Grid_Size_Y", 1))
-                                       * int(r.get("Grid_Size_Z", 1)))
-            trace[int(r["Dispatch_Id"])] = (f'{r["Kernel_Name"]} @grid{g}', int(r["Start_Timestamp"]),
-                                            int(r["End_Timestamp"]))
-    counters = collections.defaultdict(dict)
+            trace.append((int(r["Dispatch_Id"]), r["Kernel_Name"], _grid(r),
+                          (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    trace.sort()
+    for _, name, g, us in _window(trace):
+        e = out[f"{name} @grid{g}"]
+        e[0] += us
+        e[1] += 1
+    per = {}
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             did = int(r["Dispatch_Id"])
-            counters[did][r["Counter_Name"]] = counters[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-            if did not in trace:
-                trace[did] = (f'{r["Kernel_Name"]} @grid{r.get("Grid_Size", "?")}', 0, 0)
-    ids = sorted(trace)
-    sgd = [i for i in ids if "sgd_kernel" in trace[i][0]]
-    if len(sgd) >= 2:
-        lo, hi = sgd[-2], sgd[-1]
-        ids = [i for i in ids if lo < i <= hi]
-    return [(trace[i][0], (trace[i][2] - trace[i][1]) / 1e3, counters.get(i, {})) for i in ids]
+            ent = per.setdefault(did, [did, r["Kernel_Name"], _grid(r), collections.Counter()])
+            ent[3][r["Counter_Name"]] += float(r["Counter_Value"])
+    for _, name, g, cs in _window(sorted(per.values(), key=lambda x: x[0])):
+        key = f"{name} @grid{g}"
+        if key not in out:
+            # grid reported differently by the two CSVs: fall back to a unique same-name entry
+            same = [k for k in out if k.rsplit(" @grid", 1)[0] == name]
+            if len(same) == 1:
+                key = same[0]
+        out[key][2].update(cs)
+    return out
 
 
 def main():
@@ -58,14 +84,9 @@ def main():
     a = ap.parse_args()
     agg = collections.defaultdict(lambda: {"us": [], "n": 0, "c": collections.Counter()})
     for d in a.dirs:
-        per = collections.defaultdict(lambda: [0.0, 0, collections.Counter()])
-        for name, us, cs in load_run(d):
-            e = per[name]
-            e[0] += us
-            e[1] += 1
-            e[2].update(cs)
-        for name, (us, n, cs) in per.items():
-            agg[name]["us"].append(us)
+        for name, (us, n, cs) in load_run(d).items():
+            if n:
+                agg[name]["us"].append(us)
             agg[name]["n"] = max(agg[name]["n"], n)
             agg[name]["c"].update(cs)
     rows = []
