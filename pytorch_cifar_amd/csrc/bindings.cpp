@@ -115,9 +115,13 @@ void se_ds_launch(const bf16*, const bf16*, const float*, int, int, int, float*,
 void se_dx_launch(const bf16*, const float*, const float*, int, int, int, bf16*, hipStream_t);
 bool head_batch_supported(int N, int K);
 void head_fwd_launch(const bf16*, int, int, int, const float*, const float*, int, float*, float*,
-                     hipStream_t);
+                     float, int64_t*, uint8_t*, hipStream_t);
 void head_bwd_launch(const float*, const float*, const float*, int, int, int, int, bf16*, float*,
-                     float*, hipStream_t);
+                     float*, float, const uint8_t*, hipStream_t);
+void dropout_fwd_launch(const void*, bool, size_t, int64_t, float, int64_t*, uint8_t*, void*,
+                        hipStream_t);
+void dropout_bwd_launch(const void*, bool, size_t, int64_t, float, const uint8_t*, void*,
+                        hipStream_t);
 void avgpool_fwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, hipStream_t);
 void avgpool_bwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, hipStream_t);
 void maxpool_fwd_launch(const bf16*, int, int, int, int, int, int, int, int, int, bf16*, uint8_t*,
@@ -923,7 +927,15 @@ std::vector<Tensor> augment_packed(const Tensor& data, const Tensor& labels, con
 }
 
 // fused classifier head: x [N,H,W,C] bf16 -> (logits [N,K] fp32, pooled [N,C] fp32)
-std::vector<Tensor> head_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& b) {
+// rng state of the dropout kernels: int64[3] {seed, step, tickets} on the device (misc.hip)
+static void check_rng(const Tensor& rng) {
+  TORCH_CHECK(rng.is_cuda() && rng.scalar_type() == at::kLong && rng.numel() == 3 &&
+                  rng.is_contiguous(),
+              "dropout rng state must be a contiguous int64[3] device tensor {seed, step, 0}");
+}
+
+std::vector<Tensor> head_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& b,
+                             double p, const optional<Tensor>& rng) {
   check_bf16(x, "x");
   check_f32(w, "weight");
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
@@ -938,16 +950,52 @@ std::vector<Tensor> head_fwd(const Tensor& x, const Tensor& w, const optional<Te
   auto fopt = x.options().dtype(at::kFloat);
   auto logits = at::empty({N, K}, fopt);
   auto pooled = at::empty({N, C}, fopt);
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  Tensor dmask;
+  if (p > 0.0) {
+    TORCH_CHECK(rng.has_value() && rng->defined(), "dropout needs its rng state");
+    check_rng(*rng);
+    dmask = at::empty({N, C}, x.options().dtype(at::kByte));
+  }
   pca::head_fwd_launch(ptr<bf16>(x), N, HW, C, ptr<float>(w), optr<float>(b), K, ptr<float>(pooled),
-                       ptr<float>(logits), cur_stream());
-  return {logits, pooled};
+                       ptr<float>(logits), (float)p, p > 0.0 ? ptr<int64_t>(*rng) : nullptr,
+                       p > 0.0 ? ptr<uint8_t>(dmask) : nullptr, cur_stream());
+  return {logits, pooled, dmask};
+}
+
+// generic dropout / drop-connect on a contiguous bf16 or fp32 tensor: one keep byte per unit of
+// `unit_len` consecutive elements (1 = elementwise dropout; C*H*W = per-sample drop-connect)
+std::vector<Tensor> dropout_fwd(const Tensor& x, double p, int64_t unit_len, const Tensor& rng) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "dropout: contiguous bf16 / fp32 device tensor");
+  TORCH_CHECK(p > 0.0 && p < 1.0 && unit_len >= 1 && x.numel() % unit_len == 0, "dropout args");
+  check_rng(rng);
+  auto y = at::empty_like(x);
+  auto mask = at::empty({x.numel() / unit_len}, x.options().dtype(at::kByte));
+  if (x.numel())
+    pca::dropout_fwd_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, x.numel(), unit_len,
+                            (float)p, ptr<int64_t>(rng), ptr<uint8_t>(mask), y.data_ptr(), cur_stream());
+  return {y, mask};
+}
+
+Tensor dropout_bwd(const Tensor& dy, const Tensor& mask, double p, int64_t unit_len) {
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() &&
+                  (dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kFloat),
+              "dropout grad: contiguous bf16 / fp32 device tensor");
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() * unit_len == dy.numel(), "mask");
+  auto dx = at::empty_like(dy);
+  if (dy.numel())
+    pca::dropout_bwd_launch(dy.data_ptr(), dy.scalar_type() == at::kBFloat16, dy.numel(), unit_len,
+                            (float)p, ptr<uint8_t>(mask), dx.data_ptr(), cur_stream());
+  return dx;
 }
 
 // backward of head_fwd: returns {dx [N,H,W,C] bf16, dw [K,C], db [K]}; dw / db are added into
 // the given accumulators (gradient-arena views) when present, else fresh zero-based tensors
 std::vector<Tensor> head_bwd(const Tensor& dl, const Tensor& w, const Tensor& pooled, int H, int W,
                              const optional<Tensor>& dw_acc, const optional<Tensor>& db_acc,
-                             bool want_db) {
+                             bool want_db, double p, const optional<Tensor>& dmask) {
   check_f32(dl, "dlogits");
   check_f32(w, "weight");
   check_f32(pooled, "pooled");
@@ -960,9 +1008,14 @@ std::vector<Tensor> head_bwd(const Tensor& dl, const Tensor& w, const Tensor& po
   if (want_db) db = (db_acc.has_value() && db_acc->defined()) ? *db_acc : at::zeros({K}, fopt);
   TORCH_CHECK(dw.is_contiguous() && dw.numel() == (int64_t)K * C, "dw accumulator");
   if (db.defined()) TORCH_CHECK(db.is_contiguous() && db.numel() == K, "db accumulator");
+  const bool drop = dmask.has_value() && dmask->defined();
+  if (drop)
+    TORCH_CHECK(dmask->scalar_type() == at::kByte && dmask->numel() == (int64_t)N * C && p > 0.0 &&
+                    p < 1.0,
+                "dropout mask [N, C] uint8 and p in (0, 1)");
   pca::head_bwd_launch(ptr<float>(dl), ptr<float>(w), ptr<float>(pooled), N, H * W, C, K,
                        ptr<bf16>(dx), ptr<float>(dw), db.defined() ? ptr<float>(db) : nullptr,
-                       cur_stream());
+                       (float)p, drop ? ptr<uint8_t>(*dmask) : nullptr, cur_stream());
   return {dx, dw, db};
 }
 
@@ -1441,10 +1494,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("se_supported", &pca::se_mlp_supported, "fused squeeze-excite path for (C, R)?");
   m.def("se_forward", &se_forward, "squeeze-excite: pool + MLP + sigmoid scale (NHWC bf16)");
   m.def("se_backward", &se_backward);
-  m.def("head_fwd", &head_fwd, "fused global-average-pool + Linear -> (logits, pooled)");
+  m.def("head_fwd", &head_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("p") = 0.0,
+        py::arg("rng") = py::none(),
+        "fused global-average-pool [+ Philox dropout] + Linear -> (logits, pooled, keep mask)");
   m.def("head_bwd", &head_bwd, py::arg("dl"), py::arg("w"), py::arg("pooled"), py::arg("H"),
         py::arg("W"), py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none(),
-        py::arg("want_db") = true);
+        py::arg("want_db") = true, py::arg("p") = 0.0, py::arg("dmask") = py::none());
+  m.def("dropout_fwd", &dropout_fwd, "Philox dropout / drop-connect -> (y, keep mask per unit)");
+  m.def("dropout_bwd", &dropout_bwd, "dropout / drop-connect gradient from the keep mask");
   m.def("head_supported", [](int N, int C, int K) {
     return pca::head_supported(C, K) && pca::head_batch_supported(N, K);
   });

@@ -1225,6 +1225,101 @@ void augment_launch(const uint8_t* data, const int64_t* idx, const int32_t* rnd,
 }
 static bool vec8_ok(int C) { return C % 8 == 0 && C <= 2048; }
 
+// ------------------------------------------------------------------------- dropout (Philox)
+// Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11) keyed by a 64-bit seed, counter =
+// (element/unit index lo, hi, step lo, step hi). `rng` is a device int64[3] {seed, step, tickets}:
+// every block reads `step` first, then takes a ticket; the block drawing the last ticket advances
+// `step` and resets the tickets (vector atomics), so each launch — eager or a hipGraph replay —
+// draws fresh masks with no host involvement, and every block saw the same step.
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += W0;
+    k.y += W1;
+  }
+  return c;
+}
+
+// keep decision of unit u at `step` (probability 1 - p)
+__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t step, uint64_t u, float p) {
+  const uint4 r = philox4x32_10(make_uint4((uint32_t)u, (uint32_t)(u >> 32), (uint32_t)step,
+                                           (uint32_t)(step >> 32)),
+                                make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  return (float)(r.x >> 8) * (1.f / 16777216.f) >= p;
+}
+
+// last block of the launch advances the step (see above); call after the block's last read of
+// rng[1], from every thread (contains a barrier)
+__device__ __forceinline__ void drop_advance(int64_t* rng) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    unsigned long long* r = reinterpret_cast<unsigned long long*>(rng);
+    const unsigned long long t = atomicAdd(r + 2, 1ull);
+    if (t == (unsigned long long)gridDim.x - 1) {
+      atomicAdd(r + 1, 1ull);
+      atomicExch(r + 2, 0ull);
+    }
+  }
+}
+
+// y = x * keep(unit(i)) / (1 - p); unit(i) = i / unit_len (1: dropout, C*H*W: drop-connect);
+// mask[unit] = keep (written by the thread that owns the unit's first element)
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_fwd_kernel(const T* __restrict__ x, size_t n,
+                                                          int64_t unit_len, float p,
+                                                          int64_t* __restrict__ rng,
+                                                          uint8_t* __restrict__ mask,
+                                                          T* __restrict__ y) {
+  const uint64_t seed = (uint64_t)rng[0], step = (uint64_t)rng[1];
+  const float scale = 1.f / (1.f - p);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const uint64_t u = i / (uint64_t)unit_len;
+    const bool keep = drop_keep(seed, step, u, p);
+    if (i % (uint64_t)unit_len == 0) mask[u] = keep;
+    y[i] = (T)(keep ? (float)x[i] * scale : 0.f);
+  }
+  drop_advance(rng);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_bwd_kernel(const T* __restrict__ dy, size_t n,
+                                                          int64_t unit_len, float p,
+                                                          const uint8_t* __restrict__ mask,
+                                                          T* __restrict__ dx) {
+  const float scale = 1.f / (1.f - p);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    dx[i] = (T)(mask[i / (uint64_t)unit_len] ? (float)dy[i] * scale : 0.f);
+}
+
+void dropout_fwd_launch(const void* x, bool bf, size_t n, int64_t unit_len, float p, int64_t* rng,
+                        uint8_t* mask, void* y, hipStream_t st) {
+  const dim3 grid(std::min<size_t>(cdiv64((int64_t)n, 256), 2048)), block(256);
+  if (bf)
+    hipLaunchKernelGGL(dropout_fwd_kernel<bf16>, grid, block, 0, st, (const bf16*)x, n, unit_len,
+                       p, rng, mask, (bf16*)y);
+  else
+    hipLaunchKernelGGL(dropout_fwd_kernel<float>, grid, block, 0, st, (const float*)x, n, unit_len,
+                       p, rng, mask, (float*)y);
+}
+
+void dropout_bwd_launch(const void* dy, bool bf, size_t n, int64_t unit_len, float p,
+                        const uint8_t* mask, void* dx, hipStream_t st) {
+  const dim3 grid(std::min<size_t>(cdiv64((int64_t)n, 256), 2048)), block(256);
+  if (bf)
+    hipLaunchKernelGGL(dropout_bwd_kernel<bf16>, grid, block, 0, st, (const bf16*)dy, n, unit_len,
+                       p, mask, (bf16*)dx);
+  else
+    hipLaunchKernelGGL(dropout_bwd_kernel<float>, grid, block, 0, st, (const float*)dy, n, unit_len,
+                       p, mask, (float*)dx);
+}
+
 // ------------------------------------------------------------------- classifier head
 // Global average pool + Linear, fused (every zoo head: resnet.py:127-130 avg_pool2d(4) -> view ->
 // linear, mobilenetv2.py:74, efficientnet.py:145 ...). The reference runs a pooling kernel, a
@@ -1247,7 +1342,12 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ 
                                                        const float* __restrict__ w,
                                                        const float* __restrict__ b, int K,
                                                        float* __restrict__ pooled,
-                                                       float* __restrict__ logits) {
+                                                       float* __restrict__ logits, float p,
+                                                       int64_t* __restrict__ rng,
+                                                       uint8_t* __restrict__ dmask) {
+  // p > 0: training-mode dropout on the pooled features before the Linear (efficientnet.py:147-
+  // 149): pooled holds the dropped, 1/(1-p)-scaled features (the weight gradient's operand) and
+  // dmask the keep bytes (the input gradient's)
   extern __shared__ float hs[];                  // [RL][C] row-lane partials; [4][K] wave sums
   const int n = blockIdx.x, tid = threadIdx.x;
   const int CG = C >> 3;
@@ -1272,6 +1372,9 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ 
   // every thread: pooled channels c = tid, tid + 256, ... and the partial dot products of all K
   // classes over them (K independent weight loads per channel), then one block reduction per k
   const float inv = 1.f / HW;
+  const bool drop = p > 0.f;
+  const uint64_t seed = drop ? (uint64_t)rng[0] : 0, step = drop ? (uint64_t)rng[1] : 0;
+  const float dscale = drop ? 1.f / (1.f - p) : 1.f;
   float part[kHeadMaxK];
 #pragma unroll
   for (int k = 0; k < kHeadMaxK; ++k) part[k] = 0.f;
@@ -1279,6 +1382,11 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ 
     float t = 0.f;
     for (int r = 0; r < RL; ++r) t += hs[r * C + c];
     t *= inv;
+    if (drop) {
+      const bool keep = drop_keep(seed, step, (uint64_t)n * C + c, p);
+      dmask[(size_t)n * C + c] = keep;
+      t = keep ? t * dscale : 0.f;
+    }
     pooled[(size_t)n * C + c] = t;
 #pragma unroll
     for (int k = 0; k < kHeadMaxK; ++k) {
@@ -1298,6 +1406,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ 
     const float t = hs[tid] + hs[kHeadMaxK + tid] + hs[2 * kHeadMaxK + tid] + hs[3 * kHeadMaxK + tid];
     logits[(size_t)n * K + tid] = t + (b ? b[tid] : 0.f);
   }
+  if (drop) drop_advance(rng);
 }
 
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dl,
@@ -1306,12 +1415,14 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
                                                        int HW, int C, int K,
                                                        bf16* __restrict__ dx,
                                                        float* __restrict__ dw,
-                                                       float* __restrict__ db) {
+                                                       float* __restrict__ db, float p,
+                                                       const uint8_t* __restrict__ dmask) {
   extern __shared__ float hs[];
   const int tid = threadIdx.x;
   if ((int)blockIdx.x < N) {
     const int n = blockIdx.x;
-    const float inv = 1.f / HW;
+    // (dropout: the pooled-feature gradient passes kept features scaled by 1/(1-p))
+    const float inv = 1.f / HW * (dmask ? 1.f / (1.f - p) : 1.f);
     float d[kHeadMaxK];
 #pragma unroll
     for (int k = 0; k < kHeadMaxK; ++k) {
@@ -1322,7 +1433,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
       float t = 0.f;
 #pragma unroll
       for (int k = 0; k < kHeadMaxK; ++k) t += d[k] * w[(size_t)min(k, K - 1) * C + c];
-      hs[c] = t;
+      hs[c] = (dmask && !dmask[(size_t)n * C + c]) ? 0.f : t;
     }
     __syncthreads();
     const int CG = C >> 3;
@@ -1383,20 +1494,22 @@ bool head_supported(int C, int K) { return C % 8 == 0 && C <= 4096 && K >= 1 && 
 bool head_batch_supported(int N, int K) { return N >= 1 && K >= 1; }
 
 void head_fwd_launch(const bf16* x, int N, int HW, int C, const float* w, const float* b, int K,
-                     float* pooled, float* logits, hipStream_t st) {
+                     float* pooled, float* logits, float p, int64_t* rng, uint8_t* dmask,
+                     hipStream_t st) {
   const int CG = C >> 3;
   const int RL = CG >= 256 ? 1 : 256 / CG;
   const size_t lds = std::max<size_t>((size_t)RL * C, 4 * kHeadMaxK) * sizeof(float);
   hipLaunchKernelGGL(head_fwd_kernel, dim3(N), dim3(256), lds, st, x, HW, C, w, b, K, pooled,
-                     logits);
+                     logits, p, rng, dmask);
 }
 
 void head_bwd_launch(const float* dl, const float* w, const float* pooled, int N, int HW, int C,
-                     int K, bf16* dx, float* dw, float* db, hipStream_t st) {
+                     int K, bf16* dx, float* dw, float* db, float p, const uint8_t* dmask,
+                     hipStream_t st) {
   const size_t lds = std::max<size_t>((size_t)C, (size_t)kHeadMaxK * 4 * 64) * sizeof(float);
   const int wblocks = cdiv(C, 64) * cdiv(N, kHeadSamples);
   hipLaunchKernelGGL(head_bwd_kernel, dim3(N + wblocks), dim3(256), lds, st, dl, w, pooled, N,
-                     HW, C, K, dx, dw, db);
+                     HW, C, K, dx, dw, db, p, dmask);
 }
 
 void gap_fwd_launch(const bf16* x, int N, int HW, int C, float* y, hipStream_t st) {

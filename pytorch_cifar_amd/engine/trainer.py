@@ -83,6 +83,10 @@ class TrainStep:
                 add(st.get("momentum_buffer"))
         for b in inner.buffers():
             add(b)
+        from ..ops.functional import rng_states
+
+        for r in rng_states(inner):      # dropout Philox step counters
+            add(r)
         add(self.metrics)
         return out
 

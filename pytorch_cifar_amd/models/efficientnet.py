@@ -6,7 +6,6 @@ zeros), depthwise k3/k5 + BN + Swish, squeeze-excite with Swish, project 1x1 + B
 Drop-connect keeps the reference's schedule: ``b`` is never incremented (efficientnet.py:125,130),
 so every rate is 0 and drop-connect never fires; final dropout 0.2 in training.
 """
-import torch
 import torch.nn as tnn
 
 from ..nn import BatchNorm2d, Conv2d, Linear, Sequential
@@ -18,9 +17,9 @@ def swish(x):
 
 
 def drop_connect(x, drop_ratio):
-    keep_ratio = 1.0 - drop_ratio
-    mask = torch.empty([x.shape[0], 1, 1, 1], dtype=x.dtype, device=x.device).bernoulli_(keep_ratio)
-    return x / keep_ratio * mask
+    """Per-sample drop-connect (efficientnet.py:16-22): native Philox keep byte per sample on the
+    GPU (ops/functional.py drop_connect), Bernoulli mask on the CPU reference path."""
+    return F.drop_connect(x, drop_ratio)
 
 
 class SE(tnn.Module):
@@ -91,10 +90,9 @@ class EfficientNet(tnn.Module):
 
     def forward(self, x):
         out = self.layers(self.bn1(self.conv1(x), act="swish"))
-        out = F.adaptive_avg_pool2d(out, 1)
-        out = out.reshape(out.size(0), -1)
-        out = F.dropout(out, self.cfg["dropout_rate"], self.training)
-        return self.linear(out)
+        # adaptive_avg_pool2d(1) -> flatten -> dropout(0.2, training) -> linear as one fused head
+        # kernel each way (Philox keep mask; ops/functional.py pool_linear)
+        return F.pool_linear(out, None, self.linear, self.cfg["dropout_rate"], self.training)
 
 
 def EfficientNetB0():

@@ -14,6 +14,7 @@ from ..ops.functional import (  # noqa: F401
     channel_shuffle,
     cross_entropy,
     dpn_merge,
+    drop_connect,
     dropout,
     global_avg_pool,
     max_pool2d,

@@ -1150,25 +1150,26 @@ def global_avg_pool(x):
 
 
 class _PoolLinear(torch.autograd.Function):
-    """Global average pool + Linear in one kernel each way (csrc/misc.hip head_*_kernel)."""
+    """Global average pool [+ dropout] + Linear in one kernel each way (csrc/misc.hip head_*)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
-        logits, pooled = _C().head_fwd(x, weight, bias)
-        ctx.save_for_backward(weight, pooled)
+    def forward(ctx, x, weight, bias, p=0.0, rng=None):
+        logits, pooled, dmask = _C().head_fwd(x, weight, bias, p, rng)
+        ctx.save_for_backward(weight, pooled, dmask if p > 0 else None)
         ctx.hw = (x.shape[1], x.shape[2])
         ctx.params = (weight, bias)
+        ctx.p = p
         return logits
 
     @staticmethod
     def backward(ctx, dl):
-        weight, pooled = ctx.saved_tensors
+        weight, pooled, dmask = ctx.saved_tensors
         w, b = ctx.params
         ctx.params = None
         wbuf = G.grad_buffer(w) if (w.requires_grad and w.is_leaf) else None
         bbuf = G.grad_buffer(b) if (b is not None and b.requires_grad and b.is_leaf) else None
         dx, dw, db = _C().head_bwd(dl.float().contiguous(), weight, pooled, ctx.hw[0], ctx.hw[1],
-                                   wbuf, bbuf, b is not None)
+                                   wbuf, bbuf, b is not None, ctx.p, dmask)
         dw_ret = db_ret = None
         if w.requires_grad:
             if wbuf is not None:
@@ -1184,26 +1185,58 @@ class _PoolLinear(torch.autograd.Function):
                 G.accumulate(b, db)
             else:
                 db_ret = db
-        return dx, dw_ret, db_ret
+        return dx, dw_ret, db_ret, None, None
 
 
-def pool_linear(x, kernel_size, linear):
-    """``linear(avg_pool2d(x, kernel_size).flatten(1))`` — the classifier head of the zoo.
+def rng_state(owner, device):
+    """The persistent Philox state int64[3] {seed, step, tickets} of ``owner``'s dropout on
+    ``device`` (kept in the module ``__dict__``: not a buffer, so state_dict keys stay the
+    reference's). The kernels advance ``step`` themselves — eager and hipGraph replay alike."""
+    d = owner.__dict__.setdefault("_pca_rng", {})
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    t = d.get(key)
+    if t is None:
+        # seeded from torch's seed (torch.manual_seed reproduces it) and the creation order
+        _RNG_SEQ[0] += 1
+        seed = (torch.initial_seed() * 0x9E3779B97F4A7C15 + _RNG_SEQ[0] * 0xBF58476D1CE4E5B9) % (1 << 62)
+        t = d[key] = torch.tensor([seed, 0, 0], dtype=torch.int64, device=device)
+    return t
+
+
+_RNG_SEQ = [0]
+
+
+def rng_states(model):
+    """Every dropout rng state tensor attached to ``model``'s modules (training-step state)."""
+    out = []
+    for m in model.modules():
+        out += list(m.__dict__.get("_pca_rng", {}).values())
+    return out
+
+
+def pool_linear(x, kernel_size, linear, dropout_p=0.0, training=False):
+    """``linear(dropout(avg_pool2d(x, kernel_size).flatten(1)))`` — the classifier head of the zoo
+    (dropout only where the reference has it: efficientnet.py:147-149, p = 0.2 in training).
 
     ``kernel_size=None`` means a global (adaptive 1x1) pool. When the pool is global and the
-    shapes allow (C % 8 == 0, <= 16 classes, fp32 weights), the pool and the Linear run as one
-    fused kernel forward and one backward (its weight gradient is added with fp32 atomics);
-    otherwise (CPU reference path, non-global pools, deterministic mode) it is exactly the
-    unfused composition.
+    shapes allow (C % 8 == 0, <= 16 classes, fp32 weights), the pool, the dropout (Philox, keep
+    mask kept as bytes for the backward) and the Linear run as one fused kernel forward and one
+    backward (its weight gradient is added with fp32 atomics); otherwise (CPU reference path,
+    non-global pools, deterministic mode) it is exactly the unfused composition.
     """
     N, C, H, W = x.shape
     glob = kernel_size is None or (_pair1(kernel_size) == H == W)
     w, b = linear.weight, linear.bias
+    p = float(dropout_p) if training else 0.0
     if (_ref(x) or not glob or w.dtype != torch.float32 or torch.is_autocast_enabled()
             or not _C().head_supported(N, C, w.shape[0]) or _C().deterministic()):
         out = adaptive_avg_pool2d(x, 1) if kernel_size is None else avg_pool2d(x, kernel_size)
-        return linear(out.reshape(N, -1))
-    return _PoolLinear.apply(to_nhwc(x), w, b)
+        out = out.reshape(N, -1)
+        if p > 0:
+            out = dropout(out, p, True, owner=linear)
+        return linear(out)
+    rng = rng_state(linear, x.device) if p > 0 else None
+    return _PoolLinear.apply(to_nhwc(x), w, b, p, rng)
 
 
 class _AvgPool(torch.autograd.Function):
@@ -1410,10 +1443,50 @@ def cross_entropy(logits, target, metrics=None):
     return loss
 
 
-def dropout(x, p, training):
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, unit_len, rng):
+        y, mask = _C().dropout_fwd(x, p, unit_len, rng)
+        ctx.save_for_backward(mask)
+        ctx.cfg = (p, unit_len)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (mask,) = ctx.saved_tensors
+        p, unit_len = ctx.cfg
+        return _C().dropout_bwd(dy.contiguous(), mask, p, unit_len), None, None, None
+
+
+def _dropout_units(x, unit_len, p, owner):
+    # NCHW-shaped channels_last activations are contiguous as NHWC: a per-sample unit is still a
+    # contiguous run of C*H*W elements, an elementwise one ignores the layout
+    flat = x.permute(0, 2, 3, 1) if (x.dim() == 4 and not x.is_contiguous()) else x
+    if not flat.is_contiguous():
+        flat = flat.contiguous()
+    y = _Dropout.apply(flat, float(p), int(unit_len), rng_state(owner, x.device))
+    return y.permute(0, 3, 1, 2) if flat is not x else y
+
+
+def dropout(x, p, training, owner=None):
+    """Training-mode dropout (efficientnet.py:147-149): Philox keep mask, 1/(1-p) scaling."""
     if not training or p == 0:
         return x
-    return F.dropout(x, p=p, training=True)
+    if _ref(x):
+        return F.dropout(x, p=p, training=True)
+    return _dropout_units(x, 1, p, owner if owner is not None else _dropout_units)
+
+
+def drop_connect(x, drop_ratio, owner=None):
+    """Per-sample drop-connect (efficientnet.py:16-22): the whole sample kept with probability
+    1 - drop_ratio and scaled by 1/(1 - drop_ratio) — one keep byte per sample."""
+    if drop_ratio <= 0:
+        return x
+    if _ref(x):
+        keep = 1.0 - drop_ratio
+        mask = torch.empty([x.shape[0], 1, 1, 1], dtype=x.dtype, device=x.device).bernoulli_(keep)
+        return x / keep * mask
+    return _dropout_units(x, x[0].numel(), drop_ratio, owner if owner is not None else drop_connect)
 
 
 def channel_shuffle(x, groups):

@@ -504,7 +504,7 @@ def test_fused_head_matches_fp32(N, H, C, K, C_=None):
     x = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
     w = torch.randn(K, C, device="cuda") * 0.05
     b = torch.randn(K, device="cuda")
-    logits, pooled = C_.head_fwd(x, w, b)
+    logits, pooled, _ = C_.head_fwd(x, w, b)
     xr = x.float().requires_grad_(True)
     wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
     ref = torch.nn.functional.linear(xr.mean((1, 2)), wr, br)
@@ -520,6 +520,67 @@ def test_fused_head_matches_fp32(N, H, C, K, C_=None):
     assert rel_err(dx, xr.grad) < 1e-2
     assert rel_err(dw - dw0, wr.grad) < 1e-4
     assert rel_err(db - db0, br.grad) < 1e-5
+
+
+def test_fused_head_dropout(C=None):
+    """Pool + Philox dropout (p = 0.2, efficientnet.py:147-149) + Linear: keep rate, 1/(1-p)
+    scaling, logits/gradients consistent with the returned keep mask, fresh masks per launch
+    (the kernel advances its own step counter, also under hipGraph replay)."""
+    from pytorch_cifar_amd import _native
+
+    C_ = _native.lib()
+    torch.manual_seed(1)
+    N, H, Cc, K, p = 256, 2, 1280, 10, 0.2
+    x = torch.randn(N, H, H, Cc, device="cuda").to(torch.bfloat16)
+    w = torch.randn(K, Cc, device="cuda") * 0.05
+    b = torch.randn(K, device="cuda")
+    rng = torch.tensor([1234, 0, 0], dtype=torch.int64, device="cuda")
+    logits, pooled, mask = C_.head_fwd(x, w, b, p, rng)
+    keep = mask.bool()
+    rate = keep.float().mean().item()
+    assert abs(rate - (1 - p)) < 0.01, rate
+    mean = x.float().mean((1, 2))
+    assert rel_err(pooled, torch.where(keep, mean / (1 - p), torch.zeros_like(mean))) < 1e-5
+    assert rel_err(logits, pooled @ w.t() + b) < 1e-4
+    assert rng.tolist() == [1234, 1, 0]
+    dl = torch.randn(N, K, device="cuda")
+    dx, dw, db = C_.head_bwd(dl, w, pooled, H, H, None, None, True, p, mask)
+    dfeat = torch.where(keep, (dl @ w) / (1 - p), torch.zeros(N, Cc, device="cuda")) / (H * H)
+    assert rel_err(dx.float(), dfeat[:, None, None, :].expand(N, H, H, Cc)) < 1e-2
+    assert rel_err(dw, dl.t() @ pooled) < 1e-4 and rel_err(db, dl.sum(0)) < 1e-5
+    # per-step masks differ; graph replays advance the counter too
+    _, _, mask2 = C_.head_fwd(x, w, b, p, rng)
+    assert not torch.equal(mask, mask2) and rng.tolist() == [1234, 2, 0]
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            out = C_.head_fwd(x, w, b, p, rng)
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    m3 = out[2].clone()
+    g.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(m3, out[2]) and rng.tolist()[1] >= 4 and rng.tolist()[2] == 0
+
+
+@pytest.mark.parametrize("unit", [1, 4 * 4 * 96])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_dropout_and_drop_connect(C, unit, dt):
+    """Generic Philox dropout (unit 1) and per-sample drop-connect (unit = C*H*W)."""
+    N, p = 512, 0.3
+    x = torch.randn(N, 4, 4, 96, device="cuda").to(dt)
+    rng = torch.tensor([77, 5, 0], dtype=torch.int64, device="cuda")
+    y, mask = C.dropout_fwd(x, p, unit, rng)
+    assert mask.numel() == x.numel() // unit and rng.tolist() == [77, 6, 0]
+    keep = mask.bool().repeat_interleave(unit).view_as(x)
+    assert abs(mask.float().mean().item() - (1 - p)) < (0.01 if unit == 1 else 0.06)
+    ref = torch.where(keep, x.float() / (1 - p), torch.zeros_like(x, dtype=torch.float32))
+    assert rel_err(y, ref) < 1e-2
+    dy = torch.randn_like(x)
+    dx = C.dropout_bwd(dy, mask, p, unit)
+    assert rel_err(dx, torch.where(keep, dy.float() / (1 - p), torch.zeros_like(dy, dtype=torch.float32))) < 1e-2
 
 
 @pytest.mark.gpu
