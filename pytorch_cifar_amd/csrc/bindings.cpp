@@ -44,6 +44,8 @@ void wgrad_record_tuned(int N, int H, int W, int Cin, int Cout, int KH, int KW, 
 int wgrad_tuned_count();
 void wgrad_clear_tuned();
 std::vector<std::vector<int>> tune_export();
+void c64_set_prof(int64_t* p);
+int c64_grid_size(int N, int H);
 int tune_import(const std::vector<std::vector<int>>& rows);
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
@@ -1446,6 +1448,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
   m.def("conv_autotune_enabled", []() { return g_autotune; });
+  m.def("c64_set_prof", [](const optional<Tensor>& t) {
+    if (t.has_value() && t->defined()) {
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous(), "int64 device tensor");
+      pca::c64_set_prof(t->data_ptr<int64_t>());
+    } else {
+      pca::c64_set_prof(nullptr);
+    }
+  }, "diagnostics: record c64 per-wave tile stamps into t ([grid][4][16][4] int64) or stop");
+  m.def("c64_grid_size", &pca::c64_grid_size);
   m.def("tune_export", &pca::tune_export, "autotuned conv / wgrad choices as int rows");
   m.def("tune_import", &pca::tune_import, "restore rows from tune_export (returns rows taken)");
   m.def("src_digest", []() { return std::string(pca_src_digest); },

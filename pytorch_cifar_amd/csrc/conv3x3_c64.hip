@@ -17,6 +17,8 @@
 // dgrad is the same kernel on dY with the transposed weights read at the mirrored tap (8 - tap).
 #include "mfma_util.h"
 
+#include <cstdlib>
+
 namespace pca {
 
 struct C64Geom {
@@ -30,6 +32,7 @@ struct C64Geom {
   const float* bn_aux;
   float* bn_part;   // [gridDim.x][2][64]
   int shards;       // stats / bn_part: 0 = slab rows, >0 = sharded atomic accumulator
+  int64_t* prof;    // diagnostics: per-wave shader-clock stamps (c64_set_prof), else nullptr
 };
 
 namespace c64 {
@@ -40,16 +43,352 @@ constexpr int HI = (HROWS + 7) / 8;             // 43 LDS-DMA instructions (1 Ki
 constexpr int HBYTES = HI * 1024;
 constexpr int NW = 4;                           // waves: 4 x (64 pixels, 64 channels)
 constexpr int SLOTS = (HI + NW - 1) / NW;       // DMA instructions per wave per tile
-constexpr int CST = 64 + 8;                     // staged C row stride (bf16)
 constexpr int BBYTES = 64 * 576 * 2;           // resident weights
 constexpr int BI = BBYTES / 1024;               // 72 DMA instructions
-static_assert(TILE * CST * 2 <= HBYTES, "C tile must fit a halo buffer");
 static_assert(BBYTES + 2 * HBYTES <= 160 * 1024, "LDS budget");
 }  // namespace c64
 
-template <bool DGRAD, bool STATS>
+// Output layout trick (no LDS round trip in the epilogue): the MFMA is issued as
+// D = W x X^T, so a lane's accumulators hold CHANNELS of one pixel instead of pixels of one
+// channel. The weight rows are staged in LDS in a permuted channel order, perm(n) =
+// ((n >> 2) & 3) * 16 + (n >> 4) * 4 + (n & 3), which makes lane l (q = l >> 4) of every 16x16
+// tile ni hold output channels q*16 + ni*4 + [0, 4): over the 4 tiles, 16 consecutive channels of
+// pixel (l & 15) — two 16-byte global stores straight from the accumulators. (The previous
+// epilogue staged the bf16 tile through LDS with 64 two-byte writes per lane and two barriers.)
+// The next tile's halo DMA is issued one 1 KiB piece per K-step inside the MFMA loop (an LDS-DMA
+// piece costs ~60-185 issue cycles; issued back-to-back at tile start with one wave per SIMD
+// they idled the matrix core).
+__device__ __forceinline__ int c64_perm(int n) { return ((n >> 2) & 3) * 16 + (n >> 4) * 4 + (n & 3); }
+
+template <bool DGRAD, bool STATS, bool PROF = false>
 __global__ __launch_bounds__(256)
 void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
+                        bf16* __restrict__ Y, float* __restrict__ stats,
+                        const bf16* __restrict__ addend, const C64Geom g) {
+  using namespace c64;
+  __shared__ __attribute__((aligned(16))) char smem[BBYTES + 2 * HBYTES + 1024];
+  char* const Bs = smem + 2 * HBYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid;                            // 64 pixels (2 image rows) x 64 channels
+  const int q = lane >> 4;                       // this lane's 16-channel group
+  const int tiles_per_img = g.H / ROWS;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A, g.a_bytes);
+
+  // ---- DMA slots: halo rows hr = 8*i + (lane>>3), fixed (j, c) per lane and slot ----
+  int s_jc[SLOTS], s_ch[SLOTS];
+#pragma unroll
+  for (int k = 0; k < SLOTS; ++k) {
+    const int i = wid + NW * k;
+    const int hr = 8 * i + (lane >> 3);
+    const int j = hr / W2, c = hr - j * W2;
+    s_jc[k] = (hr < HROWS) ? ((j << 8) | c) : -1;
+    s_ch[k] = ((lane & 7) ^ (hr & 7)) << 4;       // logical chunk fetched into physical (lane&7)
+  }
+  // branch-free (selects only, so it does not split the K-step's scheduling region): slots past
+  // the halo (i >= HI) write their zeros into a 1 KiB dummy area behind the weights
+  auto issue_piece = [&](int n, int h0, int buf, int k) {
+    const int i = wid + NW * k;
+    const int ih = h0 + (s_jc[k] >> 8) - 1, iw = (s_jc[k] & 0xff) - 1;
+    const bool ok = (s_jc[k] >= 0) & ((uint32_t)ih < (uint32_t)g.H) & ((uint32_t)iw < (uint32_t)W);
+    const uint32_t off = ok ? (uint32_t)((((n * g.H + ih) * W + iw) * 64) * 2 + s_ch[k]) : kOOB;
+    dma16(rsA, i < HI ? smem + buf * HBYTES + i * 1024 : smem + 2 * HBYTES + BBYTES, off);
+  };
+
+  if (blockIdx.x < g.tiles) {
+    const int n0 = blockIdx.x / tiles_per_img;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) issue_piece(n0, (blockIdx.x - n0 * tiles_per_img) * ROWS, 0, k);
+  }
+
+  // ---- weights -> LDS once: LDS row n holds output channel perm(n); 72 chunks of 8 K-values;
+  // physical chunk pc holds logical chunk (pc & ~7) | ((pc ^ n) & 7). K order = (tap, input
+  // channel). ----
+  {
+    const __amdgpu_buffer_rsrc_t rsW = make_rsrc(Wm, BBYTES);
+    for (int i = wid; i < BI; i += NW) {
+      const int qq = i * 64 + lane;
+      const int n = qq / 72, pc = qq - n * 72;
+      const int lc = (pc & ~7) | ((pc ^ n) & 7);
+      const int tap = lc >> 3, c8 = lc & 7;
+      const int src_tap = DGRAD ? 8 - tap : tap;
+      dma16(rsW, Bs + i * 1024, (uint32_t)((c64_perm(n) * 576 + src_tap * 64 + c8 * 8) * 2));
+    }
+  }
+
+  // per-lane fragment byte offsets (even 32-channel half): halo row R of tap (kh, kw) for pixel
+  // (2*wm + (mi>>1), (mi&1)*16 + l&15) with its XOR-swizzled 16-byte chunk; weight row nn
+  const int kq = lane >> 4;                      // 8-channel chunk within a 32-channel half
+  // (fragment mi | 1 is 16 halo rows after mi & ~1: same swizzle key, +2048 bytes)
+  int aoff[9][2], boff[4];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh) {
+      const int R = (2 * wm + mh + tap / 3) * W2 + (lane & 15) + tap % 3;
+      aoff[tap][mh] = R * 128 + ((kq ^ (R & 7)) << 4);
+    }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int nn = ni * 16 + (lane & 15);
+    boff[ni] = nn * 1152 + ((kq ^ (nn & 7)) << 4);
+  }
+
+  // per-lane BatchNorm sums of channels q*16 + e, accumulated over every tile (forward)
+  float st_s[16], st_q[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) st_s[e] = st_q[e] = 0.f;
+  // fused BN-backward reduce (dgrad): sums of dz and dz * xhat of channels q*16 + e
+  const bool bnf = DGRAD && g.bn_part != nullptr;
+  float bs1[16], bs2[16], bmean[16], bistd[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    bs1[e] = bs2[e] = 0.f;
+    bmean[e] = bnf ? g.bn_aux[q * 16 + e] : 0.f;
+    bistd[e] = bnf ? g.bn_aux[64 + q * 16 + e] : 0.f;
+  }
+
+  // Deferred epilogue: tile t's accumulators are stored (and reduced into the BN sums) during
+  // K-steps 11, 13, 15, 17 of tile t+1, one 16-pixel fragment row per step, in the MFMA
+  // shadow (one wave per SIMD: run after the K loop it idled the matrix core for ~1.8k cycles
+  // per tile). Two accumulator sets alternate between tiles (the tile loop is unrolled by two).
+  // Its dgrad operands (residual addend, BN input y, ReLU mask) are loaded at step 0.
+  constexpr int STORES = 8;                      // global stores per lane per tile (4 px x 2)
+  uint4 pre_a[4][2], pre_y[4][2];
+  uint32_t pre_m[4];
+  auto pre_load = [&](size_t pix0p) {
+    if constexpr (DGRAD) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const size_t o = (pix0p + wm * 64 + mi * 16 + (lane & 15)) * 64 + q * 16;
+        if (addend) {
+          pre_a[mi][0] = *reinterpret_cast<const uint4*>(addend + o);
+          pre_a[mi][1] = *reinterpret_cast<const uint4*>(addend + o + 8);
+        }
+        if (bnf) {
+          pre_y[mi][0] = *reinterpret_cast<const uint4*>(g.bn_y + o);
+          pre_y[mi][1] = *reinterpret_cast<const uint4*>(g.bn_y + o + 8);
+          pre_m[mi] = *reinterpret_cast<const uint16_t*>(g.bn_mask + (o >> 3));
+        }
+      }
+    }
+  };
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  auto epi_part = [&](f32x4 (&A)[4][4], int mi, size_t pix0p) {
+    // lane holds channels q*16 + [0,16) of pixel wm*64 + mi*16 + (lane&15)
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = A[mi][e >> 2][e & 3];
+    if constexpr (STATS) {
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {   // packed f32 adds / FMAs (no MFMA to share issue with)
+        f32x2 x = {v[e], v[e + 1]};
+        f32x2 s2 = {st_s[e], st_s[e + 1]}, q2 = {st_q[e], st_q[e + 1]};
+        s2 += x;
+        q2 += x * x;
+        st_s[e] = s2.x;
+        st_s[e + 1] = s2.y;
+        st_q[e] = q2.x;
+        st_q[e + 1] = q2.y;
+      }
+    }
+    uint4 o0 = pack8(v), o1 = pack8(v + 8);
+    if constexpr (DGRAD) {
+      if (addend) {
+        float a2[16], b2[16];
+        unpack8(o0, a2);
+        unpack8(o1, a2 + 8);
+        unpack8(pre_a[mi][0], b2);
+        unpack8(pre_a[mi][1], b2 + 8);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) a2[e] += b2[e];
+        o0 = pack8(a2);
+        o1 = pack8(a2 + 8);
+      }
+      if (bnf) {
+        float f[16], yy[16];
+        unpack8(o0, f);
+        unpack8(o1, f + 8);
+        unpack8(pre_y[mi][0], yy);
+        unpack8(pre_y[mi][1], yy + 8);
+        const uint32_t m = pre_m[mi];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
+          bs1[e] += dz;
+          bs2[e] += dz * (yy[e] - bmean[e]) * bistd[e];
+        }
+      }
+    }
+    bf16* dst = Y + (pix0p + wm * 64 + mi * 16 + (lane & 15)) * 64 + q * 16;
+    *reinterpret_cast<uint4*>(dst) = o0;
+    *reinterpret_cast<uint4*>(dst + 8) = o1;
+  };
+
+  // (dgrad keeps the epilogue after its K loop: its fused addend / BN-reduce operands and sums
+  // with a second accumulator set exceed the 512 registers)
+  constexpr bool DEFER = !DGRAD;
+  auto pix0_of = [&](int t) {
+    const int n = t / tiles_per_img, h0 = (t - n * tiles_per_img) * ROWS;
+    return ((size_t)n * g.H + h0) * W;
+  };
+  auto tile_body = [&](int t, int it, f32x4 (&Acc)[4][4], f32x4 (&Prev)[4][4], bool have_prev,
+                       size_t pix0p) {
+    const int buf = it & 1;
+    // this tile's halo landed (every piece was issued before the previous tile's 8 deferred
+    // stores, which may stay in flight)
+    wait_vmcnt<STORES>();
+    raw_barrier();
+    int64_t* pst = nullptr;
+    if constexpr (PROF) {
+      pst = g.prof + ((size_t)(blockIdx.x * 4 + wid) * 16 + (it & 15)) * 4;
+      const int64_t t0 = (int64_t)__builtin_amdgcn_s_memtime();
+      if (lane == 0) pst[0] = t0;
+    }
+    const char* S = smem + buf * HBYTES;
+    const int tn = t + (int)gridDim.x;
+    const int nn_img = tn / tiles_per_img, nn_h0 = (tn - nn_img * tiles_per_img) * ROWS;
+    if (DEFER && have_prev) pre_load(pix0p);
+    if (!DEFER) pre_load(pix0_of(t));
+
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) Acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // K loop: step s = (tap s>>1, 32-channel half s&1). The fragments of step s+1 (separate
+    // registers) are read while step s's 16 MFMAs run, interleaved one ds_read per MFMA
+    // (sched_group_barrier): with one wave per SIMD, reads issued as a block after the MFMAs
+    // cost their full issue time every step. Addresses are precomputed per (tap, fragment); the
+    // odd half flips bit 6 (chunk ^ 4) and the tap adds 128 B to the weight row offset.
+    auto load_step = [&](int st, bf16x8* af, bf16x8* bv) {
+      const int tap = st >> 1, hx = (st & 1) << 6;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+        af[mi] = *reinterpret_cast<const bf16x8*>(S + (aoff[tap][mi >> 1] ^ hx) + (mi & 1) * 2048);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        bv[ni] = *reinterpret_cast<const bf16x8*>(Bs + (boff[ni] ^ hx) + tap * 128);
+    };
+    bf16x8 fa[2][4], fb[2][4];
+    load_step(0, fa[0], fb[0]);
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {
+      const int cur = st & 1;
+      // one scheduling region per step: {DMA piece, reads of step st+1, MFMAs of step st}
+      __builtin_amdgcn_sched_barrier(0);
+      // (past the last tile the offsets fall outside the input: the pieces land zeros)
+      if (st < SLOTS) issue_piece(nn_img, nn_h0, buf ^ 1, st);
+      if (st + 1 < 18) load_step(st + 1, fa[cur ^ 1], fb[cur ^ 1]);
+      // (no s_setprio here: it is a scheduling boundary and would keep the reads out of the
+      // MFMA region; with one wave per SIMD priority has nothing to arbitrate)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          Acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][ni], fa[cur][mi], Acc[mi][ni], 0, 0, 0);
+      if (st + 1 < 18) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (DEFER && st >= 11 && (st & 1) && have_prev) epi_part(Prev, (st - 11) >> 1, pix0p);
+    }
+    if constexpr (!DEFER) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) epi_part(Acc, mi, pix0_of(t));
+    }
+    if constexpr (PROF) {
+      const int64_t t1 = (int64_t)__builtin_amdgcn_s_memtime();
+      if (lane == 0) pst[1] = t1;
+      if (lane == 0) pst[2] = t1;
+    }
+  };
+  f32x4 accA[4][4], accB[4][4];
+  wait_vmcnt<0>();                                // weights + first halo
+  {
+    int t = blockIdx.x, it = 0;
+    bool have_prev = false;
+    size_t pix0p = 0;
+    while (t < g.tiles) {
+      tile_body(t, it, accA, accB, have_prev, pix0p);
+      have_prev = true;
+      pix0p = pix0_of(t);
+      t += gridDim.x;
+      ++it;
+      if (t >= g.tiles) {                         // last tile: its epilogue now
+        if constexpr (DEFER) {
+          pre_load(pix0p);
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) epi_part(accA, mi, pix0p);
+        }
+        break;
+      }
+      if constexpr (DEFER) {
+        tile_body(t, it, accB, accA, have_prev, pix0p);
+      } else {
+        tile_body(t, it, accA, accB, have_prev, pix0p);
+      }
+      pix0p = pix0_of(t);
+      t += gridDim.x;
+      ++it;
+      if (t >= g.tiles) {
+        if constexpr (DEFER) {
+          pre_load(pix0p);
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) epi_part(accB, mi, pix0p);
+        }
+        break;
+      }
+    }
+  }
+
+  // ---- per-block channel sums: lanes of one 16-lane group share channels q*16 + e ----
+  if (STATS || bnf) {
+    float* s1 = STATS ? st_s : bs1;
+    float* s2 = STATS ? st_q : bs2;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+#pragma unroll
+      for (int x = 1; x < 16; x <<= 1) {
+        s1[e] += __shfl_xor(s1[e], x, 64);
+        s2[e] += __shfl_xor(s2[e], x, 64);
+      }
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [4 waves][64 ch][2]
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        red[(wm * 64 + q * 16 + e) * 2 + 0] = s1[e];
+        red[(wm * 64 + q * 16 + e) * 2 + 1] = s2[e];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {   // fixed order: deterministic per block
+        a += red[(w * 64 + tid) * 2 + 0];
+        b += red[(w * 64 + tid) * 2 + 1];
+      }
+      float* dst = STATS ? stats : g.bn_part;
+      stat_out(dst, blockIdx.x, g.shards, 128, tid, a);
+      stat_out(dst, blockIdx.x, g.shards, 128, 64 + tid, b);
+    }
+  }
+}
+
+// round-2 version (LDS-staged epilogue, halo DMA issued at tile start): PCA_C64_V=1 (A/B)
+template <bool DGRAD, bool STATS>
+__global__ __launch_bounds__(256)
+void conv3x3_c64_v1_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
                         bf16* __restrict__ Y, float* __restrict__ stats,
                         const bf16* __restrict__ addend, const C64Geom g) {
   using namespace c64;
@@ -122,7 +461,8 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
     bistd[q] = bnf ? g.bn_aux[64 + (tid & 7) * 8 + q] : 0.f;
   }
 
-  constexpr int STORES = (TILE * 8) / 256;      // global stores per thread per tile
+  constexpr int STORES = (TILE * 8) / 256;
+  constexpr int CST = 64 + 8;      // global stores per thread per tile
   wait_vmcnt<0>();                                // weights + first halo
   int it = 0;
   for (int t = blockIdx.x; t < g.tiles; t += gridDim.x, ++it) {
@@ -321,6 +661,11 @@ static int c64_grid(int tiles) {
 }
 
 // shape gate (the caller falls back to the generic implicit GEMM otherwise)
+// diagnostics: when set, launches record per-wave tile stamps [grid][4][16][4] (int64) here
+static int64_t* g_c64_prof = nullptr;
+void c64_set_prof(int64_t* p) { g_c64_prof = p; }
+int c64_grid_size(int N, int H) { return c64_grid(N * H / 8); }
+
 bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                          int pad, int groups) {
   static const bool off = [] {
@@ -346,7 +691,34 @@ void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const 
   g.bn_aux = bn_aux;
   g.bn_part = dgrad ? bn_part : nullptr;
   g.shards = stat_shards();
+  g.prof = nullptr;
   const dim3 grid(c64_grid(g.tiles)), block(256);
+  static const int ver = [] {
+    const char* e = getenv("PCA_C64_V");
+    return e ? atoi(e) : 2;
+  }();
+  g.prof = g_c64_prof;
+  if (g.prof) {
+    if (dgrad)
+      hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, true>), grid, block, 0, st, a, w, y, nullptr,
+                         addend, g);
+    else
+      hipLaunchKernelGGL((conv3x3_c64_kernel<false, true, true>), grid, block, 0, st, a, w, y, stats,
+                         addend, g);
+    return;
+  }
+  if (ver == 1) {
+    if (dgrad)
+      hipLaunchKernelGGL((conv3x3_c64_v1_kernel<true, false>), grid, block, 0, st, a, w, y, nullptr,
+                         addend, g);
+    else if (stats)
+      hipLaunchKernelGGL((conv3x3_c64_v1_kernel<false, true>), grid, block, 0, st, a, w, y, stats,
+                         addend, g);
+    else
+      hipLaunchKernelGGL((conv3x3_c64_v1_kernel<false, false>), grid, block, 0, st, a, w, y, nullptr,
+                         addend, g);
+    return;
+  }
   if (dgrad)
     hipLaunchKernelGGL((conv3x3_c64_kernel<true, false>), grid, block, 0, st, a, w, y, nullptr,
                        addend, g);
