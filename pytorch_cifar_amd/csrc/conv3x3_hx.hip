@@ -1,0 +1,432 @@
+// Halo-staged implicit GEMM for the 3x3 / stride-1 / pad-1 convolutions of ResNet layers 2-4
+// (reference models/resnet.py:23-27, 61-64 on 16x16 / 8x8 / 4x4 maps with 128-512 channels;
+// SURVEY §2.8 K1/K2), forward and stride-1 dgrad.
+//
+// Why a separate kernel: in the generic implicit GEMM (conv_mfma.hip) every K-step re-gathers a
+// tap-shifted copy of the input tile through LDS-DMA, so a 128x128 tile moves 32 KiB (32 DMA
+// pieces) per 128x128x64 MACs. An LDS-DMA piece costs ~60-185 issue cycles of its wave, and at
+// that rate the DMA issue, not the matrix core, bounds the kernel (~30-35 % MFMA busy,
+// profiles/pmc_top10_r3.md). Here a workgroup owns whole images (BM = 128 / 256 pixels) and, per
+// 64-channel input chunk, stages the images' zero-padded halo ONCE ((W+2)^2 rows per image); the
+// nine taps read it at row offsets kh*(W+2) + kw. Per K-step only the weight tile (BN rows x
+// 128 B) is staged: ~2.3x fewer DMA pieces per MAC than the 256x128 generic tile.
+//
+// Layout (cf. conv3x3_c64.hip, the 64-channel layer-1 version with resident weights):
+//   * WM x WN waves, each 64 pixels x 64 output channels (4 x 4 16x16x32 MFMA tiles);
+//   * the MFMA is issued as W x X^T with the weight rows staged in a permuted channel order, so a
+//     lane's accumulators are 16 consecutive channels of one pixel: epilogue stores (bf16, and
+//     the fused dgrad addend / BatchNorm-backward sums) go straight from registers;
+//   * K loop = chunk (64 input channels) x tap (9) x half (32 channels); the weight tile of the
+//     next tap and the halo of the next chunk (or of the next tile's first chunk) stream in while
+//     the current one computes: one barrier + counted vmcnt per tap, weight ring of 2, halo ring
+//     of 2;
+//   * dgrad: the same kernel on dY with the transposed weights read at the mirrored tap 8 - t.
+#include "mfma_util.h"
+
+namespace pca {
+
+struct HxGeom {
+  int N;            // images
+  int CA;           // channels of the gathered tensor (x: Cin, dgrad: dY's Cout)
+  int CO;           // channels produced (forward: Cout, dgrad: Cin)
+  int KC;           // 64-channel chunks of CA
+  int tiles;        // N * H * W / BM
+  uint32_t a_bytes, b_bytes;
+  int shards;       // stats / bn_part: 0 = slab rows, >0 = sharded atomic accumulator
+  // dgrad: fused backward reduce of the BN(+ReLU) that produced this conv's input (bn_part != 0)
+  const bf16* bn_y;
+  const uint8_t* bn_mask;
+  const float* bn_aux;
+  float* bn_part;
+};
+
+__device__ __forceinline__ int hx_perm(int n) { return ((n >> 2) & 3) * 16 + (n >> 4) * 4 + (n & 3); }
+
+template <int W, int IMGS, int WM, int WN>
+struct HxShape {
+  static constexpr int NW = WM * WN;
+  static constexpr int BM = WM * 64, BN = WN * 64;
+  static constexpr int W2 = W + 2;
+  static constexpr int IMG_ROWS = W2 * W2;
+  static constexpr int HROWS = IMGS * IMG_ROWS;
+  static constexpr int HI = (HROWS + 7) / 8;          // halo DMA pieces per chunk
+  static constexpr int HBYTES = HI * 1024;
+  static constexpr int HS = (HI + NW - 1) / NW;       // halo pieces per wave per chunk
+  static constexpr int BPC = BN / 8;                  // weight pieces per tap
+  static constexpr int BS = BPC / NW;                 // ... per wave
+  static constexpr int BBYTES = BN * 128;
+  static constexpr int LDS = 2 * HBYTES + 2 * BBYTES + 1024 + BN * 8;
+  static_assert(IMGS * W * W == BM, "a tile is whole images");
+  static_assert(BPC % NW == 0, "weight pieces split evenly over the waves");
+  // halo piece k is issued during tap k % 8 (taps 0..7; tap 8 stages the next chunk's weights)
+  static constexpr int pieces_at(int tap) { return tap >= 8 ? 0 : (HS - tap + 7) / 8; }
+  static_assert(HS <= 16, "at most two halo pieces per tap");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <int W, int IMGS, int WM, int WN, bool DGRAD, bool STATS>
+__global__ __launch_bounds__(WM * WN * 64)
+void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
+                       bf16* __restrict__ Y, float* __restrict__ stats,
+                       const bf16* __restrict__ addend, const float* __restrict__ bias,
+                       const HxGeom g) {
+  using SH = HxShape<W, IMGS, WM, WN>;
+  constexpr int NW = SH::NW, BM = SH::BM, BN = SH::BN, W2 = SH::W2;
+  constexpr int HB = SH::HBYTES, BB = SH::BBYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SH::LDS];
+  char* const Hs = smem;                       // [2][HBYTES] halo ring
+  char* const Bs = smem + 2 * HB;              // [2][BBYTES] weight ring
+  char* const dummy = smem + 2 * HB + 2 * BB;  // landing place of padding DMA slots
+  float* const auxs = reinterpret_cast<float*>(dummy + 1024);   // dgrad: BN mean | istd
+
+  typedef __attribute__((address_space(3))) const char lds_char;
+  typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+  lds_char* const lds_base = (lds_char*)smem;   // fragment reads through explicit LDS pointers
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int q = lane >> 4, kq = lane >> 4;
+  const int nb0 = blockIdx.y * BN;             // first produced channel of this workgroup
+  const int KA = 9 * g.CA;                     // weight row length (elements)
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A, g.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(Bw, g.b_bytes);
+
+  // ---- halo DMA slots: halo row hr = 8*i + (lane>>3) of piece i = wid + NW*k ----
+  int s_px[SH::HS], s_ch[SH::HS];
+#pragma unroll
+  for (int k = 0; k < SH::HS; ++k) {
+    const int i = wid + NW * k;
+    const int hr = 8 * i + (lane >> 3);
+    const int img = hr / SH::IMG_ROWS, rem = hr - img * SH::IMG_ROWS;
+    const int jr = rem / W2, c = rem - jr * W2;
+    // packed (img, ih + 1, iw + 1) of the source pixel, -1 for padding rows
+    s_px[k] = (i < SH::HI && hr < SH::HROWS) ? ((img << 16) | (jr << 8) | c) : -1;
+    s_ch[k] = ((lane & 7) ^ (hr & 7)) << 4;    // logical chunk fetched into physical (lane&7)
+  }
+  // halo piece k of chunk `ch` of tile `t` into ring slot `hb`
+  auto halo_piece = [&](int t, int ch, int hb, int k) {
+    const int i = wid + NW * k;
+    const int sp = s_px[k];
+    const int n = t * IMGS + (sp >> 16);
+    const int ih = ((sp >> 8) & 0xff) - 1, iw = (sp & 0xff) - 1;
+    const bool ok = (sp >= 0) & (n < g.N) & ((uint32_t)ih < (uint32_t)W) & ((uint32_t)iw < (uint32_t)W);
+    const uint32_t off = ok ? (uint32_t)(((((n * W + ih) * W + iw) * g.CA) + ch * 64) * 2 + s_ch[k]) : kOOB;
+    dma16(rsA, smem + (i < SH::HI ? hb * HB + i * 1024 : 2 * HB + 2 * BB), off);
+  };
+  // weight tile of (tap, chunk) into ring slot `bb`: LDS row r = 64-channel block r/64 of this
+  // workgroup, channel hx_perm(r % 64) within it; 16-byte chunks XOR-swizzled by (r & 7)
+  int b_row[SH::BS];
+#pragma unroll
+  for (int k = 0; k < SH::BS; ++k) {
+    const int r = 8 * (wid + NW * k) + (lane >> 3);
+    const int ch = nb0 + (r & ~63) + hx_perm(r & 63);
+    b_row[k] = (ch * KA + (((lane & 7) ^ (r & 7)) << 3)) * 2;
+  }
+  auto b_tile = [&](int tap, int ch, int bb) {
+    const int src_tap = DGRAD ? 8 - tap : tap;
+    const int delta = (src_tap * g.CA + ch * 64) * 2;
+#pragma unroll
+    for (int k = 0; k < SH::BS; ++k)
+      dma16(rsB, Bs + bb * BB + (wid + NW * k) * 1024, (uint32_t)(b_row[k] + delta));
+  };
+
+  // ---- fragment addressing ----
+  // A (pixels): tile pixel p = wm*64 + mi*16 + (lane&15) -> halo row of tap (0,0)
+  int rb[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int p = wm * 64 + mi * 16 + (lane & 15);
+    const int img = p / (W * W), r = p - img * (W * W);
+    rb[mi] = img * SH::IMG_ROWS + (r / W) * W2 + (r % W);
+  }
+  // B (weights): LDS row wn*64 + ni*16 + (lane&15)
+  int boff[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int nn = wn * 64 + ni * 16 + (lane & 15);
+    boff[ni] = nn * 128 + ((kq ^ (nn & 7)) << 4);
+  }
+
+  // per-lane BatchNorm sums of channels nb0 + wn*64 + q*16 + e (forward stats / dgrad reduce)
+  const bool bnf = DGRAD && g.bn_part != nullptr;
+  float s1[16], s2[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) s1[e] = s2[e] = 0.f;
+  const int ch_lane = nb0 + wn * 64 + q * 16;  // first of this lane's 16 output channels
+  if (bnf) {   // the block's BN mean / istd once into LDS (read per element in the epilogue)
+    for (int i = tid; i < 2 * BN; i += NW * 64)
+      auxs[i] = g.bn_aux[(i >= BN ? g.CO : 0) + nb0 + (i % BN)];
+    __syncthreads();
+  }
+
+  constexpr int STORES = 8;                    // global stores per lane per tile
+  // prologue: first tile's chunk-0 halo and tap-0 weights
+  if ((int)blockIdx.x < g.tiles) {
+#pragma unroll
+    for (int k = 0; k < SH::HS; ++k) halo_piece(blockIdx.x, 0, 0, k);
+    b_tile(0, 0, 0);
+  }
+  wait_vmcnt<0>();
+
+  int hc = 0;   // global chunk counter (halo ring slot = hc & 1)
+  int bc = 0;   // global tap counter (weight ring slot = bc & 1)
+  for (int t = blockIdx.x; t < g.tiles; t += gridDim.x) {
+    const int tn = t + (int)gridDim.x;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 pre_a[4][2], pre_y[4][2];
+    uint32_t pre_m[4];
+
+    for (int ch = 0; ch < g.KC; ++ch, ++hc) {
+      const bool last_chunk = ch + 1 == g.KC;
+      // what streams in during this chunk: the next chunk's halo (or the next tile's first)
+      const int h_t = last_chunk ? tn : t, h_ch = last_chunk ? 0 : ch + 1;
+      const int Soff = (hc & 1) * HB;          // this chunk's halo slot (byte offset in smem)
+      // (a runtime tap loop: unrolled, the 9 taps' fragment offsets were hoisted as loop
+      // invariants and pushed the 8-wave variants past 256 registers into spills)
+#pragma unroll 1
+      for (int tap = 0; tap < 9; ++tap, ++bc) {
+        // weights of this tap were issued one tap ago; after them came at most one halo piece,
+        // or, at a tile's first tap, the previous tile's epilogue stores (may stay in flight)
+        if (tap == 0) {
+          if (ch == 0) wait_vmcnt<STORES>();
+          else wait_vmcnt<0>();
+        } else {
+          switch (SH::pieces_at(tap - 1)) {   // wave-uniform
+            case 0: wait_vmcnt<0>(); break;
+            case 1: wait_vmcnt<1>(); break;
+            default: wait_vmcnt<2>(); break;
+          }
+        }
+        raw_barrier();
+        // next tap's weights (past the last tile: harmless re-load of real rows)
+        if (tap < 8) b_tile(tap + 1, ch, (bc + 1) & 1);
+        else b_tile(0, last_chunk ? 0 : ch + 1, (bc + 1) & 1);
+#pragma unroll
+        for (int k = 0; k < SH::HS; ++k)
+          if ((k & 7) == tap) halo_piece(h_t, h_ch, (hc + 1) & 1, k);   // wave-uniform
+        if constexpr (DGRAD) {
+          if (last_chunk && tap == 8) {
+            // epilogue operands (residual-gradient addend; BN input y + ReLU mask), read
+            // behind this tap's MFMAs
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+              const size_t o = ((size_t)t * BM + wm * 64 + mi * 16 + (lane & 15)) * g.CO + ch_lane;
+              if (addend) {
+                pre_a[mi][0] = *reinterpret_cast<const uint4*>(addend + o);
+                pre_a[mi][1] = *reinterpret_cast<const uint4*>(addend + o + 8);
+              }
+              if (bnf) {
+                pre_y[mi][0] = *reinterpret_cast<const uint4*>(g.bn_y + o);
+                pre_y[mi][1] = *reinterpret_cast<const uint4*>(g.bn_y + o + 8);
+                pre_m[mi] = *reinterpret_cast<const uint16_t*>(g.bn_mask + (o >> 3));
+              }
+            }
+          }
+        }
+        const int Boff = 2 * HB + (bc & 1) * BB; // this tap's weight slot
+        const int toff = (tap / 3) * W2 + (tap % 3);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 fa[4], fb[4];
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            const int R = rb[mi] + toff;
+            const int o = Soff + R * 128 + ((((h << 2) | kq) ^ (R & 7)) << 4);
+            fa[mi] = *reinterpret_cast<const lds_bf16x8*>(lds_base + o);
+          }
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            fb[ni] = *reinterpret_cast<const lds_bf16x8*>(lds_base + Boff + (boff[ni] ^ (h << 6)));
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ni], fa[mi], acc[mi][ni], 0, 0, 0);
+        }
+      }
+    }
+
+    // ---- epilogue: lane holds channels ch_lane + [0,16) of tile pixel wm*64 + mi*16 + lane&15 ----
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = acc[mi][e >> 2][e & 3];
+      if (bias) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] += bias[ch_lane + e];
+      }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          s1[e] += v[e];
+          s2[e] += v[e] * v[e];
+        }
+      }
+      uint4 o0 = pack8(v), o1 = pack8(v + 8);
+      if constexpr (DGRAD) {
+        if (addend) {
+          float a2[16], b2[16];
+          unpack8(o0, a2);
+          unpack8(o1, a2 + 8);
+          unpack8(pre_a[mi][0], b2);
+          unpack8(pre_a[mi][1], b2 + 8);
+#pragma unroll
+          for (int e = 0; e < 16; ++e) a2[e] += b2[e];
+          o0 = pack8(a2);
+          o1 = pack8(a2 + 8);
+        }
+        if (bnf) {
+          float f[16], yy[16];
+          unpack8(o0, f);
+          unpack8(o1, f + 8);
+          unpack8(pre_y[mi][0], yy);
+          unpack8(pre_y[mi][1], yy + 8);
+          const uint32_t m = pre_m[mi];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
+            s1[e] += dz;
+            const int c = ch_lane - nb0 + e;
+            s2[e] += dz * (yy[e] - auxs[c]) * auxs[BN + c];
+          }
+        }
+      }
+      bf16* dst = Y + ((size_t)t * BM + wm * 64 + mi * 16 + (lane & 15)) * g.CO + ch_lane;
+      *reinterpret_cast<uint4*>(dst) = o0;
+      *reinterpret_cast<uint4*>(dst + 8) = o1;
+    }
+  }
+
+  // ---- per-block channel sums: the 16 lanes of a group share channels; WM waves per column ----
+  if (STATS || bnf) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+#pragma unroll
+      for (int x = 1; x < 16; x <<= 1) {
+        s1[e] += __shfl_xor(s1[e], x, 64);
+        s2[e] += __shfl_xor(s2[e], x, 64);
+      }
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        red[(wm * BN + wn * 64 + q * 16 + e) * 2 + 0] = s1[e];
+        red[(wm * BN + wn * 64 + q * 16 + e) * 2 + 1] = s2[e];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {   // fixed order: deterministic per block
+        a += red[(w * BN + tid) * 2 + 0];
+        b += red[(w * BN + tid) * 2 + 1];
+      }
+      float* dst = STATS ? stats : g.bn_part;
+      stat_out(dst, blockIdx.x, g.shards, 2 * g.CO, nb0 + tid, a);
+      stat_out(dst, blockIdx.x, g.shards, 2 * g.CO, g.CO + nb0 + tid, b);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------
+int stat_shards();
+
+static int hx_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+// shape gate: 3x3 s1 p1, square 16 / 8 / 4 maps, channel counts multiples of 128
+bool conv_hx_applicable(int N, int H, int W, int CA, int CO, int KH, int KW, int stride, int pad,
+                        int groups) {
+  static const bool off = [] {
+    const char* e = getenv("PCA_CONV_HX");
+    return e && e[0] == '0';
+  }();
+  if (off || KH != 3 || KW != 3 || stride != 1 || pad != 1 || groups != 1 || H != W) return false;
+  if (CA % 64 || CO % 128) return false;
+  const int bm = W == 4 ? 128 : 256;
+  return (W == 16 || W == 8 || W == 4) && (N * H * W) % bm == 0;
+}
+
+template <int W, int IMGS, int WM, int WN, bool DGRAD, bool STATS>
+static int hx_occ() {
+  static int occ = 0;
+  if (occ == 0)
+    occ = blocks_per_cu((const void*)conv3x3_hx_kernel<W, IMGS, WM, WN, DGRAD, STATS>, WM * WN * 64,
+                        "conv3x3_hx");
+  return occ;
+}
+
+template <int W, int IMGS, int WM, int WN>
+static int hx_grid_x(const HxGeom& g, int nblocks) {
+  const int slots = hx_occ<W, IMGS, WM, WN, false, true>() * hx_cus();
+  int gx = std::max(1, slots / std::max(1, nblocks));
+  gx = std::min(gx, g.tiles);
+  const int per = cdiv(g.tiles, gx);
+  return cdiv(g.tiles, per);
+}
+
+template <int W, int IMGS, int WM, int WN>
+static int hx_run(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
+                  const float* bias, const HxGeom& g, bool dgrad, hipStream_t st, bool launch) {
+  constexpr int BN = WN * 64;
+  const int nblocks = g.CO / BN;
+  const int gx = hx_grid_x<W, IMGS, WM, WN>(g, nblocks);
+  if (!launch) return gx;
+  const dim3 grid(gx, nblocks), block(WM * WN * 64);
+  if (dgrad)
+    hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, true, false>), grid, block, 0, st, a, b,
+                       y, nullptr, addend, nullptr, g);
+  else if (stats)
+    hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, false, true>), grid, block, 0, st, a, b,
+                       y, stats, nullptr, bias, g);
+  else
+    hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, false, false>), grid, block, 0, st, a, b,
+                       y, nullptr, nullptr, bias, g);
+  return gx;
+}
+
+// launch (or, with launch = false, only size: returns grid.x = the BN-statistics slab rows)
+int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
+                   const float* bias, int N, int H, int CA, int CO, bool dgrad, hipStream_t st,
+                   const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
+                   bool launch) {
+  HxGeom g;
+  g.N = N;
+  g.CA = CA;
+  g.CO = CO;
+  g.KC = CA / 64;
+  g.a_bytes = (uint32_t)((size_t)N * H * H * CA * 2);
+  g.b_bytes = (uint32_t)((size_t)CO * 9 * CA * 2);
+  g.shards = stat_shards();
+  g.bn_y = bn_y;
+  g.bn_mask = bn_mask;
+  g.bn_aux = bn_aux;
+  g.bn_part = dgrad ? bn_part : nullptr;
+  switch (H) {
+    case 16: g.tiles = N; return hx_run<16, 1, 4, 2>(a, b, y, stats, addend, bias, g, dgrad, st, launch);
+    case 8: g.tiles = N / 4; return hx_run<8, 4, 4, 2>(a, b, y, stats, addend, bias, g, dgrad, st, launch);
+    default: g.tiles = N / 8; return hx_run<4, 8, 2, 2>(a, b, y, stats, addend, bias, g, dgrad, st, launch);
+  }
+}
+
+}  // namespace pca

@@ -94,7 +94,7 @@ constexpr bool halo_fits() {
   return 3 * halo_stage_bytes<W, MB, KP>() <= 160 * 1024;
 }
 
-template <int W, int MB, int WM, int WN, int KP>
+template <int W, int MB, int WM, int WN, int KP, int TG = 9>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wgrad_halo_kernel(const bf16* __restrict__ X,
                                                                   const bf16* __restrict__ DY,
                                                                   float* __restrict__ out,
@@ -107,7 +107,11 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   constexpr int A_OFF = SH::HBYTES;              // dY blocks follow the halo image
   constexpr int J_OFF = A_OFF + MB * KP * 128;   // junk KiB for the padding DMA slots
   constexpr int STAGE = J_OFF + 1024;
-  constexpr int BM = MB * 64, BN = 9 * 64;
+  // TG = 3: a workgroup owns one kernel row (3 taps) of the output tile, so the grid has 3x the
+  // tiles and needs 3x fewer pixel splits to fill the chip (slab traffic / 3; none at all when
+  // the tiles alone fill it, e.g. ResNet layer 4 on the 8-GPU shard)
+  static_assert(TG == 9 || TG == 3, "taps per workgroup");
+  constexpr int BM = MB * 64, BN = TG * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int T = SH::HI + DYI * MB;           // real DMA instructions per stage
@@ -123,7 +127,9 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   const int split = blockIdx.z % g.splits;
   const int grp = blockIdx.z / g.splits;
   const int m0 = blockIdx.x * BM;              // output channel tile (within group)
-  const int cib = blockIdx.y;                  // 64-channel input block
+  const int cinb = g.cin_g / 64;
+  const int cib = (int)blockIdx.y % cinb;      // 64-channel input block
+  const int tap0 = TG == 9 ? 0 : ((int)blockIdx.y / cinb) * 3;   // first tap of this row
   const int p_begin = split * g.chunk;
   const int p_end = min(g.P, p_begin + g.chunk);
 
@@ -239,7 +245,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const int n = wn * WTN + ni * 16;
-        const int tap = n >> 6, kh = tap / 3, kw = tap % 3;
+        const int tap = tap0 + (n >> 6), kh = tap / 3, kw = tap % 3;
         const int c0 = n & 63;
         const int cx = ((c0 >> 3) ^ (((kh * W2P / 8) & 1) ? 4 : 0)) << 4;
         const int rsh = (kh * W2P + kw) * 128;
@@ -279,7 +285,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = wn * WTN + ni * 16 + (lane & 15);
-      const int col = (n >> 6) * g.cin_g + cib * 64 + (n & 63);
+      const int col = (tap0 + (n >> 6)) * g.cin_g + cib * 64 + (n & 63);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + j;
@@ -296,8 +302,9 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
 // [wave][mi][ni][lane] float4 = rows m..m+3 of one column).
 struct HaloSlabMap {
   int TM, TN, WN, WTM, WTN, BM, BN;
-  int tiles_x, tiles_y;   // grid.x (output-channel tiles), grid.y (64-channel input blocks)
+  int tiles_x, tiles_y;   // grid.x (output-channel tiles), grid.y (input blocks x tap rows)
   int cout_g, cin_g, Ktot;
+  int TG;                 // taps per tile (9, or 3 = one kernel row)
 };
 
 // dW += sum_s slab[s] in a fixed order: a block owns 64 float4 slots; its L = blockDim/64 split
@@ -348,7 +355,9 @@ __global__ __launch_bounds__(1024) void halo_slab_reduce_kernel(const float4* __
   const int bx = (tile / mp.tiles_y) % mp.tiles_x;
   const int grp = tile / (mp.tiles_y * mp.tiles_x);
   const int n = wn * mp.WTN + ni * 16 + (lane & 15);
-  const int col = (n >> 6) * mp.cin_g + by * 64 + (n & 63);
+  const int cinb = mp.cin_g / 64;
+  const int tap0 = mp.TG == 9 ? 0 : (by / cinb) * 3;
+  const int col = (tap0 + (n >> 6)) * mp.cin_g + (by % cinb) * 64 + (n & 63);
   const int mb = bx * mp.BM + wm * mp.WTM + mi * 16 + (lane >> 4) * 4;
   const float v[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
@@ -409,22 +418,26 @@ static int halo_cus() {
   return n;
 }
 
-// X(cfg, MB, WM, WN, KP)
-#define PCA_HALO_CFGS(X) \
-  X(0, 1, 1, 4, 32)      \
-  X(1, 2, 2, 4, 32)      \
-  X(2, 1, 2, 4, 32)      \
-  X(3, 1, 2, 4, 64)      \
-  X(4, 2, 2, 4, 64)      \
-  X(5, 1, 2, 4, 128)     \
-  X(6, 1, 1, 4, 64)
-constexpr int kHaloCfgs = 7;
+// X(cfg, MB, WM, WN, KP, TG)
+#define PCA_HALO_CFGS(X)    \
+  X(0, 1, 1, 4, 32, 9)      \
+  X(1, 2, 2, 4, 32, 9)      \
+  X(2, 1, 2, 4, 32, 9)      \
+  X(3, 1, 2, 4, 64, 9)      \
+  X(4, 2, 2, 4, 64, 9)      \
+  X(5, 1, 2, 4, 128, 9)     \
+  X(6, 1, 1, 4, 64, 9)      \
+  X(7, 1, 2, 4, 64, 3)      \
+  X(8, 1, 1, 4, 64, 3)      \
+  X(9, 2, 2, 4, 64, 3)
+constexpr int kHaloCfgs = 10;
 
-template <int W, int MB, int WM, int WN, int KP>
+template <int W, int MB, int WM, int WN, int KP, int TG>
 static int halo_occupancy() {
   static int occ = 0;
   if (occ == 0) {
-occ = blocks_per_cu((const void*)wgrad_halo_kernel<W, MB, WM, WN, KP>, WM * WN * 64, "wgrad_halo");
+    occ = blocks_per_cu((const void*)wgrad_halo_kernel<W, MB, WM, WN, KP, TG>, WM * WN * 64,
+                        "wgrad_halo");
   }
   return occ;
 }
@@ -483,10 +496,10 @@ static int halo_select(const HaloGeom& g) {
   return g.cout_g <= 64 ? 0 : 1;
 }
 
-template <int W, int MB, int WM, int WN, int KP>
+template <int W, int MB, int WM, int WN, int KP, int TG>
 static int64_t halo_plan(HaloGeom& g) {
-  const int tiles = cdiv(g.cout_g, 64 * MB) * (g.cin_g / 64) * g.groups;
-  const int slots = halo_occupancy<W, MB, WM, WN, KP>() * halo_cus();
+  const int tiles = cdiv(g.cout_g, 64 * MB) * (g.cin_g / 64) * (9 / TG) * g.groups;
+  const int slots = halo_occupancy<W, MB, WM, WN, KP, TG>() * halo_cus();
   int splits = std::max(1, slots / tiles);
   splits = std::min(splits, std::max(1, cdiv(g.P, 256)));
   const int forced = wgrad_split_force();
@@ -501,21 +514,21 @@ static int64_t halo_plan(HaloGeom& g) {
   static const bool verbose = getenv("PCA_CONV_VERBOSE") != nullptr;
   if (verbose)
     fprintf(stderr, "[pca] halo wgrad W=%d MB=%d waves=%d KP=%d: occ=%d cus=%d tiles=%d splits=%d chunk=%d atomic=%d\n",
-            W, MB, WM * WN, KP, halo_occupancy<W, MB, WM, WN, KP>(), halo_cus(), tiles, splits, chunk,
-            g.atomic);
+            W, MB, WM * WN, KP, halo_occupancy<W, MB, WM, WN, KP, TG>(), halo_cus(), tiles, splits,
+            chunk, g.atomic);
   if (g.atomic) return 0;
-  return slab_ws_floats(splits, (int64_t)tiles * (64 * MB) * (9 * 64));
+  return slab_ws_floats(splits, (int64_t)tiles * (64 * MB) * (TG * 64));
 }
 
-template <int W, int MB, int WM, int WN, int KP>
+template <int W, int MB, int WM, int WN, int KP, int TG>
 static void launch_halo(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom g,
                         hipStream_t st) {
-  halo_plan<W, MB, WM, WN, KP>(g);
-  dim3 grid(cdiv(g.cout_g, 64 * MB), g.cin_g / 64, g.splits * g.groups);
-  hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP>), grid, dim3(WM * WN * 64), 0, st, x,
+  halo_plan<W, MB, WM, WN, KP, TG>(g);
+  dim3 grid(cdiv(g.cout_g, 64 * MB), (g.cin_g / 64) * (9 / TG), g.splits * g.groups);
+  hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP, TG>), grid, dim3(WM * WN * 64), 0, st, x,
                      dy, g.atomic ? dw : ws, g);
   if (g.atomic) return;
-  constexpr int BM = 64 * MB, BN = 9 * 64;
+  constexpr int BM = 64 * MB, BN = TG * 64;
   HaloSlabMap mp;
   mp.BM = BM;
   mp.BN = BN;
@@ -529,6 +542,7 @@ static void launch_halo(const bf16* x, const bf16* dy, float* dw, float* ws, Hal
   mp.cout_g = g.cout_g;
   mp.cin_g = g.cin_g;
   mp.Ktot = g.Ktot;
+  mp.TG = TG;
   const int64_t n4 = (int64_t)grid.x * grid.y * g.groups * (BM * BN / 4);
   int L = 1;   // split lanes per slot: a power of two <= min(16, splits)
   while (L < 16 && 2 * L <= g.splits) L *= 2;
@@ -541,11 +555,11 @@ template <int W>
 static int64_t halo_dispatch_w(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom& g,
                                hipStream_t st, bool plan_only) {
   switch (halo_select(g)) {
-#define PCA_CASE(C, MB, WM, WN, KP)                                    \
+#define PCA_CASE(C, MB, WM, WN, KP, TG)                                \
     case C:                                                            \
       if constexpr (halo_fits<W, MB, KP>()) {                          \
-        if (plan_only) return halo_plan<W, MB, WM, WN, KP>(g);         \
-        launch_halo<W, MB, WM, WN, KP>(x, dy, dw, ws, g, st);          \
+        if (plan_only) return halo_plan<W, MB, WM, WN, KP, TG>(g);     \
+        launch_halo<W, MB, WM, WN, KP, TG>(x, dy, dw, ws, g, st);      \
         return 0;                                                      \
       }                                                                \
       break;
@@ -555,8 +569,8 @@ static int64_t halo_dispatch_w(const bf16* x, const bf16* dy, float* dw, float* 
       break;
   }
   // (a configuration whose LDS stages do not fit this image width falls back to cfg 0)
-  if (plan_only) return halo_plan<W, 1, 1, 4, 32>(g);
-  launch_halo<W, 1, 1, 4, 32>(x, dy, dw, ws, g, st);
+  if (plan_only) return halo_plan<W, 1, 1, 4, 32, 9>(g);
+  launch_halo<W, 1, 1, 4, 32, 9>(x, dy, dw, ws, g, st);
   return 0;
 }
 

@@ -1572,6 +1572,29 @@ static void launch_ph(const bf16* A, const bf16* B, bf16* Y, float* stats, const
                        A, B, Y, stats, bias, addend, g);
 }
 
+// ---- halo-staged 3x3 kernel (conv3x3_hx.hip): cfg 30, forward and stride-1 dgrad ----
+constexpr int kHxCfg = 30;
+bool conv_hx_applicable(int N, int H, int W, int CA, int CO, int KH, int KW, int stride, int pad,
+                        int groups);
+int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
+                   const float* bias, int N, int H, int CA, int CO, bool dgrad, hipStream_t st,
+                   const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
+                   bool launch);
+static bool hx_ok(const ConvGeom& g, int mode) {
+  return (mode == 0 || mode == 1) && g.Ho == g.Hs && g.Wo == g.Ws &&
+         conv_hx_applicable(g.N, g.Hs, g.Ws, g.Cs, g.Co, g.KH, g.KW, g.stride, g.pad, g.groups);
+}
+static int igemm_select(const ConvGeom& g);
+template <int MODE>
+static bool use_hx(const ConvGeom& g) {
+  return igemm_select(g) == kHxCfg && hx_ok(g, MODE);
+}
+template <int MODE>
+static int hx_grid(const ConvGeom& g) {
+  return conv_hx_launch(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, g.N, g.Hs, g.Cs, g.Co,
+                        MODE == 1, nullptr, nullptr, nullptr, nullptr, nullptr, false);
+}
+
 // cfg of the phased kernel to use for this launch, or -1 (generic tile configs)
 template <int MODE>
 static int ph_cfg(const ConvGeom& g) {
@@ -1619,6 +1642,11 @@ static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, 
                            const ConvGeom& g, hipStream_t st, const bf16* addend = nullptr,
                            float* ws = nullptr) {
   if (ph_launch<MODE>(ph_cfg<MODE>(g), A, B, Y, stats, bias, g, st, addend)) return;
+  if (use_hx<MODE>(g)) {
+    conv_hx_launch(A, B, Y, stats, addend, bias, g.N, g.Hs, g.Cs, g.Co, MODE == 1, st, g.bn_y,
+                   g.bn_mask, g.bn_aux, g.bn_part, true);
+    return;
+  }
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
     case C: launch_igemm<BM, BN, WM, WN, ST, MODE>(A, B, Y, stats, bias, g, st, addend, ws); break;
@@ -1631,6 +1659,7 @@ static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, 
 template <int MODE>
 static int64_t igemm_ws_floats(const ConvGeom& g) {
   if (ph_cfg<MODE>(g) >= 0) return 0;   // no split-K in the phased kernel
+  if (use_hx<MODE>(g)) return 0;
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
     case C: return igemm_ws_floats_t<BM, BN, WM, WN, ST, MODE>(g);
@@ -1643,6 +1672,7 @@ static int64_t igemm_ws_floats(const ConvGeom& g) {
 template <int MODE>
 static int igemm_grid_x(const ConvGeom& g) {
   if (const int pc = ph_cfg<MODE>(g); pc >= 0) return ph_grid<MODE>(pc, g);
+  if (use_hx<MODE>(g)) return hx_grid<MODE>(g);
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
     case C: return igemm_grid_x_t<BM, BN, WM, WN, ST, MODE>(g);
@@ -1785,6 +1815,7 @@ std::vector<std::pair<int, int>> conv_tune_candidates(int kind, int N, int H, in
     // cover the DMA / LDS latency; not a candidate)
     if (g.Cn >= 128) c.emplace_back(21, 1);
   }
+  if (hx_ok(g, g.mode)) c.emplace_back(kHxCfg, 1);   // halo-staged 3x3 (conv3x3_hx.hip)
   for (int cfg : cfgs) {
     if (bn_of[cfg] >= 128 && g.Cn <= 64) continue;   // 128-wide N tiles on <= 64 channels
     if (bn_of[cfg] <= 32 && g.Cn > 64) continue;     // 32-wide N tiles on wide layers
@@ -2076,7 +2107,7 @@ std::vector<std::pair<int, int>> wgrad_tune_candidates(int N, int H, int W, int 
                                                        int groups) {
   std::vector<int> cfgs;
   const bool halo = wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) >= 0;
-  if (halo) cfgs.insert(cfgs.end(), {32, 33, 34, 35, 36, 37, 38});
+  if (halo) cfgs.insert(cfgs.end(), {32, 33, 34, 35, 36, 37, 38, 39, 40, 41});
   const int cin_g = Cin / groups, cout_g = Cout / groups;
   if (cin_g % 64 == 0 && cout_g % 64 == 0) cfgs.insert(cfgs.end(), {16, 17, 18, 19, 20, 21});
   cfgs.insert(cfgs.end(), {0, 1, 2, 3, 6, 7});

@@ -130,6 +130,52 @@ def test_conv_every_tile_config(C, case):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("case", [(4, 128, 16, 128), (8, 256, 8, 256), (8, 128, 8, 256),
+                                  (16, 512, 4, 512), (8, 256, 4, 128), (12, 128, 16, 256)])
+def test_conv3x3_halo_kernel(C, case):
+    """Halo-staged 3x3 s1 kernel (conv3x3_hx.hip, cfg 30) for layers 2-4: forward (+BN sums,
+    +bias), dgrad, and dgrad with the fused residual addend + BatchNorm-backward reduce, against
+    fp32 torch."""
+    N, Cin, H, Cout = case
+    torch.manual_seed(4)
+    x = bf(torch.randn(N, Cin, H, H, device="cuda")).requires_grad_(True)
+    w = bf(torch.randn(Cout, Cin, 3, 3, device="cuda") * (2.0 / (Cin * 9)) ** 0.5)
+    b = torch.randn(Cout, device="cuda") * 0.1
+    ref = F.conv2d(x, w, padding=1)
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    x_n = nhwc(x.detach()).to(torch.bfloat16)
+    wb, wt = C.weight_prep(w.permute(0, 2, 3, 1).contiguous(), 1, True)
+    dy_n = nhwc(dy).to(torch.bfloat16)
+    # BN(+ReLU) that produced x: y, 1-bit mask, mean | istd (for the fused backward reduce)
+    ybn = torch.randn(N, H, H, Cin, device="cuda").to(torch.bfloat16)
+    mask_b = torch.rand(N, H, H, Cin, device="cuda") > 0.4
+    bits = (mask_b.view(-1, 8).to(torch.int32) << torch.arange(8, device="cuda")).sum(1).to(torch.uint8)
+    mean, istd = torch.randn(Cin, device="cuda") * 0.1, torch.rand(Cin, device="cuda") + 0.5
+    aux = torch.cat([mean, istd])
+    add = torch.randn(N, H, H, Cin, device="cuda").to(torch.bfloat16)
+    try:
+        C.set_conv_tile(0, 30)
+        y, stats = C.conv_fwd(x_n, wb, None, 1, 1, 1, True)
+        assert rel_err(nchw(y), ref) < 2e-2
+        assert rel_err(stats[:, 0, :].sum(0), ref.detach().sum((0, 2, 3))) < 1e-2
+        assert rel_err(stats[:, 1, :].sum(0), (ref.detach() ** 2).sum((0, 2, 3))) < 1e-2
+        yb, _ = C.conv_fwd(x_n, wb, b, 1, 1, 1, False)
+        assert rel_err(nchw(yb), ref + b[None, :, None, None]) < 2e-2
+        dx = C.conv_dgrad(dy_n, wt, H, H, 1, 1, 1)
+        assert rel_err(nchw(dx), x.grad) < 2e-2
+        dx2, part = C.conv_dgrad_bn(dy_n, wt, H, H, 1, 1, 1, add, ybn, bits, aux)
+        full = nhwc(x.grad) + add.float()
+        assert rel_err(dx2, full) < 2e-2
+        dz = torch.where(mask_b, dx2.float(), torch.zeros_like(full))
+        s1 = dz.sum((0, 1, 2))
+        s2 = (dz * (ybn.float() - mean) * istd).sum((0, 1, 2))
+        assert part.numel() > 0
+        assert rel_err(part[:, 0, :].sum(0), s1) < 1e-2 and rel_err(part[:, 1, :].sum(0), s2) < 1e-2
+    finally:
+        C.set_conv_tile(0, -1)
+
+
 @pytest.mark.parametrize("case", [(2, 64, 16, 64, 3, 1, 1, 1), (3, 128, 8, 256, 3, 2, 1, 1),
                                   (2, 64, 16, 128, 1, 2, 0, 1), (2, 128, 8, 128, 3, 1, 1, 2)])
 def test_wgrad_autotune_candidates(C, case):
@@ -158,7 +204,7 @@ def test_wgrad_autotune_candidates(C, case):
     assert not bad, bad
 
 
-WGRAD_CFGS = list(range(8)) + list(range(16, 22)) + list(range(32, 39))
+WGRAD_CFGS = list(range(8)) + list(range(16, 22)) + list(range(32, 42))   # 39-41: one kernel row (3 taps) per halo tile
 
 
 @pytest.mark.parametrize("case", [(3, 64, 16, 64, 3, 1, 1, 1), (2, 128, 8, 256, 3, 2, 1, 1),

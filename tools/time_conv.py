@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--s", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--passes", default="fwd,dgrad,dgrad_bn,wgrad")
+    ap.add_argument("--cfg", type=int, default=-1, help="force a fwd/dgrad tile config (-1: autotune)")
+    ap.add_argument("--tag", default="")
     a = ap.parse_args()
     from pytorch_cifar_amd import _native
 
@@ -37,6 +39,7 @@ def main():
     w = torch.randn(a.cout, a.k, a.k, a.cin, device="cuda") * 0.05
     dy = torch.randn(N, Ho, Ho, a.cout, device="cuda").to(torch.bfloat16)
     wb, wt = C.weight_prep(w, 1, True)
+    C.set_conv_tile(0, a.cfg)
     # BN-backward fusion operands of the layer that produced x (y, 1-bit ReLU mask, mean | istd)
     ybn = torch.randn_like(x)
     mask = torch.randint(0, 256, (x.numel() // 8,), device="cuda", dtype=torch.uint8)
@@ -62,7 +65,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.iters
-        print(json.dumps({"shape": [N, a.cin, a.cout, a.h, a.k, a.s], "pass": name, "us": round(us, 1),
+        print(json.dumps({"tag": a.tag, "shape": [N, a.cin, a.cout, a.h, a.k, a.s], "pass": name, "us": round(us, 1),
                           "tflops": round(2 * macs / us / 1e6, 1)}), flush=True)
 
 
