@@ -835,9 +835,16 @@ static bool rows_enabled() {
 }
 
 static int rows_grid(int M, int C) {
+  // every block first folds the R x 2 x C accumulator rows (16 KiB): the cap bounds that prologue
+  // traffic and latency against the streaming passes' need for resident waves (PCA_BN_ROWS_CAP)
+  static const int cap = [] {
+    const char* e = getenv("PCA_BN_ROWS_CAP");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 512;   // measured: 512 -0.6 % vs 2048 at bs1024, equal at bs128
+  }();
   const int RPB = 256 / (C >> 3);
   int b = cdiv(M, RPB * kRowsInFlight);
-  return b < 2048 ? (b ? b : 1) : 2048;
+  return b < cap ? (b ? b : 1) : cap;
 }
 
 // =========================================== host ========================================
