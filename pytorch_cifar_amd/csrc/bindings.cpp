@@ -370,15 +370,24 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
   }
   if (g_autotune && !stream_capturing(cur_stream()) &&
       pca::conv_needs_tune(1, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, false)) {
+    // trials run the call as issued: with the fused BN-backward reduce when it is requested
+    // (its epilogue traffic decides between candidates that tie on the plain dgrad)
     autotune_conv(1, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, [&] {
       auto dxt = at::empty({N, H, W, Cin}, dy.options());
-      Tensor wst;
+      Tensor wst, pt;
       const int64_t n = pca::conv_dgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups,
                                                   Ho, Wo);
       if (n > 0) wst = at::empty({n}, dy.options().dtype(at::kFloat));
+      const int r = want_bn ? pca::conv_dgrad_bn_rows(N, H, W, Cin, Cout, KH, KW, stride, pad,
+                                                      groups, Ho, Wo)
+                            : 0;
+      if (r > 0) pt = at::empty({r, 2, Cin}, dy.options().dtype(at::kFloat));
       pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dxt), N, H, W, Cin, Cout, KH,
                              KW, stride, pad, groups, Ho, Wo, cur_stream(), add,
-                             n > 0 ? ptr<float>(wst) : nullptr);
+                             n > 0 ? ptr<float>(wst) : nullptr,
+                             r > 0 ? ptr<bf16>(*bn_y) : nullptr,
+                             r > 0 ? bn_mask->data_ptr<uint8_t>() : nullptr,
+                             r > 0 ? ptr<float>(*bn_aux) : nullptr, r > 0 ? ptr<float>(pt) : nullptr);
     });
   }
   auto dx = at::empty({N, H, W, Cin}, dy.options());

@@ -28,7 +28,8 @@ namespace pca {
 struct HxGeom {
   int N;            // images
   int CA;           // channels of the gathered tensor (x: Cin, dgrad: dY's Cout)
-  int CO;           // channels produced (forward: Cout, dgrad: Cin)
+  int CO;           // channels produced (forward: Cout, dgrad: Cin; stride-2 dgrad: 4 x Cin)
+  int COUT;         // channels of the output tensor (CO, or Cin for the stride-2 dgrad)
   int KC;           // 64-channel chunks of CA
   int tiles;        // N * H * W / BM
   uint32_t a_bytes, b_bytes;
@@ -42,7 +43,7 @@ struct HxGeom {
 
 __device__ __forceinline__ int hx_perm(int n) { return ((n >> 2) & 3) * 16 + (n >> 4) * 4 + (n & 3); }
 
-template <int W, int IMGS, int WM, int WN>
+template <int W, int IMGS, int WM, int WN, int TAPS = 9>
 struct HxShape {
   static constexpr int NW = WM * WN;
   static constexpr int BM = WM * 64, BN = WN * 64;
@@ -58,19 +59,30 @@ struct HxShape {
   static constexpr int LDS = 2 * HBYTES + 2 * BBYTES + 1024 + BN * 8;
   static_assert(IMGS * W * W == BM, "a tile is whole images");
   static_assert(BPC % NW == 0, "weight pieces split evenly over the waves");
-  // halo piece k is issued during tap k % 8 (taps 0..7; tap 8 stages the next chunk's weights)
-  static constexpr int pieces_at(int tap) { return tap >= 8 ? 0 : (HS - tap + 7) / 8; }
-  static_assert(HS <= 16, "at most two halo pieces per tap");
+  // halo piece k is issued during tap k % (TAPS-1) (the last tap stages the next chunk's weights)
+  static constexpr int pieces_at(int tap) {
+    return tap >= TAPS - 1 ? 0 : (HS - tap + TAPS - 2) / (TAPS - 1);
+  }
+  static_assert(HS <= 3 * (TAPS - 1), "at most three halo pieces per tap");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int W, int IMGS, int WM, int WN, bool DGRAD, bool STATS>
+// MODE 0: forward (3x3 taps); 1: stride-1 dgrad (mirrored taps, fused dgrad epilogue);
+// 2: stride-2 dgrad as a 2x2 convolution over dY producing the four output parity classes as
+// 4 x Cin channels (weights pre-arranged by hx_s2_weight_kernel, zero where a class does not meet
+// a tap), written depth-to-space: class (ph, pw) of dY pixel (y, x) is dX pixel (2y+ph, 2x+pw).
+// No zero-inserted MACs and no per-class launches (the generic parity-class kernel ran 1-4 taps
+// per tile and was epilogue-bound: 205 us for ResNet-18's layer-2 downsample at bs1024).
+template <int W, int IMGS, int WM, int WN, int MODE, bool STATS>
 __global__ __launch_bounds__(WM * WN * 64)
 void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
                        bf16* __restrict__ Y, float* __restrict__ stats,
                        const bf16* __restrict__ addend, const float* __restrict__ bias,
                        const HxGeom g) {
-  using SH = HxShape<W, IMGS, WM, WN>;
+  constexpr bool DGRAD = MODE != 0;
+  constexpr bool D2S = MODE == 2;
+  constexpr int KS = D2S ? 2 : 3, TAPS = KS * KS;
+  using SH = HxShape<W, IMGS, WM, WN, TAPS>;
   constexpr int NW = SH::NW, BM = SH::BM, BN = SH::BN, W2 = SH::W2;
   constexpr int HB = SH::HBYTES, BB = SH::BBYTES;
   __shared__ __attribute__((aligned(16))) char smem[SH::LDS];
@@ -88,7 +100,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
   const int wm = wid / WN, wn = wid % WN;
   const int q = lane >> 4, kq = lane >> 4;
   const int nb0 = blockIdx.y * BN;             // first produced channel of this workgroup
-  const int KA = 9 * g.CA;                     // weight row length (elements)
+  const int KA = TAPS * g.CA;                  // weight row length (elements)
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A, g.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(Bw, g.b_bytes);
 
@@ -124,7 +136,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
     b_row[k] = (ch * KA + (((lane & 7) ^ (r & 7)) << 3)) * 2;
   }
   auto b_tile = [&](int tap, int ch, int bb) {
-    const int src_tap = DGRAD ? 8 - tap : tap;
+    const int src_tap = MODE == 1 ? 8 - tap : tap;
     const int delta = (src_tap * g.CA + ch * 64) * 2;
 #pragma unroll
     for (int k = 0; k < SH::BS; ++k)
@@ -153,12 +165,25 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
   float s1[16], s2[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) s1[e] = s2[e] = 0.f;
-  const int ch_lane = nb0 + wn * 64 + q * 16;  // first of this lane's 16 output channels
+  const int ch_lane = nb0 + wn * 64 + q * 16;  // first of this lane's 16 produced channels
+  // its output-tensor channel (depth-to-space: class ch / COUT, channel ch % COUT)
+  const int co_lane = D2S ? ch_lane % g.COUT : ch_lane;
+  const int cls_lane = D2S ? ch_lane / g.COUT : 0;
   if (bnf) {   // the block's BN mean / istd once into LDS (read per element in the epilogue)
     for (int i = tid; i < 2 * BN; i += NW * 64)
-      auxs[i] = g.bn_aux[(i >= BN ? g.CO : 0) + nb0 + (i % BN)];
+      auxs[i] = g.bn_aux[(i >= BN ? g.COUT : 0) + (nb0 + (i % BN)) % g.COUT];
     __syncthreads();
   }
+  // output pixel of tile pixel p (the dY-resolution pixel for D2S, shifted to its class)
+  auto out_pix = [&](int t, int p) -> size_t {
+    if constexpr (!D2S) {
+      return (size_t)t * BM + p;
+    } else {
+      const int img = t * IMGS + p / (W * W), r = p % (W * W);
+      const int y = r / W, x = r % W;
+      return ((size_t)img * (2 * W) + 2 * y + (cls_lane >> 1)) * (2 * W) + 2 * x + (cls_lane & 1);
+    }
+  };
 
   constexpr int STORES = 8;                    // global stores per lane per tile
   // prologue: first tile's chunk-0 halo and tap-0 weights
@@ -189,7 +214,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
       // (a runtime tap loop: unrolled, the 9 taps' fragment offsets were hoisted as loop
       // invariants and pushed the 8-wave variants past 256 registers into spills)
 #pragma unroll 1
-      for (int tap = 0; tap < 9; ++tap, ++bc) {
+      for (int tap = 0; tap < TAPS; ++tap, ++bc) {
         // weights of this tap were issued one tap ago; after them came at most one halo piece,
         // or, at a tile's first tap, the previous tile's epilogue stores (may stay in flight)
         if (tap == 0) {
@@ -199,23 +224,24 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
           switch (SH::pieces_at(tap - 1)) {   // wave-uniform
             case 0: wait_vmcnt<0>(); break;
             case 1: wait_vmcnt<1>(); break;
-            default: wait_vmcnt<2>(); break;
+            case 2: wait_vmcnt<2>(); break;
+            default: wait_vmcnt<3>(); break;
           }
         }
         raw_barrier();
         // next tap's weights (past the last tile: harmless re-load of real rows)
-        if (tap < 8) b_tile(tap + 1, ch, (bc + 1) & 1);
+        if (tap < TAPS - 1) b_tile(tap + 1, ch, (bc + 1) & 1);
         else b_tile(0, last_chunk ? 0 : ch + 1, (bc + 1) & 1);
 #pragma unroll
         for (int k = 0; k < SH::HS; ++k)
-          if ((k & 7) == tap) halo_piece(h_t, h_ch, (hc + 1) & 1, k);   // wave-uniform
+          if (k % (TAPS - 1) == tap) halo_piece(h_t, h_ch, (hc + 1) & 1, k);   // wave-uniform
         if constexpr (DGRAD) {
-          if (last_chunk && tap == 8) {
+          if (last_chunk && tap == TAPS - 1) {
             // epilogue operands (residual-gradient addend; BN input y + ReLU mask), read
             // behind this tap's MFMAs
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
-              const size_t o = ((size_t)t * BM + wm * 64 + mi * 16 + (lane & 15)) * g.CO + ch_lane;
+              const size_t o = out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
               if (addend) {
                 pre_a[mi][0] = *reinterpret_cast<const uint4*>(addend + o);
                 pre_a[mi][1] = *reinterpret_cast<const uint4*>(addend + o + 8);
@@ -229,7 +255,9 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
           }
         }
         const int Boff = 2 * HB + (bc & 1) * BB; // this tap's weight slot
-        const int toff = (tap / 3) * W2 + (tap % 3);
+        // tap (kh, kw) reads halo row offset kh*(W+2) + kw; the 2x2 stride-2 dgrad taps are the
+        // dY pixels (y, x) .. (y+1, x+1): halo offsets 1..2
+        const int toff = KS == 3 ? (tap / 3) * W2 + (tap % 3) : (1 + tap / 2) * W2 + 1 + (tap % 2);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           bf16x8 fa[4], fb[4];
@@ -293,11 +321,11 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
             const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
             s1[e] += dz;
             const int c = ch_lane - nb0 + e;
-            s2[e] += dz * (yy[e] - auxs[c]) * auxs[BN + c];
+            s2[e] += dz * (yy[e] - auxs[c]) * auxs[BN + c];   // (aux of channel c % COUT)
           }
         }
       }
-      bf16* dst = Y + ((size_t)t * BM + wm * 64 + mi * 16 + (lane & 15)) * g.CO + ch_lane;
+      bf16* dst = Y + out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
       *reinterpret_cast<uint4*>(dst) = o0;
       *reinterpret_cast<uint4*>(dst + 8) = o1;
     }
@@ -324,16 +352,26 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
       }
     }
     __syncthreads();
-    if (tid < BN) {
+    // output channel c of this block gathers its produced channels c, c + COUT, ... (the
+    // parity classes of the stride-2 dgrad); slab row per (M walker, N block) for D2S
+    const int nco = D2S ? (BN < g.COUT ? BN : g.COUT) : BN;
+    if (tid < nco) {
       float a = 0.f, b = 0.f;
+      for (int j = tid; j < BN; j += (D2S ? g.COUT : BN)) {
 #pragma unroll
-      for (int w = 0; w < WM; ++w) {   // fixed order: deterministic per block
-        a += red[(w * BN + tid) * 2 + 0];
-        b += red[(w * BN + tid) * 2 + 1];
+        for (int w = 0; w < WM; ++w) {   // fixed order: deterministic per block
+          a += red[(w * BN + j) * 2 + 0];
+          b += red[(w * BN + j) * 2 + 1];
+        }
       }
       float* dst = STATS ? stats : g.bn_part;
-      stat_out(dst, blockIdx.x, g.shards, 2 * g.CO, nb0 + tid, a);
-      stat_out(dst, blockIdx.x, g.shards, 2 * g.CO, g.CO + nb0 + tid, b);
+      // (D2S: the N blocks that share columns — one per class when COUT >= BN — get rows of
+      // their own; together the rows of one M walker cover every column)
+      const int cb = D2S && g.COUT > BN ? g.COUT / BN : 1;
+      const int row = D2S ? (int)(blockIdx.x * (gridDim.y / cb) + blockIdx.y / cb) : (int)blockIdx.x;
+      const int col = (nb0 + tid) % g.COUT;
+      stat_out(dst, row, g.shards, 2 * g.COUT, col, a);
+      stat_out(dst, row, g.shards, 2 * g.COUT, g.COUT + col, b);
     }
   }
 }
@@ -367,66 +405,119 @@ bool conv_hx_applicable(int N, int H, int W, int CA, int CO, int KH, int KW, int
   return (W == 16 || W == 8 || W == 4) && (N * H * W) % bm == 0;
 }
 
-template <int W, int IMGS, int WM, int WN, bool DGRAD, bool STATS>
+template <int W, int IMGS, int WM, int WN, int MODE, bool STATS>
 static int hx_occ() {
   static int occ = 0;
   if (occ == 0)
-    occ = blocks_per_cu((const void*)conv3x3_hx_kernel<W, IMGS, WM, WN, DGRAD, STATS>, WM * WN * 64,
+    occ = blocks_per_cu((const void*)conv3x3_hx_kernel<W, IMGS, WM, WN, MODE, STATS>, WM * WN * 64,
                         "conv3x3_hx");
   return occ;
 }
 
-template <int W, int IMGS, int WM, int WN>
+template <int W, int IMGS, int WM, int WN, int MODE>
 static int hx_grid_x(const HxGeom& g, int nblocks) {
-  const int slots = hx_occ<W, IMGS, WM, WN, false, true>() * hx_cus();
+  const int slots = hx_occ<W, IMGS, WM, WN, MODE, MODE == 0>() * hx_cus();
   int gx = std::max(1, slots / std::max(1, nblocks));
   gx = std::min(gx, g.tiles);
   const int per = cdiv(g.tiles, gx);
   return cdiv(g.tiles, per);
 }
 
-template <int W, int IMGS, int WM, int WN>
+// returns the BN-sum slab rows the launch writes (grid.x; MODE 2: grid.x x the N blocks per column)
+template <int W, int IMGS, int WM, int WN, int MODE>
 static int hx_run(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
-                  const float* bias, const HxGeom& g, bool dgrad, hipStream_t st, bool launch) {
+                  const float* bias, const HxGeom& g, hipStream_t st, bool launch) {
   constexpr int BN = WN * 64;
   const int nblocks = g.CO / BN;
-  const int gx = hx_grid_x<W, IMGS, WM, WN>(g, nblocks);
-  if (!launch) return gx;
-  const dim3 grid(gx, nblocks), block(WM * WN * 64);
-  if (dgrad)
-    hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, true, false>), grid, block, 0, st, a, b,
-                       y, nullptr, addend, nullptr, g);
-  else if (stats)
-    hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, false, true>), grid, block, 0, st, a, b,
-                       y, stats, nullptr, bias, g);
-  else
-    hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, false, false>), grid, block, 0, st, a, b,
-                       y, nullptr, nullptr, bias, g);
-  return gx;
+  const int gx = hx_grid_x<W, IMGS, WM, WN, MODE>(g, nblocks);
+  if (launch) {
+    const dim3 grid(gx, nblocks), block(WM * WN * 64);
+    if (MODE != 0)
+      hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, MODE, false>), grid, block, 0, st, a, b,
+                         y, nullptr, addend, nullptr, g);
+    else if (stats)
+      hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, 0, true>), grid, block, 0, st, a, b, y,
+                         stats, nullptr, bias, g);
+    else
+      hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, 0, false>), grid, block, 0, st, a, b, y,
+                         nullptr, nullptr, bias, g);
+  }
+  return MODE == 2 ? gx * nblocks / (g.COUT > BN ? g.COUT / BN : 1) : gx;
 }
 
-// launch (or, with launch = false, only size: returns grid.x = the BN-statistics slab rows)
+template <int MODE>
+static int hx_dispatch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
+                       const float* bias, HxGeom& g, int H, hipStream_t st, bool launch) {
+  switch (H) {
+    case 16: g.tiles = g.N; return hx_run<16, 1, 4, 2, MODE>(a, b, y, stats, addend, bias, g, st, launch);
+    case 8: g.tiles = g.N / 4; return hx_run<8, 4, 4, 2, MODE>(a, b, y, stats, addend, bias, g, st, launch);
+    default: g.tiles = g.N / 8; return hx_run<4, 8, 2, 2, MODE>(a, b, y, stats, addend, bias, g, st, launch);
+  }
+}
+
+// launch (or, with launch = false, only size: returns the BN-statistics slab rows).
+// dgrad: H is the produced (= dY) map size; mode 2 (stride-2 dgrad) takes H = the dY map size and
+// b = the 2x2 class weights from conv_hx_s2_weights (CO = 4 x Cin).
 int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
-                   const float* bias, int N, int H, int CA, int CO, bool dgrad, hipStream_t st,
+                   const float* bias, int N, int H, int CA, int CO, int mode, hipStream_t st,
                    const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
                    bool launch) {
   HxGeom g;
   g.N = N;
   g.CA = CA;
   g.CO = CO;
+  g.COUT = mode == 2 ? CO / 4 : CO;
   g.KC = CA / 64;
   g.a_bytes = (uint32_t)((size_t)N * H * H * CA * 2);
-  g.b_bytes = (uint32_t)((size_t)CO * 9 * CA * 2);
+  g.b_bytes = (uint32_t)((size_t)CO * (mode == 2 ? 4 : 9) * CA * 2);
   g.shards = stat_shards();
   g.bn_y = bn_y;
   g.bn_mask = bn_mask;
   g.bn_aux = bn_aux;
-  g.bn_part = dgrad ? bn_part : nullptr;
-  switch (H) {
-    case 16: g.tiles = N; return hx_run<16, 1, 4, 2>(a, b, y, stats, addend, bias, g, dgrad, st, launch);
-    case 8: g.tiles = N / 4; return hx_run<8, 4, 4, 2>(a, b, y, stats, addend, bias, g, dgrad, st, launch);
-    default: g.tiles = N / 8; return hx_run<4, 8, 2, 2>(a, b, y, stats, addend, bias, g, dgrad, st, launch);
+  g.bn_part = mode != 0 ? bn_part : nullptr;
+  if (mode == 0) return hx_dispatch<0>(a, b, y, stats, addend, bias, g, H, st, launch);
+  if (mode == 1) return hx_dispatch<1>(a, b, y, stats, addend, bias, g, H, st, launch);
+  return hx_dispatch<2>(a, b, y, stats, addend, bias, g, H, st, launch);
+}
+
+// stride-2 dgrad applicability: 3x3 / stride 2 / pad 1 forward conv with H = 2 * Ho, dY maps of
+// 16 / 8 / 4, Cout % 64 (the gathered dY chunks), 4 * Cin % 128 (the produced class channels),
+// Cin % 128 past 128 (a 128-channel N block then stays inside one class)
+bool conv_hx_s2_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                           int pad, int groups, int Ho, int Wo) {
+  static const bool off = [] {
+    const char* e = getenv("PCA_CONV_HX");
+    return e && e[0] == '0';
+  }();
+  if (off || KH != 3 || KW != 3 || stride != 2 || pad != 1 || groups != 1 || H != W) return false;
+  if (Ho != Wo || H != 2 * Ho || (Ho != 16 && Ho != 8 && Ho != 4)) return false;
+  if (Cout % 64 || (4 * Cin) % 128 || (Cin > 128 && Cin % 128)) return false;
+  const int bm = Ho == 4 ? 128 : 256;
+  return (N * Ho * Ho) % bm == 0;
+}
+
+// 2x2 class weights of the stride-2 dgrad from the transposed 3x3 weights wt[Cin][3][3][Cout]:
+//   w2[(ph*2 + pw)*Cin + ci][a*2 + b][co] = wt[ci][ph + 1 - 2a][pw + 1 - 2b][co]  (0 if out of range)
+// (dX pixel (2y+ph, 2x+pw) meets dY pixel (y+a, x+b) through tap (ph+1-2a, pw+1-2b))
+__global__ __launch_bounds__(256) void hx_s2_weight_kernel(const bf16* __restrict__ wt, int Cin,
+                                                           int Cout, bf16* __restrict__ w2) {
+  const int c8 = Cout / 8;
+  const int total = 4 * Cin * 4 * c8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cc = i % c8, t = (i / c8) % 4, z = i / (c8 * 4);
+    const int cls = z / Cin, ci = z % Cin;
+    const int kh = (cls >> 1) + 1 - 2 * (t >> 1), kw = (cls & 1) + 1 - 2 * (t & 1);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (kh >= 0 && kh < 3 && kw >= 0 && kw < 3)
+      v = *reinterpret_cast<const uint4*>(wt + (((size_t)ci * 3 + kh) * 3 + kw) * Cout + cc * 8);
+    *reinterpret_cast<uint4*>(w2 + ((size_t)z * 4 + t) * Cout + cc * 8) = v;
   }
+}
+
+void conv_hx_s2_weights(const bf16* wt, int Cin, int Cout, bf16* w2, hipStream_t st) {
+  const int total = 4 * Cin * 4 * (Cout / 8);
+  hipLaunchKernelGGL(hx_s2_weight_kernel, dim3(std::min(cdiv(total, 256), 1024)), dim3(256), 0, st, wt,
+                     Cin, Cout, w2);
 }
 
 }  // namespace pca

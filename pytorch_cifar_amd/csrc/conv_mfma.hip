@@ -1577,13 +1577,22 @@ constexpr int kHxCfg = 30;
 bool conv_hx_applicable(int N, int H, int W, int CA, int CO, int KH, int KW, int stride, int pad,
                         int groups);
 int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
-                   const float* bias, int N, int H, int CA, int CO, bool dgrad, hipStream_t st,
+                   const float* bias, int N, int H, int CA, int CO, int mode, hipStream_t st,
                    const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
                    bool launch);
+bool conv_hx_s2_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                           int pad, int groups, int Ho, int Wo);
+void conv_hx_s2_weights(const bf16* wt, int Cin, int Cout, bf16* w2, hipStream_t st);
+// (for a dgrad geometry g: Hs/Ws/Cs = dY, Ho/Wo/Co = dX)
 static bool hx_ok(const ConvGeom& g, int mode) {
+  if (mode == 2)
+    return conv_hx_s2_applicable(g.N, g.Ho, g.Wo, g.Co, g.Cs, g.KH, g.KW, g.stride, g.pad, g.groups,
+                                 g.Hs, g.Ws);
   return (mode == 0 || mode == 1) && g.Ho == g.Hs && g.Wo == g.Ws &&
          conv_hx_applicable(g.N, g.Hs, g.Ws, g.Cs, g.Co, g.KH, g.KW, g.stride, g.pad, g.groups);
 }
+// stride-2 dgrad: bf16 2x2 class weights live in the launch workspace (in floats)
+static int64_t hx_s2_ws_floats(const ConvGeom& g) { return (int64_t)16 * g.Co * g.Cs / 2; }
 static int igemm_select(const ConvGeom& g);
 template <int MODE>
 static bool use_hx(const ConvGeom& g) {
@@ -1591,8 +1600,9 @@ static bool use_hx(const ConvGeom& g) {
 }
 template <int MODE>
 static int hx_grid(const ConvGeom& g) {
-  return conv_hx_launch(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, g.N, g.Hs, g.Cs, g.Co,
-                        MODE == 1, nullptr, nullptr, nullptr, nullptr, nullptr, false);
+  return conv_hx_launch(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, g.N, g.Hs, g.Cs,
+                        MODE == 2 ? 4 * g.Co : g.Co, MODE, nullptr, nullptr, nullptr, nullptr, nullptr,
+                        false);
 }
 
 // cfg of the phased kernel to use for this launch, or -1 (generic tile configs)
@@ -1643,8 +1653,14 @@ static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, 
                            float* ws = nullptr) {
   if (ph_launch<MODE>(ph_cfg<MODE>(g), A, B, Y, stats, bias, g, st, addend)) return;
   if (use_hx<MODE>(g)) {
-    conv_hx_launch(A, B, Y, stats, addend, bias, g.N, g.Hs, g.Cs, g.Co, MODE == 1, st, g.bn_y,
-                   g.bn_mask, g.bn_aux, g.bn_part, true);
+    const bf16* Bw = B;
+    if constexpr (MODE == 2) {   // the 2x2 class weights, into the workspace
+      bf16* w2 = reinterpret_cast<bf16*>(ws);
+      conv_hx_s2_weights(B, g.Co, g.Cs, w2, st);
+      Bw = w2;
+    }
+    conv_hx_launch(A, Bw, Y, stats, addend, bias, g.N, g.Hs, g.Cs, MODE == 2 ? 4 * g.Co : g.Co,
+                   MODE, st, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, true);
     return;
   }
   switch (igemm_select(g)) {
@@ -1659,7 +1675,7 @@ static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, 
 template <int MODE>
 static int64_t igemm_ws_floats(const ConvGeom& g) {
   if (ph_cfg<MODE>(g) >= 0) return 0;   // no split-K in the phased kernel
-  if (use_hx<MODE>(g)) return 0;
+  if (use_hx<MODE>(g)) return MODE == 2 ? hx_s2_ws_floats(g) : 0;
   switch (igemm_select(g)) {
 #define PCA_CASE(C, BM, BN, WM, WN, ST) \
     case C: return igemm_ws_floats_t<BM, BN, WM, WN, ST, MODE>(g);
@@ -1758,6 +1774,7 @@ int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
   const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   if (g.Co % 8 != 0) return 0;
   if (g.mode == 2) {
+    if (use_hx<2>(g)) return hx_grid<2>(g);   // one slab row per (tile group, class-channel block)
     if (igemm_ws_floats<2>(g) > 0) {
       int rpb;
       return splitk_reduce_grid(g.N * g.Ho * g.Wo, g.Co, &rpb);
@@ -1815,7 +1832,8 @@ std::vector<std::pair<int, int>> conv_tune_candidates(int kind, int N, int H, in
     // cover the DMA / LDS latency; not a candidate)
     if (g.Cn >= 128) c.emplace_back(21, 1);
   }
-  if (hx_ok(g, g.mode)) c.emplace_back(kHxCfg, 1);   // halo-staged 3x3 (conv3x3_hx.hip)
+  if (hx_ok(g, g.mode)) c.emplace_back(kHxCfg, 1);   // halo-staged 3x3 (conv3x3_hx.hip; the
+                                                      // stride-2 dgrad as its 2x2 class form)
   for (int cfg : cfgs) {
     if (bn_of[cfg] >= 128 && g.Cn <= 64) continue;   // 128-wide N tiles on <= 64 channels
     if (bn_of[cfg] <= 32 && g.Cn > 64) continue;     // 32-wide N tiles on wide layers

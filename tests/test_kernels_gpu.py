@@ -176,6 +176,43 @@ def test_conv3x3_halo_kernel(C, case):
         C.set_conv_tile(0, -1)
 
 
+@pytest.mark.parametrize("case", [(4, 64, 32, 128), (8, 128, 16, 256), (16, 256, 8, 512),
+                                  (8, 32, 16, 64), (4, 96, 32, 64)])
+def test_conv3x3_s2_dgrad_halo_kernel(C, case):
+    """Stride-2 dgrad through the halo kernel (cfg 30, mode 2): a 2x2 convolution over dY whose
+    4 x Cin output channels are the four parity classes of dX, written depth-to-space; plain,
+    and with the fused residual addend + BatchNorm-backward reduce, against fp32 torch."""
+    N, Cin, H, Cout = case
+    torch.manual_seed(5)
+    x = bf(torch.randn(N, Cin, H, H, device="cuda")).requires_grad_(True)
+    w = bf(torch.randn(Cout, Cin, 3, 3, device="cuda") * (2.0 / (Cin * 9)) ** 0.5)
+    ref = F.conv2d(x, w, stride=2, padding=1)
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    wb, wt = C.weight_prep(w.permute(0, 2, 3, 1).contiguous(), 1, True)
+    dy_n = nhwc(dy).to(torch.bfloat16)
+    ybn = torch.randn(N, H, H, Cin, device="cuda").to(torch.bfloat16)
+    mask_b = torch.rand(N, H, H, Cin, device="cuda") > 0.4
+    bits = (mask_b.view(-1, 8).to(torch.int32) << torch.arange(8, device="cuda")).sum(1).to(torch.uint8)
+    mean, istd = torch.randn(Cin, device="cuda") * 0.1, torch.rand(Cin, device="cuda") + 0.5
+    aux = torch.cat([mean, istd])
+    add = torch.randn(N, H, H, Cin, device="cuda").to(torch.bfloat16)
+    try:
+        C.set_conv_tile(0, 30)
+        dx = C.conv_dgrad(dy_n, wt, H, H, 2, 1, 1)
+        assert rel_err(nchw(dx), x.grad) < 2e-2
+        dx2, part = C.conv_dgrad_bn(dy_n, wt, H, H, 2, 1, 1, add, ybn, bits, aux)
+        full = nhwc(x.grad) + add.float()
+        assert rel_err(dx2, full) < 2e-2
+        dz = torch.where(mask_b, dx2.float(), torch.zeros_like(full))
+        s1 = dz.sum((0, 1, 2))
+        s2 = (dz * (ybn.float() - mean) * istd).sum((0, 1, 2))
+        assert part.numel() > 0
+        assert rel_err(part[:, 0, :].sum(0), s1) < 1e-2 and rel_err(part[:, 1, :].sum(0), s2) < 1e-2
+    finally:
+        C.set_conv_tile(0, -1)
+
+
 @pytest.mark.parametrize("case", [(2, 64, 16, 64, 3, 1, 1, 1), (3, 128, 8, 256, 3, 2, 1, 1),
                                   (2, 64, 16, 128, 1, 2, 0, 1), (2, 128, 8, 128, 3, 1, 1, 2)])
 def test_wgrad_autotune_candidates(C, case):
