@@ -134,6 +134,9 @@ void ce_fused_launch(const float*, const int64_t*, int, int, float*, float*, dou
 void scale_by_scalar_launch(const float*, const float*, size_t, float*, hipStream_t);
 void sgd_launch(const int64_t*, int, float* const*, const float* const*, float* const*,
                 bf16* const*, const float*, float, float, float, float, int, int, hipStream_t);
+void sgd_prep_launch(const int64_t*, int, float* const*, const float* const*, float* const*,
+                     const float*, float, float, float, float, int, int, const int64_t*,
+                     const int64_t*, int, const int64_t*, hipStream_t);
 void se_scale_fwd_launch(const bf16*, const float*, int, int, int, bf16*, hipStream_t);
 struct CatArgs {
   const bf16* src[8];
@@ -1197,6 +1200,29 @@ void sgd_step(const Tensor& chunks, const Tensor& pptr, const Tensor& gptr, cons
                   nesterov ? 1 : 0, first ? 1 : 0, cur_stream());
 }
 
+// optimizer step + bf16 operand refresh in one launch: `chunks` (SGD chunks of the arena ranges
+// no conv operand is built from) + `pchunks` (WeightPrepPlan chunks over `desc`, whose masters
+// are updated in place; gm[t] = {grad, momentum} of desc tensor t)
+void sgd_prep_step(const Tensor& chunks, const Tensor& pptr, const Tensor& gptr, const Tensor& bptr,
+                   const Tensor& lr, double momentum, double dampening, double wd,
+                   double grad_scale, bool nesterov, bool first, const Tensor& desc,
+                   const Tensor& pchunks, const Tensor& gm) {
+  for (const Tensor* t : {&chunks, &pptr, &gptr, &bptr, &desc, &pchunks, &gm})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous(),
+                "sgd_prep_step tables: contiguous int64 on the GPU");
+  TORCH_CHECK(chunks.numel() == 0 || (chunks.dim() == 2 && chunks.size(1) == 3), "chunks [n][3]");
+  TORCH_CHECK(pchunks.dim() == 2 && pchunks.size(1) == 4, "pchunks [n][4]");
+  TORCH_CHECK(desc.dim() == 2 && desc.size(1) == 8 && gm.numel() == 2 * desc.size(0),
+              "desc [t][8], gm [t][2]");
+  check_f32(lr, "lr");
+  pca::sgd_prep_launch(chunks.numel() ? ptr<int64_t>(chunks) : nullptr,
+                       chunks.numel() ? (int)chunks.size(0) : 0, ptr<float* const>(pptr),
+                       ptr<const float* const>(gptr), ptr<float* const>(bptr), ptr<float>(lr),
+                       (float)momentum, (float)dampening, (float)wd, (float)grad_scale,
+                       nesterov ? 1 : 0, first ? 1 : 0, ptr<int64_t>(desc), ptr<int64_t>(pchunks),
+                       (int)pchunks.size(0), ptr<int64_t>(gm), cur_stream());
+}
+
 Tensor se_scale_fwd(const Tensor& x, const Tensor& s) {
   check_bf16(x, "x");
   check_f32(s, "s");
@@ -1533,6 +1559,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fused", &ce_fused);
   m.def("scale_by_scalar", &scale_by_scalar);
   m.def("sgd_step", &sgd_step);
+  m.def("sgd_prep_step", &sgd_prep_step);
   m.def("se_scale_fwd", &se_scale_fwd);
   m.def("se_scale_bwd", &se_scale_bwd);
   m.def("dpn_merge_fwd", &dpn_merge_fwd);

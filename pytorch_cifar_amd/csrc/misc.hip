@@ -637,8 +637,22 @@ struct SgdArgs {
   int nesterov, first;
 };
 
-__global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) {
-  const int64_t* ch = a.chunks + (size_t)blockIdx.x * 3;
+// one element of the update with explicit FMAs, shared by every SGD path (the plain chunks and
+// the fused update + prep) so that all of them round identically
+__device__ __forceinline__ float sgd_elem(float pv, float gv, float& bv, float lr, float momentum,
+                                          float dampening, float wd, float grad_scale, int nesterov,
+                                          int first) {
+  float d = gv * grad_scale;
+  if (wd != 0.f) d = __builtin_fmaf(wd, pv, d);
+  if (momentum != 0.f) {
+    bv = first ? d : __builtin_fmaf(momentum, bv, (1.f - dampening) * d);
+    d = nesterov ? __builtin_fmaf(momentum, bv, d) : bv;
+  }
+  return __builtin_fmaf(-lr, d, pv);
+}
+
+__device__ __forceinline__ void sgd_chunk(const SgdArgs& a, int blk) {
+  const int64_t* ch = a.chunks + (size_t)blk * 3;
   const int t = (int)ch[0];
   const int64_t s = ch[1], e = ch[2];
   float* p = a.params[t];
@@ -660,34 +674,44 @@ __global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) {
         bf[0] = bv.x; bf[1] = bv.y; bf[2] = bv.z; bf[3] = bv.w;
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float d = gf[k] * a.grad_scale;
-        if (a.wd != 0.f) d += a.wd * pf[k];
-        if (a.momentum != 0.f) {
-          const float bv = a.first ? d : a.momentum * bf[k] + (1.f - a.dampening) * d;
-          bf[k] = bv;
-          d = a.nesterov ? d + a.momentum * bv : bv;
-        }
-        pf[k] -= lr * d;
-      }
+      for (int k = 0; k < 4; ++k)
+        pf[k] = sgd_elem(pf[k], gf[k], bf[k], lr, a.momentum, a.dampening, a.wd, a.grad_scale,
+                         a.nesterov, a.first);
       if (a.momentum != 0.f) b4[i] = make_float4(bf[0], bf[1], bf[2], bf[3]);
       p4[i] = make_float4(pf[0], pf[1], pf[2], pf[3]);
     }
     return;
   }
   for (int64_t i = s + threadIdx.x; i < e; i += 256) {
-    float d = g ? g[i] * a.grad_scale : 0.f;
-    const float pv = p[i];
-    if (a.wd != 0.f) d += a.wd * pv;
-    if (a.momentum != 0.f) {
-      float bv = a.first ? d : a.momentum * b[i] + (1.f - a.dampening) * d;
-      b[i] = bv;
-      d = a.nesterov ? d + a.momentum * bv : bv;
-    }
-    const float np = pv - lr * d;
+    float bv = (a.momentum != 0.f && !a.first) ? b[i] : 0.f;
+    const float np = sgd_elem(p[i], g ? g[i] : 0.f, bv, lr, a.momentum, a.dampening, a.wd,
+                              a.grad_scale, a.nesterov, a.first);
+    if (a.momentum != 0.f) b[i] = bv;
     p[i] = np;
     if (sh) sh[i] = f2bf(np);
   }
+}
+
+__global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) { sgd_chunk(a, blockIdx.x); }
+
+// The SGD update of one element for the fused update + weight-prep launch (same arithmetic as
+// sgd_chunk): reads grad / momentum at index i of the tensor's arena views, writes the new master
+// and momentum, returns the new master for the bf16 operand copies.
+struct SgdUpd {
+  const int64_t* gm;       // [tensors][2] {grad, momentum} pointers parallel to the prep desc
+  const float* lr;
+  float momentum, dampening, wd, grad_scale;
+  int nesterov, first;
+};
+
+__device__ __forceinline__ float sgd_upd(const SgdUpd& u, float lr, float* w, const float* g,
+                                         float* m, int i) {
+  float bv = (u.momentum != 0.f && !u.first) ? m[i] : 0.f;
+  const float np = sgd_elem(w[i], g[i], bv, lr, u.momentum, u.dampening, u.wd, u.grad_scale,
+                            u.nesterov, u.first);
+  if (u.momentum != 0.f) m[i] = bv;
+  w[i] = np;
+  return np;
 }
 
 // -------------------------------------------------------------------------- SE / acts
@@ -1114,20 +1138,31 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, int G, int Cn, i
 //           master feeds both operands; the plan then issues no pass-0 chunks for the weight).
 // All index math is 32-bit and per block / per 8 elements (64-bit div/mod per element made the
 // first version of this kernel 10x slower than its bandwidth).
-__global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* __restrict__ desc,
-                                                                const int64_t* __restrict__ chunks) {
-  __shared__ float tile[64][65];
-  const int64_t* ch = chunks + (size_t)blockIdx.x * 4;
+// UPD: the fused optimizer form — every master element is read exactly once by the chunk plan,
+// so it is SGD-updated there (sgd_upd) and the bf16 operands are written from the new value: the
+// next forward finds its operands current and the separate prep pass (a full re-read of the
+// masters right after the optimizer wrote them) is gone.
+template <bool UPD>
+__device__ __forceinline__ void prep_chunk(const int64_t* __restrict__ desc,
+                                           const int64_t* __restrict__ ch, const SgdUpd& u,
+                                           float (*tile)[65]) {
   const int64_t* d = desc + ch[0] * 8;
-  const float* w = reinterpret_cast<const float*>(d[0]);
+  float* const w = reinterpret_cast<float*>(d[0]);
   const int Cn = (int)d[4], T = (int)d[5], Cr = (int)d[6];
   const int tid = threadIdx.x;
+  const float* ug = UPD ? reinterpret_cast<const float*>(u.gm[ch[0] * 2]) : nullptr;
+  float* um = UPD ? reinterpret_cast<float*>(u.gm[ch[0] * 2 + 1]) : nullptr;
+  const float lr = UPD ? u.lr[0] : 0.f;
+  auto ld = [&](int i) -> float {
+    if constexpr (UPD) return sgd_upd(u, lr, w, ug, um, i);
+    else return w[i];
+  };
   if (ch[3] == 2) {
     float* wtf = reinterpret_cast<float*>(d[1]);
     const int c0 = (int)ch[1], nc = (int)ch[2] - c0;
     for (int k = tid; k < nc * T; k += 256) {
       const int co = c0 + k / T, tap = k % T;
-      wtf[tap * Cn + co] = w[co * T + tap];
+      wtf[tap * Cn + co] = ld(co * T + tap);
     }
     return;
   }
@@ -1138,7 +1173,7 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* _
     const int Cp = (int)d[7], r0 = (int)ch[1], nr = (int)ch[2] - r0;
     for (int k = tid; k < nr * Cp; k += 256) {
       const int r = r0 + k / Cp, c = k % Cp;
-      wb[r * Cp + c] = f2bf(c < Cr ? w[r * Cr + c] : 0.f);
+      wb[r * Cp + c] = f2bf(c < Cr ? ld(r * Cr + c) : 0.f);
     }
     return;
   }
@@ -1146,9 +1181,16 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* _
     bf16* wb = reinterpret_cast<bf16*>(d[1]);
     const int s0 = (int)ch[1], s1 = (int)ch[2];
     for (int i = s0 + tid * 8; i < s1; i += 256 * 8) {
-      const float4 v0 = *reinterpret_cast<const float4*>(w + i);
-      const float4 v1 = *reinterpret_cast<const float4*>(w + i + 4);
-      const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      float f[8];
+      if constexpr (UPD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = ld(i + j);
+      } else {
+        const float4 v0 = *reinterpret_cast<const float4*>(w + i);
+        const float4 v1 = *reinterpret_cast<const float4*>(w + i + 4);
+        f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w;
+        f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
+      }
       *reinterpret_cast<uint4*>(wb + i) = pack8(f);
     }
     return;
@@ -1167,7 +1209,7 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* _
   for (int k = tid; k < 64 * 64; k += 256) {
     const int r = k >> 6, c = k & 63;               // r: co, c: ci (contiguous in w)
     const int co = co0 + r, ci = ci0 + c;
-    tile[r][c] = (co < Cn && ci < Cr) ? w[((g * Cn + co) * T + tap) * Cr + ci] : 0.f;
+    tile[r][c] = (co < Cn && ci < Cr) ? ld(((g * Cn + co) * T + tap) * Cr + ci) : 0.f;
   }
   __syncthreads();
   if (wbt) {   // forward copy of the tile: 8 consecutive ci per thread, 16-byte stores
@@ -1200,6 +1242,26 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* _
     const int ci = ci0 + r, co = co0 + c;
     if (ci < Cr && co < Cn) wt[((g * Cr + ci) * T + tap) * Cn + co] = f2bf(tile[c][r]);
   }
+}
+
+__global__ __launch_bounds__(256) void weight_prep_multi_kernel(const int64_t* __restrict__ desc,
+                                                                const int64_t* __restrict__ chunks) {
+  __shared__ float tile[64][65];
+  prep_chunk<false>(desc, chunks + (size_t)blockIdx.x * 4, SgdUpd{}, tile);
+}
+
+// One launch for the whole optimizer step: blocks [0, nsgd) run the plain SGD chunks (every
+// arena range that no conv operand is built from), the rest the fused update + prep chunks.
+__global__ __launch_bounds__(256) void sgd_prep_kernel(SgdArgs a, int nsgd,
+                                                       const int64_t* __restrict__ desc,
+                                                       const int64_t* __restrict__ chunks,
+                                                       SgdUpd u) {
+  __shared__ float tile[64][65];
+  if ((int)blockIdx.x < nsgd) {
+    sgd_chunk(a, blockIdx.x);
+    return;
+  }
+  prep_chunk<true>(desc, chunks + (size_t)(blockIdx.x - nsgd) * 4, u, tile);
 }
 
 // ================================================================================ host
@@ -1581,6 +1643,18 @@ void sgd_launch(const int64_t* chunks, int nchunks, float* const* params, const 
   SgdArgs a{chunks, params, grads, bufs, shadows, lr, momentum, dampening, wd, grad_scale,
             nesterov, first};
   hipLaunchKernelGGL(sgd_kernel, dim3(nchunks), dim3(256), 0, st, a);
+}
+void sgd_prep_launch(const int64_t* chunks, int nchunks, float* const* params,
+                     const float* const* grads, float* const* bufs, const float* lr, float momentum,
+                     float dampening, float wd, float grad_scale, int nesterov, int first,
+                     const int64_t* desc, const int64_t* pchunks, int npchunks, const int64_t* gm,
+                     hipStream_t st) {
+  SgdArgs a{chunks, params, grads, bufs, nullptr, lr, momentum, dampening, wd, grad_scale,
+            nesterov, first};
+  SgdUpd u{gm, lr, momentum, dampening, wd, grad_scale, nesterov, first};
+  if (nchunks + npchunks > 0)
+    hipLaunchKernelGGL(sgd_prep_kernel, dim3(nchunks + npchunks), dim3(256), 0, st, a, nchunks, desc,
+                       pchunks, u);
 }
 void se_scale_fwd_launch(const bf16* x, const float* s, int N, int HW, int C, bf16* out,
                          hipStream_t st) {

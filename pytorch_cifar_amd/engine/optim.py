@@ -16,6 +16,7 @@ from __future__ import annotations
 import torch
 
 from .. import _native
+from . import grads
 
 _CHUNK = 8192
 
@@ -105,6 +106,58 @@ class SGD(torch.optim.Optimizer):
             self.state[p]["momentum_buffer"] = v
         return self
 
+    def attach_weight_prep(self, plan):
+        """Fuse the model's bf16 conv-operand refresh (ops.functional.WeightPrepPlan) into the
+        arena step: one launch updates every master and writes the operands from the new values
+        (the optimizer emits the bf16 shadows), so the forward's separate prep pass
+        (a full re-read of the masters) disappears. Needs ``attach_arena`` first."""
+        if getattr(self, "arena", None) is None:
+            raise ValueError("attach_weight_prep needs attach_arena first")
+        self._wplan = plan
+        plan.skip_when_fresh = True
+        plan.watch = (self.arena.param_flat,)
+        return self
+
+    def _fused_tables(self, plan):
+        """(sgd chunks of the arena ranges outside the plan, desc, prep chunks, {grad, mom} table)
+        or None when some plan weight is not an arena member."""
+        tabs = plan.ensure_tables()
+        if tabs is None:
+            return None
+        arena = self.arena
+        key = (id(tabs[0]), id(tabs[1]), tabs[2], arena.param_flat.data_ptr(), arena.mom_flat.data_ptr())
+        ent = getattr(self, "_fused", None)
+        if ent is not None and ent[0] == key:
+            return ent[1]
+        ranges, gm = [], []
+        for e in plan.entries:
+            if id(e.w) not in arena.offsets:
+                self._fused = (key, None)
+                return None
+            off, n = arena.offsets[id(e.w)]
+            if grads.physical(e.w).data_ptr() != arena.param_flat.data_ptr() + 4 * off:
+                self._fused = (key, None)
+                return None
+            ranges.append((off, off + n))
+            gm.append([arena.grad_flat.data_ptr() + 4 * off, arena.mom_flat.data_ptr() + 4 * off])
+        ranges.sort()
+        free, pos = [], 0
+        for a, b in ranges:
+            if a > pos:
+                free.append((pos, a))
+            pos = max(pos, b)
+        if pos < arena.numel:
+            free.append((pos, arena.numel))
+        chunks = [(0, s, min(b, s + _CHUNK)) for a, b in free for s in range(a, b, _CHUNK)]
+        dev = arena.param_flat.device
+        out = (torch.tensor(chunks, dtype=torch.int64).reshape(-1, 3).to(dev),
+               torch.tensor([arena.param_flat.data_ptr()], dtype=torch.int64).to(dev),
+               torch.tensor([arena.grad_flat.data_ptr()], dtype=torch.int64).to(dev),
+               torch.tensor([arena.mom_flat.data_ptr()], dtype=torch.int64).to(dev),
+               torch.tensor(gm, dtype=torch.int64).to(dev))
+        self._fused = (key, out)
+        return out
+
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         arena = getattr(self, "arena", None)
@@ -133,11 +186,23 @@ class SGD(torch.optim.Optimizer):
         arena = getattr(self, "arena", None)
         if arena is not None and arena.param_flat.is_cuda:
             group = self.param_groups[0]
-            chunks, pp, gp, bp = self._table(0, [arena.param_flat], [arena.grad_flat], [arena.mom_flat])
             lr = self._lr_tensor(0, group, arena.param_flat.device)
-            _native.lib().sgd_step(chunks, pp, gp, bp, None, lr, group["momentum"], group["dampening"],
-                                   group["weight_decay"], self.grad_scale, group["nesterov"],
-                                   self._arena_first)
+            plan = getattr(self, "_wplan", None)
+            fused = self._fused_tables(plan) if plan is not None and plan.entries else None
+            if fused is not None:
+                chunks, pp, gp, bp, gm = fused
+                _native.lib().sgd_prep_step(chunks, pp, gp, bp, lr, group["momentum"],
+                                            group["dampening"], group["weight_decay"],
+                                            self.grad_scale, group["nesterov"], self._arena_first,
+                                            plan.tables[0], plan.tables[1], gm)
+                plan.mark_fresh()      # masters and operands updated together, versions untouched
+            else:
+                chunks, pp, gp, bp = self._table(0, [arena.param_flat], [arena.grad_flat], [arena.mom_flat])
+                _native.lib().sgd_step(chunks, pp, gp, bp, None, lr, group["momentum"], group["dampening"],
+                                       group["weight_decay"], self.grad_scale, group["nesterov"],
+                                       self._arena_first)
+                if plan is not None:
+                    plan.invalidate()   # raw-pointer update: the operands are stale
             self._arena_first = False
             return loss
         for i, group in enumerate(self.param_groups):

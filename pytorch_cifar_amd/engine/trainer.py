@@ -37,6 +37,10 @@ class TrainStep:
             from ..ops.functional import enable_batched_weight_prep
 
             enable_batched_weight_prep(inner)
+            # the optimizer step writes the bf16 operands (no prep pass at the next forward)
+            if getattr(optimizer, "arena", None) is not None and hasattr(optimizer, "attach_weight_prep") \
+                    and os.environ.get("PCA_FUSED_SGD_PREP", "1") != "0":
+                optimizer.attach_weight_prep(inner.__dict__["_pca_wplan"])
         self.ddp = ddp
         self.device = loader.device
         self.metrics = metrics if metrics is not None else torch.zeros(3, dtype=torch.float64, device=self.device)
@@ -61,6 +65,14 @@ class TrainStep:
         with trace_range("optimizer"):
             self.opt.step()
         return loss
+
+    def _fresh_operands(self):
+        """A captured step with the fused optimizer has no prep pass: when the masters changed
+        outside it (restore, checkpoint load, user writes), refresh the operands before replay."""
+        plan = getattr(self.opt, "_wplan", None)
+        if plan is not None and plan.skip_when_fresh and plan.entries and not plan.is_fresh():
+            with torch.no_grad():
+                plan.run()
 
     def _state_tensors(self):
         """Every tensor a training step mutates: parameters, BN buffers, momenta, metrics."""
@@ -126,6 +138,7 @@ class TrainStep:
             restore()
             raise
         restore()
+        self._fresh_operands()   # (the restore rewrote the masters: the capture sees current operands)
         # If this is the run's first step, the restored momenta are zero and the captured
         # steady-state rule buf = 0.9 * buf + d equals the first-step rule buf = d (dampening 0),
         # so the graph is exact from its first replay; keep recording the steady-state rule.
@@ -163,6 +176,7 @@ class TrainStep:
             if self.graph is not None:
                 self.static_idx.copy_(idx)
                 self.opt.sync_lr()
+                self._fresh_operands()
                 self.graph.replay()
                 self.last_loss = self.static_loss
                 return self.last_loss

@@ -218,11 +218,42 @@ class _PrepEntry:
 
 
 class WeightPrepPlan:
+    """The model's bf16 conv operands, refreshed from the fp32 masters in one launch.
+
+    With a fused optimizer attached (``SGD.attach_weight_prep``) the optimizer step itself writes
+    the operands from the updated masters (sgd_prep_kernel), and the forward pre-hook skips the
+    refresh while the masters are unchanged since the operands were last written. "Unchanged" is
+    tracked through the autograd version counters of every weight and of the parameter arena
+    (in-place writes, checkpoint loads and snapshot restores all bump them); writers that bypass
+    them (the native optimizer kernels) either refresh the operands themselves or ``invalidate``.
+    """
+
     def __init__(self):
         self.entries = []
         self.by_id = {}
         self.tables = None
         self.owner = None
+        self.skip_when_fresh = False   # set by a fused optimizer
+        self.watch = ()                # extra tensors whose versions guard freshness (the arena)
+        self.fresh_key = None
+
+    def _key(self):
+        return (tuple(e.w._version for e in self.entries), tuple(t._version for t in self.watch),
+                self.tables[2] if self.tables is not None else None)
+
+    def is_fresh(self):
+        return self.fresh_key is not None and self.tables is not None and self.fresh_key == self._key()
+
+    def mark_fresh(self):
+        self.fresh_key = self._key() if self.tables is not None else None
+
+    def invalidate(self):
+        self.fresh_key = None
+
+    def ensure_tables(self):
+        if self.entries and (self.tables is None or self.tables[2] != tuple(G.physical(e.w).data_ptr() for e in self.entries)):
+            self._build()
+        return self.tables
 
     def lookup(self, w, groups):
         e = self.by_id.get(id(w))
@@ -249,6 +280,7 @@ class WeightPrepPlan:
         self.entries.append(e)
         self.by_id[id(w)] = e
         self.tables = None
+        self.fresh_key = None
         return e
 
     def _build(self):
@@ -283,9 +315,9 @@ class WeightPrepPlan:
     def run(self):
         if not self.entries:
             return
-        if self.tables is None or self.tables[2] != tuple(G.physical(e.w).data_ptr() for e in self.entries):
-            self._build()
+        self.ensure_tables()
         _C().weight_prep_multi(self.tables[0], self.tables[1])
+        self.mark_fresh()
 
 
 def _plan_pre_hook(module, args):
@@ -293,7 +325,8 @@ def _plan_pre_hook(module, args):
     # replicas made by torch DataParallel share __dict__ entries: only the owner runs the plan
     if plan is not None and plan.owner == id(module) and not _FORCE_REFERENCE and \
             next(iter(module.parameters())).is_cuda:
-        plan.run()
+        if not (plan.skip_when_fresh and plan.is_fresh()):
+            plan.run()
         _PLAN["cur"] = plan
 
 
