@@ -133,10 +133,11 @@ void maxpool_bwd_launch(const bf16*, const uint8_t*, int, int, int, int, int, in
 void ce_fused_launch(const float*, const int64_t*, int, int, float*, float*, double*, hipStream_t);
 void scale_by_scalar_launch(const float*, const float*, size_t, float*, hipStream_t);
 void sgd_launch(const int64_t*, int, float* const*, const float* const*, float* const*,
-                bf16* const*, const float*, float, float, float, float, int, int, hipStream_t);
+                bf16* const*, const float*, float, float, float, float, int, int, hipStream_t,
+                int zero_grad);
 void sgd_prep_launch(const int64_t*, int, float* const*, const float* const*, float* const*,
                      const float*, float, float, float, float, int, int, const int64_t*,
-                     const int64_t*, int, const int64_t*, hipStream_t);
+                     const int64_t*, int, const int64_t*, hipStream_t, int zero_grad);
 void se_scale_fwd_launch(const bf16*, const float*, int, int, int, bf16*, hipStream_t);
 struct CatArgs {
   const bf16* src[8];
@@ -1190,14 +1191,14 @@ Tensor scale_by_scalar(const Tensor& g, const Tensor& s) {
 // ptr tables are int64 GPU tensors holding device addresses; chunks [n,3] int64 on GPU
 void sgd_step(const Tensor& chunks, const Tensor& pptr, const Tensor& gptr, const Tensor& bptr,
               const optional<Tensor>& sptr, const Tensor& lr, double momentum, double dampening,
-              double wd, double grad_scale, bool nesterov, bool first) {
+              double wd, double grad_scale, bool nesterov, bool first, bool zero_grad) {
   TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == at::kLong, "chunks");
   TORCH_CHECK(lr.is_cuda() && lr.scalar_type() == at::kFloat, "lr must be a GPU fp32 scalar");
   pca::sgd_launch(ptr<int64_t>(chunks), chunks.size(0), ptr<float* const>(pptr),
                   ptr<const float* const>(gptr), ptr<float* const>(bptr),
                   sptr.has_value() && sptr->defined() ? ptr<bf16* const>(*sptr) : nullptr,
                   ptr<float>(lr), (float)momentum, (float)dampening, (float)wd, (float)grad_scale,
-                  nesterov ? 1 : 0, first ? 1 : 0, cur_stream());
+                  nesterov ? 1 : 0, first ? 1 : 0, cur_stream(), zero_grad ? 1 : 0);
 }
 
 // optimizer step + bf16 operand refresh in one launch: `chunks` (SGD chunks of the arena ranges
@@ -1206,7 +1207,7 @@ void sgd_step(const Tensor& chunks, const Tensor& pptr, const Tensor& gptr, cons
 void sgd_prep_step(const Tensor& chunks, const Tensor& pptr, const Tensor& gptr, const Tensor& bptr,
                    const Tensor& lr, double momentum, double dampening, double wd,
                    double grad_scale, bool nesterov, bool first, const Tensor& desc,
-                   const Tensor& pchunks, const Tensor& gm) {
+                   const Tensor& pchunks, const Tensor& gm, bool zero_grad) {
   for (const Tensor* t : {&chunks, &pptr, &gptr, &bptr, &desc, &pchunks, &gm})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous(),
                 "sgd_prep_step tables: contiguous int64 on the GPU");
@@ -1220,7 +1221,7 @@ void sgd_prep_step(const Tensor& chunks, const Tensor& pptr, const Tensor& gptr,
                        ptr<const float* const>(gptr), ptr<float* const>(bptr), ptr<float>(lr),
                        (float)momentum, (float)dampening, (float)wd, (float)grad_scale,
                        nesterov ? 1 : 0, first ? 1 : 0, ptr<int64_t>(desc), ptr<int64_t>(pchunks),
-                       (int)pchunks.size(0), ptr<int64_t>(gm), cur_stream());
+                       (int)pchunks.size(0), ptr<int64_t>(gm), cur_stream(), zero_grad ? 1 : 0);
 }
 
 Tensor se_scale_fwd(const Tensor& x, const Tensor& s) {
@@ -1558,8 +1559,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("ce_fused", &ce_fused);
   m.def("scale_by_scalar", &scale_by_scalar);
-  m.def("sgd_step", &sgd_step);
-  m.def("sgd_prep_step", &sgd_prep_step);
+  m.def("sgd_step", &sgd_step, py::arg("chunks"), py::arg("pptr"), py::arg("gptr"), py::arg("bptr"),
+        py::arg("sptr"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"),
+        py::arg("grad_scale"), py::arg("nesterov"), py::arg("first"), py::arg("zero_grad") = false);
+  m.def("sgd_prep_step", &sgd_prep_step, py::arg("chunks"), py::arg("pptr"), py::arg("gptr"),
+        py::arg("bptr"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"),
+        py::arg("grad_scale"), py::arg("nesterov"), py::arg("first"), py::arg("desc"),
+        py::arg("pchunks"), py::arg("gm"), py::arg("zero_grad") = false);
   m.def("se_scale_fwd", &se_scale_fwd);
   m.def("se_scale_bwd", &se_scale_bwd);
   m.def("dpn_merge_fwd", &dpn_merge_fwd);

@@ -34,6 +34,7 @@ struct HaloGeom {
   int HI;                 // halo DMA instructions per stage = ceil(HR / 8)
   int chunk, splits, atomic;
   int ablate;             // diagnostics (PCA_HALO_ABLATE): 1 = no DMA, 2 = no MFMA phase, 4 = no epilogue
+  int xcd;                // XCD-aware block order (PCA_HALO_XCD=1; default: dispatch order)
   uint32_t x_bytes, dy_bytes;
   FastDiv fd_hw, fd_w;
 };
@@ -124,12 +125,24 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const int split = blockIdx.z % g.splits;
-  const int grp = blockIdx.z / g.splits;
-  const int m0 = blockIdx.x * BM;              // output channel tile (within group)
+  // XCD-aware block order: consecutive workgroups go to consecutive XCDs, so the tiles of one
+  // pixel split (which stage the same X halo and dY rows) were spread over all eight L2s. The
+  // remap gives each XCD a contiguous range of the (split, tile) order: one split's tiles share
+  // an L2, and the staged pixels are fetched beyond it once per XCD instead of once per tile.
+  const int gxy = gridDim.x * gridDim.y;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (g.xcd) {
+    const int q = xcd_remap(bx + gridDim.x * (by + gridDim.y * bz), gxy * gridDim.z);
+    bx = q % gridDim.x;
+    by = (q / gridDim.x) % gridDim.y;
+    bz = q / gxy;
+  }
+  const int split = bz % g.splits;
+  const int grp = bz / g.splits;
+  const int m0 = bx * BM;                      // output channel tile (within group)
   const int cinb = g.cin_g / 64;
-  const int cib = (int)blockIdx.y % cinb;      // 64-channel input block
-  const int tap0 = TG == 9 ? 0 : ((int)blockIdx.y / cinb) * 3;   // first tap of this row
+  const int cib = by % cinb;                   // 64-channel input block
+  const int tap0 = TG == 9 ? 0 : (by / cinb) * 3;   // first tap of this row
   const int p_begin = split * g.chunk;
   const int p_end = min(g.P, p_begin + g.chunk);
 
@@ -270,7 +283,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
     // store tail alone took ~18 us of the ~25 us kernel on the bs128 shard: 256 blocks x 147 KB).
     // halo_slab_reduce_kernel maps the order back to dW[co][tap][ci].
     const int tiles = gridDim.x * gridDim.y * g.groups;
-    const int tile = (grp * gridDim.x + blockIdx.x) * gridDim.y + blockIdx.y;
+    const int tile = (grp * gridDim.x + bx) * gridDim.y + by;
     float4* dst4 = reinterpret_cast<float4*>(out) + (size_t)(split * tiles + tile) * (BM * BN / 4);
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
@@ -488,6 +501,12 @@ static bool halo_geom(HaloGeom& g, int N, int H, int W, int Cin, int Cout, int g
     return e ? atoi(e) : 0;
   }();
   g.ablate = abl;
+  // (measured neutral on the ResNet-18 wgrad shapes at bs1024 and bs128: off by default)
+  static const int xcd = [] {
+    const char* e = getenv("PCA_HALO_XCD");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  g.xcd = xcd;
   return true;
 }
 

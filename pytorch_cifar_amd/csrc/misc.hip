@@ -635,6 +635,7 @@ struct SgdArgs {
   const float* lr;         // device scalar (graph-capture friendly)
   float momentum, dampening, wd, grad_scale;
   int nesterov, first;
+  int zero_grad;           // clear each gradient after reading it (the next step's zero_grad)
 };
 
 // one element of the update with explicit FMAs, shared by every SGD path (the plain chunks and
@@ -679,6 +680,7 @@ __device__ __forceinline__ void sgd_chunk(const SgdArgs& a, int blk) {
                          a.nesterov, a.first);
       if (a.momentum != 0.f) b4[i] = make_float4(bf[0], bf[1], bf[2], bf[3]);
       p4[i] = make_float4(pf[0], pf[1], pf[2], pf[3]);
+      if (a.zero_grad) const_cast<float4*>(g4)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     return;
   }
@@ -688,6 +690,7 @@ __device__ __forceinline__ void sgd_chunk(const SgdArgs& a, int blk) {
                               a.grad_scale, a.nesterov, a.first);
     if (a.momentum != 0.f) b[i] = bv;
     p[i] = np;
+    if (a.zero_grad && g) const_cast<float*>(g)[i] = 0.f;
     if (sh) sh[i] = f2bf(np);
   }
 }
@@ -701,7 +704,7 @@ struct SgdUpd {
   const int64_t* gm;       // [tensors][2] {grad, momentum} pointers parallel to the prep desc
   const float* lr;
   float momentum, dampening, wd, grad_scale;
-  int nesterov, first;
+  int nesterov, first, zero_grad;
 };
 
 __device__ __forceinline__ float sgd_upd(const SgdUpd& u, float lr, float* w, const float* g,
@@ -711,6 +714,7 @@ __device__ __forceinline__ float sgd_upd(const SgdUpd& u, float lr, float* w, co
                             u.nesterov, u.first);
   if (u.momentum != 0.f) m[i] = bv;
   w[i] = np;
+  if (u.zero_grad) const_cast<float*>(g)[i] = 0.f;
   return np;
 }
 
@@ -1639,19 +1643,19 @@ void scale_by_scalar_launch(const float* g, const float* s, size_t n, float* out
 void sgd_launch(const int64_t* chunks, int nchunks, float* const* params, const float* const* grads,
                 float* const* bufs, bf16* const* shadows, const float* lr, float momentum,
                 float dampening, float wd, float grad_scale, int nesterov, int first,
-                hipStream_t st) {
+                hipStream_t st, int zero_grad) {
   SgdArgs a{chunks, params, grads, bufs, shadows, lr, momentum, dampening, wd, grad_scale,
-            nesterov, first};
+            nesterov, first, zero_grad};
   hipLaunchKernelGGL(sgd_kernel, dim3(nchunks), dim3(256), 0, st, a);
 }
 void sgd_prep_launch(const int64_t* chunks, int nchunks, float* const* params,
                      const float* const* grads, float* const* bufs, const float* lr, float momentum,
                      float dampening, float wd, float grad_scale, int nesterov, int first,
                      const int64_t* desc, const int64_t* pchunks, int npchunks, const int64_t* gm,
-                     hipStream_t st) {
+                     hipStream_t st, int zero_grad) {
   SgdArgs a{chunks, params, grads, bufs, nullptr, lr, momentum, dampening, wd, grad_scale,
-            nesterov, first};
-  SgdUpd u{gm, lr, momentum, dampening, wd, grad_scale, nesterov, first};
+            nesterov, first, zero_grad};
+  SgdUpd u{gm, lr, momentum, dampening, wd, grad_scale, nesterov, first, zero_grad};
   if (nchunks + npchunks > 0)
     hipLaunchKernelGGL(sgd_prep_kernel, dim3(nchunks + npchunks), dim3(256), 0, st, a, nchunks, desc,
                        pchunks, u);

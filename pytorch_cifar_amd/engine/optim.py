@@ -36,6 +36,10 @@ class SGD(torch.optim.Optimizer):
         self._lr_host = {}
         self._tables = {}
         self.capturing = False
+        # arena step only: clear each gradient after reading it (the trainer then skips the next
+        # zero_grad fill); _zeroed_grads reports whether the last step did
+        self.zero_grad_in_step = False
+        self._zeroed_grads = False
 
     # -------------------------------------------------------------------------- helpers
     def sync_lr(self):
@@ -194,17 +198,20 @@ class SGD(torch.optim.Optimizer):
                 _native.lib().sgd_prep_step(chunks, pp, gp, bp, lr, group["momentum"],
                                             group["dampening"], group["weight_decay"],
                                             self.grad_scale, group["nesterov"], self._arena_first,
-                                            plan.tables[0], plan.tables[1], gm)
+                                            plan.tables[0], plan.tables[1], gm,
+                                            self.zero_grad_in_step)
                 plan.mark_fresh()      # masters and operands updated together, versions untouched
             else:
                 chunks, pp, gp, bp = self._table(0, [arena.param_flat], [arena.grad_flat], [arena.mom_flat])
                 _native.lib().sgd_step(chunks, pp, gp, bp, None, lr, group["momentum"], group["dampening"],
                                        group["weight_decay"], self.grad_scale, group["nesterov"],
-                                       self._arena_first)
+                                       self._arena_first, self.zero_grad_in_step)
                 if plan is not None:
                     plan.invalidate()   # raw-pointer update: the operands are stale
             self._arena_first = False
+            self._zeroed_grads = self.zero_grad_in_step
             return loss
+        self._zeroed_grads = False
         for i, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:

@@ -41,6 +41,12 @@ class TrainStep:
             if getattr(optimizer, "arena", None) is not None and hasattr(optimizer, "attach_weight_prep") \
                     and os.environ.get("PCA_FUSED_SGD_PREP", "1") != "0":
                 optimizer.attach_weight_prep(inner.__dict__["_pca_wplan"])
+        # the arena step clears the gradients it consumed, so the next step needs no zero_grad
+        # fill (one launch and a full gradient-arena write per step)
+        if getattr(optimizer, "arena", None) is not None and hasattr(optimizer, "zero_grad_in_step") \
+                and os.environ.get("PCA_SGD_ZERO_GRAD", "1") != "0":
+            optimizer.zero_grad_in_step = True
+        self._grads_clean = False
         self.ddp = ddp
         self.device = loader.device
         self.metrics = metrics if metrics is not None else torch.zeros(3, dtype=torch.float64, device=self.device)
@@ -54,7 +60,9 @@ class TrainStep:
     def _body(self, idx):
         with trace_range("data"):
             x, y = self.loader.make_batch(idx)
-        self.opt.zero_grad()
+        if not self._grads_clean:
+            self.opt.zero_grad()
+        self._grads_clean = False
         with trace_range("forward"):
             out = self.net(x)
             loss = cross_entropy(out, y, self.metrics)
@@ -64,6 +72,7 @@ class TrainStep:
                 self.ddp.finish()
         with trace_range("optimizer"):
             self.opt.step()
+        self._grads_clean = bool(getattr(self.opt, "_zeroed_grads", False))
         return loss
 
     def _fresh_operands(self):
@@ -144,6 +153,8 @@ class TrainStep:
         # so the graph is exact from its first replay; keep recording the steady-state rule.
         if first and self.opt.param_groups[0].get("dampening", 0) != 0:
             raise RuntimeError("hipGraph capture of the first SGD step needs dampening == 0")
+        if first:
+            self.opt._arena_first = False   # record the steady-state rule (see above)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         self.opt.capturing = True
@@ -152,7 +163,7 @@ class TrainStep:
                 self.static_loss = self._body(self.static_idx)
         except BaseException:
             self.opt.capturing = False
-            restore()
+            restore()                      # (also puts back the first-step flag)
             raise
         finally:
             self.opt.capturing = False

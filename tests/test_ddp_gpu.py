@@ -65,6 +65,7 @@ def _build(model_name, batch, graph, bucket_mb):
     loader = DeviceLoader(imgs, labs, batch, dev, train=True, crop_pad=4, flip=True, seed=0,
                           drop_last=True)
     step = TrainStep(ddp, opt, loader, batch, ddp=ddp, graph=graph)
+    opt.zero_grad_in_step = False   # keep the step's gradients readable after it (compared below)
     return step, ddp, arena, rec, loader
 
 
