@@ -163,6 +163,11 @@ void dw_fwd_launch(const bf16*, const float*, int, int, int, int, int, int, int,
 void dw_dgrad_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int, int,
                      int, bf16*, hipStream_t);
 int dw_wgrad_partials(int, int, int);
+bool dw_fwd_stats_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int,
+                         int, int, bf16*, float*, int, hipStream_t);
+bool dw_dgrad_bn_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int,
+                        int, int, bf16*, const bf16*, const uint8_t*, const float*, int, float*,
+                        int, hipStream_t);
 void dw_wgrad_launch(const bf16*, const bf16*, int, int, int, int, int, int, int, int, int, int,
                      int, float*, int, int, float*, hipStream_t);
 // conv_direct.hip
@@ -1382,6 +1387,58 @@ Tensor dw_dgrad(const Tensor& dy, const Tensor& wT, int H, int W, int C, int KH,
   return dx;
 }
 
+// forward + the consumer BN's statistics added into its zeroed sharded accumulator
+// [rows][2][Co]; returns {y, flag} with flag = 1 when the fused kernel ran (else nothing added)
+std::vector<Tensor> dw_fwd_stats(const Tensor& x, const Tensor& wT, int KH, int KW, int stride,
+                                 int pad, const Tensor& acc, int acc_rows) {
+  check_bf16(x, "x");
+  check_f32(wT, "wT");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Co = wT.size(1);
+  TORCH_CHECK(wT.size(0) == KH * KW, "wT [KH*KW][Co]");
+  const int Ho = out_dim(H, KH, stride, pad), Wo = out_dim(W, KW, stride, pad);
+  check_acc(acc, acc_rows, 2, Co);
+  auto y = at::empty({N, Ho, Wo, Co}, x.options());
+  const bool ok = pca::dw_fwd_stats_launch(ptr<bf16>(x), ptr<float>(wT), N, H, W, C, Ho, Wo, Co,
+                                           KH, KW, stride, pad, ptr<bf16>(y), ptr<float>(acc),
+                                           acc_rows, cur_stream());
+  if (!ok)
+    pca::dw_fwd_launch(ptr<bf16>(x), ptr<float>(wT), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad,
+                       ptr<bf16>(y), cur_stream());
+  return {y, at::full({1}, ok ? 1 : 0, x.options().dtype(at::kInt).device(at::kCPU))};
+}
+
+// dgrad + the backward reduce of the BN(+act) that produced x, added into that BN's zeroed
+// backward accumulator [rows][2][C] (act 1: ReLU via the 1-bit mask, 2: swish via aux rows
+// scale | shift); returns {dx, flag}
+std::vector<Tensor> dw_dgrad_bn(const Tensor& dy, const Tensor& wT, int H, int W, int C, int KH,
+                                int KW, int stride, int pad, const Tensor& bn_y,
+                                const optional<Tensor>& bn_mask, const Tensor& bn_aux, int act,
+                                const Tensor& acc, int acc_rows) {
+  check_bf16(dy, "dy");
+  check_f32(wT, "wT");
+  check_bf16(bn_y, "bn_y");
+  check_f32(bn_aux, "bn_aux");
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo, "geometry");
+  TORCH_CHECK(bn_y.numel() == (int64_t)N * H * W * C && bn_y.is_contiguous(), "bn_y must match dx");
+  TORCH_CHECK(bn_aux.numel() >= (act == 2 ? 4 : 2) * C, "bn_aux [mean|istd|scale|shift][C]");
+  const bool has_mask = bn_mask.has_value() && bn_mask->defined();
+  if (has_mask)
+    TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == bn_y.numel(),
+                "bn_mask: one bit per element");
+  check_acc(acc, acc_rows, 2, C);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  const bool ok = pca::dw_dgrad_bn_launch(
+      ptr<bf16>(dy), ptr<float>(wT), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad, ptr<bf16>(dx),
+      ptr<bf16>(bn_y), has_mask ? bn_mask->data_ptr<uint8_t>() : nullptr, ptr<float>(bn_aux), act,
+      ptr<float>(acc), acc_rows, cur_stream());
+  if (!ok)
+    pca::dw_dgrad_launch(ptr<bf16>(dy), ptr<float>(wT), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad,
+                         ptr<bf16>(dx), cur_stream());
+  return {dx, at::full({1}, ok ? 1 : 0, dy.options().dtype(at::kInt).device(at::kCPU))};
+}
+
 // returns dw fp32 [Cout, KH*KW]
 // dW [Co, KH*KW] fp32; with `accum` given (fp32, Co*KH*KW contiguous, e.g. the parameter's view
 // of the gradient arena) the result is added into it by the final reduce and `accum` returned
@@ -1559,6 +1616,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("ce_fused", &ce_fused);
   m.def("scale_by_scalar", &scale_by_scalar);
+  m.def("dw_fwd_stats", &dw_fwd_stats);
+  m.def("dw_dgrad_bn", &dw_dgrad_bn);
   m.def("sgd_step", &sgd_step, py::arg("chunks"), py::arg("pptr"), py::arg("gptr"), py::arg("bptr"),
         py::arg("sptr"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"),
         py::arg("grad_scale"), py::arg("nesterov"), py::arg("first"), py::arg("zero_grad") = false);

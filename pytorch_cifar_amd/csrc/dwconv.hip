@@ -481,6 +481,239 @@ __global__ __launch_bounds__(256) void dw_wgrad_final4_kernel(const float* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused BatchNorm epilogues (k3 / k5, stride 1 or 2, 8-channel vectors).
+//   MODE 1 (forward): per-channel (sum, sumsq) of the output — the statistics of the BN that
+//          consumes it, so that BN runs no separate statistics + finalize passes;
+//   MODE 2 / 3 (dgrad): the backward reduce of the BN(+act) that produced this conv's input —
+//          sum dz and sum dz * xhat, dz = dX * relu'(1-bit mask) (2) or dX * swish'(z),
+//          z = y * scale + shift (3) — so that BN's backward runs no reduce + finalize passes.
+// Channel-tiled mapping: a block owns CT (<= 8) channel groups of 8 and a share of the pixel
+// strips, so its flush into the sharded accumulator is 2 x 64 columns (the plain kernels' mapping
+// put every channel in every block: 2C atomics per block, ~16 MB of atomics per launch at
+// MobileNetV2 bs1024 and 1.1-1.7x the plain time).
+// ---------------------------------------------------------------------------------------
+struct DwEpi {
+  int mode;
+  float* part;            // accumulator [shards][2][C]
+  int shards;
+  const bf16* y;          // dgrad modes: the BN input
+  const uint8_t* mask;    // mode 2
+  const float* aux;       // [mean | istd | scale | shift][C]
+};
+
+template <int MODE>
+__device__ __forceinline__ void dw_epi_acc(const float* acc, const uint4& packed, const uint4& yv,
+                                           uint32_t mb, const float* ax, float* s1, float* s2) {
+  // ax: LDS [4][8] of this thread's channels (mean, istd, scale, shift)
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      s1[v] += acc[v];
+      s2[v] += acc[v] * acc[v];
+    }
+  } else {
+    float f[8], yy[8];
+    unpack8(packed, f);
+    unpack8(yv, yy);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      float dz;
+      if constexpr (MODE == 2) dz = ((mb >> v) & 1u) ? f[v] : 0.f;
+      else dz = f[v] * act_grad(yy[v] * ax[16 + v] + ax[24 + v], ACT_SWISH);
+      s1[v] += dz;
+      s2[v] += dz * (yy[v] - ax[v]) * ax[8 + v];
+    }
+  }
+}
+
+// block tile geometry: CT groups x (256 / CT) workers
+struct DwTile {
+  int ct, ntile, gl, wk, nwk, g0, part, parts;
+  __device__ DwTile(int G) {
+    ct = G < 8 ? G : 8;
+    ntile = (G + ct - 1) / ct;
+    gl = threadIdx.x % ct;
+    wk = threadIdx.x / ct;
+    nwk = 256 / ct;
+    const int tile = blockIdx.x % ntile;
+    g0 = tile * ct;
+    part = blockIdx.x / ntile;
+    parts = gridDim.x / ntile;
+  }
+};
+
+// LDS: aux [CT*8][4 rows interleaved per channel group] then the flush sums [2][CT*8]
+template <int MODE>
+__device__ __forceinline__ void dw_epi_setup(const DwEpi& e, const DwTile& t, int G, int C,
+                                             float* ax_s, float* red) {
+  const int nch = t.ct * 8;
+  for (int k = threadIdx.x; k < 2 * nch; k += 256) red[k] = 0.f;
+  if constexpr (MODE >= 2) {
+    for (int k = threadIdx.x; k < t.ct * 32; k += 256) {
+      const int gl = k / 32, r = (k / 8) % 4, v = k % 8;
+      const int c = (t.g0 + gl) * 8 + v;
+      ax_s[k] = (t.g0 + gl < G) ? e.aux[r * C + c] : 0.f;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void dw_epi_flush2(const DwEpi& e, const DwTile& t, bool has, int C,
+                                              const float* s1, const float* s2, float* red) {
+  const int nch = t.ct * 8;
+  if (has) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      atomicAdd(red + t.gl * 8 + v, s1[v]);
+      atomicAdd(red + nch + t.gl * 8 + v, s2[v]);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 2 * nch; k += 256) {
+    const int half = k / nch, cc = k % nch;
+    const int c = t.g0 * 8 + cc;
+    if (c < C) stat_out(e.part, blockIdx.x, e.shards, 2 * C, half * C + c, red[k]);
+  }
+}
+
+template <int K, int S, bool FLIP, int MODE>
+__global__ __launch_bounds__(256) void dwk_epi_kernel(const bf16* __restrict__ x,
+                                                      const float* __restrict__ wT, DwGeom g,
+                                                      int rpt, bf16* __restrict__ y, DwEpi e) {
+  constexpr int KK = K * K;
+  constexpr int V = 8;
+  using T = uint4;
+  __shared__ float ax_s[8 * 32];
+  __shared__ float red[2 * 64];
+  const int G = g.C / V;
+  const DwTile t(G);
+  dw_epi_setup<MODE>(e, t, G, g.Co, ax_s, red);
+  const int gi = t.g0 + t.gl;
+  const bool active = t.wk < t.nwk && gi < G;
+  const int c = gi * V;
+  const int nstrip = (g.Ho + rpt - 1) / rpt;
+  const int items = g.N * nstrip * g.Wo;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) s1[v] = s2[v] = 0.f;
+  if (active) {
+    float w[KK][V];
+#pragma unroll
+    for (int tp = 0; tp < KK; ++tp) {
+      const int src = FLIP ? KK - 1 - tp : tp;
+#pragma unroll
+      for (int v4 = 0; v4 < V; v4 += 4) {
+        const float4 wv = *reinterpret_cast<const float4*>(wT + src * g.Co + c + v4);
+        w[tp][v4] = wv.x; w[tp][v4 + 1] = wv.y; w[tp][v4 + 2] = wv.z; w[tp][v4 + 3] = wv.w;
+      }
+    }
+    const float* ax = ax_s + t.gl * 32;
+    for (int j = t.part * t.nwk + t.wk; j < items; j += t.parts * t.nwk) {
+      const int ow = j % g.Wo;
+      const int q = j / g.Wo;
+      const int strip = q % nstrip;
+      const int n = q / nstrip;
+      const bf16* xn = x + (size_t)n * g.H * g.W * g.C + c;
+      const int oh0 = strip * rpt, oh1 = min(g.Ho, oh0 + rpt);
+      const int iw0 = ow * S - g.p;
+      T win[K][K];
+#pragma unroll
+      for (int k = 0; k < K - S; ++k) dwk_load_row<K, V>(xn, g, oh0 * S - g.p + k, iw0, win[k]);
+      bf16* yr = y + (((size_t)n * g.Ho + oh0) * g.Wo + ow) * g.Co + c;
+#pragma unroll 1
+      for (int oh = oh0; oh < oh1; ++oh) {
+        const int ih0 = oh * S - g.p;
+#pragma unroll
+        for (int k = K - S; k < K; ++k) dwk_load_row<K, V>(xn, g, ih0 + k, iw0, win[k]);
+        const size_t o = (size_t)(yr - y);
+        uint4 yv = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t mb = 0;
+        if constexpr (MODE >= 2) yv = *reinterpret_cast<const uint4*>(e.y + o);
+        if constexpr (MODE == 2) mb = e.mask[o >> 3];
+        float acc[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw) {
+            float f[V];
+            dw_unpack<V>(win[kh][kw], f);
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[v] += f[v] * w[kh * K + kw][v];
+          }
+        const uint4 packed = pack8(acc);
+        *reinterpret_cast<uint4*>(yr) = packed;
+        dw_epi_acc<MODE>(acc, packed, yv, mb, ax, s1, s2);
+        yr += (size_t)g.Wo * g.Co;
+        dwk_roll<K, S>(win);
+      }
+    }
+  }
+  dw_epi_flush2(e, t, active, g.Co, s1, s2, red);
+}
+
+// stride-2 dgrad (the parity-exact tap walk of dwk_dgrad_s2_kernel) with MODE 2 / 3
+template <int K, int MODE>
+__global__ __launch_bounds__(256) void dwk_epi_s2_kernel(const bf16* __restrict__ dy,
+                                                         const float* __restrict__ wT, DwGeom g,
+                                                         bf16* __restrict__ dx, DwEpi e) {
+  __shared__ float ax_s[8 * 32];
+  __shared__ float red[2 * 64];
+  const int G = g.C >> 3;
+  const DwTile t(G);
+  dw_epi_setup<MODE>(e, t, G, g.C, ax_s, red);
+  const int gi = t.g0 + t.gl;
+  const bool active = t.wk < t.nwk && gi < G;
+  const int c = gi * 8;
+  const int items = g.N * g.H * g.W;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) s1[v] = s2[v] = 0.f;
+  if (active) {
+    const float* ax = ax_s + t.gl * 32;
+    for (int j = t.part * t.nwk + t.wk; j < items; j += t.parts * t.nwk) {
+      const int iw = j % g.W;
+      const int q = j / g.W;
+      const int ih = q % g.H;
+      const int n = q / g.H;
+      const size_t o = (size_t)j * g.C + c;
+      uint4 yv = *reinterpret_cast<const uint4*>(e.y + o);
+      uint32_t mb = 0;
+      if constexpr (MODE == 2) mb = e.mask[o >> 3];
+      float acc[8];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) acc[v] = 0.f;
+      const int kh0 = (ih + g.p) & 1, kw0 = (iw + g.p) & 1;
+      const bf16* dyn = dy + (size_t)n * g.Ho * g.Wo * g.Co + c;
+#pragma unroll
+      for (int th = 0; th < (K + 1) / 2; ++th) {
+        const int kh = kh0 + 2 * th;
+        const int oh = (ih + g.p - kh) >> 1;
+        if (kh >= K || (unsigned)oh >= (unsigned)g.Ho) continue;
+#pragma unroll
+        for (int tw = 0; tw < (K + 1) / 2; ++tw) {
+          const int kw = kw0 + 2 * tw;
+          const int ow = (iw + g.p - kw) >> 1;
+          if (kw >= K || (unsigned)ow >= (unsigned)g.Wo) continue;
+          float f[8];
+          unpack8(*reinterpret_cast<const uint4*>(dyn + (oh * g.Wo + ow) * g.Co), f);
+          const float* wr = wT + (kh * K + kw) * g.Co + c;
+          const float4 w0 = *reinterpret_cast<const float4*>(wr);
+          const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
+          acc[0] += f[0] * w0.x; acc[1] += f[1] * w0.y; acc[2] += f[2] * w0.z; acc[3] += f[3] * w0.w;
+          acc[4] += f[4] * w1.x; acc[5] += f[5] * w1.y; acc[6] += f[6] * w1.z; acc[7] += f[7] * w1.w;
+        }
+      }
+      const uint4 packed = pack8(acc);
+      *reinterpret_cast<uint4*>(dx + o) = packed;
+      dw_epi_acc<MODE>(acc, packed, yv, mb, ax, s1, s2);
+    }
+  }
+  dw_epi_flush2(e, t, active, g.C, s1, s2, red);
+}
+
 // ================================================================================ host
 static DwGeom dwg(int N, int H, int W, int C, int Ho, int Wo, int Co, int KH, int KW, int s, int p) {
   DwGeom g{N, H, W, C, Ho, Wo, Co, KH, KW, s, p, Co / C};
@@ -557,6 +790,71 @@ static void dwk_wgrad_t(const bf16* x, const bf16* dy, const DwGeom& g, int chun
     hipLaunchKernelGGL((dwk_wgrad_kernel<K, 1, V>), grid, block, 0, st, x, dy, g, rpt, GB, partial);
   else
     hipLaunchKernelGGL((dwk_wgrad_kernel<K, 2, V>), grid, block, 0, st, x, dy, g, rpt, GB, partial);
+}
+
+// k3 with 8-channel groups
+static bool dw_epi_ok(const DwGeom& g) {
+  // (k5 x 8 channels holds 200 weight registers: one wave per SIMD — k5 keeps the plain passes)
+  return dwk_kind(g) == 3 && g.C % 8 == 0 && g.mult == 1;
+}
+
+// blocks: channel tiles x pixel parts, ~2048 in all (2 x 64 accumulator adds each)
+static int dw_epi_blocks(int G, int items) {
+  const int ct = G < 8 ? G : 8;
+  const int ntile = cdiv(G, ct);
+  const int nwk = 256 / ct;
+  int parts = std::max(1, std::min(cdiv(items, nwk), cdiv(2048, ntile)));
+  return ntile * parts;
+}
+
+template <int MODE>
+static void dw_epi_launch(int kind, bool flip, const bf16* x, const float* wT, const DwGeom& g,
+                          bf16* y, const DwEpi& e, hipStream_t st) {
+  const int rpt = dwk_rpt(g.Ho);
+  const int items = g.N * cdiv(g.Ho, rpt) * g.Wo;
+  const dim3 grid(dw_epi_blocks(g.C / 8, items)), block(256);
+#define PCA_DWE(K, S, F) \
+  hipLaunchKernelGGL((dwk_epi_kernel<K, S, F, MODE>), grid, block, 0, st, x, wT, g, rpt, y, e)
+  (void)kind;   // k3 only (dw_epi_ok)
+  if (g.s == 2) PCA_DWE(3, 2, false);
+  else if (flip) PCA_DWE(3, 1, true);
+  else PCA_DWE(3, 1, false);
+#undef PCA_DWE
+}
+
+// forward with the consumer BN's statistics fused (mode 1); false: not launched
+bool dw_fwd_stats_launch(const bf16* x, const float* wT, int N, int H, int W, int C, int Ho,
+                         int Wo, int Co, int KH, int KW, int s, int p, bf16* y, float* acc,
+                         int shards, hipStream_t st) {
+  DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
+  if (!dw_epi_ok(g) || shards <= 0) return false;
+  const DwEpi e{1, acc, shards, nullptr, nullptr, nullptr};
+  dw_epi_launch<1>(dwk_kind(g), false, x, wT, g, y, e, st);
+  return true;
+}
+
+// dgrad with the producer BN's backward reduce fused (act 1: ReLU through the 1-bit mask, 2:
+// swish from y and aux); false: not launched
+bool dw_dgrad_bn_launch(const bf16* dy, const float* wT, int N, int H, int W, int C, int Ho,
+                        int Wo, int Co, int KH, int KW, int s, int p, bf16* dx, const bf16* bn_y,
+                        const uint8_t* bn_mask, const float* bn_aux, int act, float* acc,
+                        int shards, hipStream_t st) {
+  DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
+  if (!dw_epi_ok(g) || shards <= 0 || (act != 1 && act != 2) || (act == 1 && !bn_mask))
+    return false;
+  const DwEpi e{act == 1 ? 2 : 3, acc, shards, bn_y, bn_mask, bn_aux};
+  const int kind = dwk_kind(g);
+  if (s == 1) {
+    const DwGeom gd = dwg(N, Ho, Wo, Co, H, W, C, KH, KW, 1, KH - 1 - p);
+    if (act == 1) dw_epi_launch<2>(kind, true, dy, wT, gd, dx, e, st);
+    else dw_epi_launch<3>(kind, true, dy, wT, gd, dx, e, st);
+    return true;
+  }
+  const dim3 grid(dw_epi_blocks(C / 8, N * H * W)), block(256);
+  (void)kind;
+  if (act == 1) hipLaunchKernelGGL((dwk_epi_s2_kernel<3, 2>), grid, block, 0, st, dy, wT, g, dx, e);
+  else hipLaunchKernelGGL((dwk_epi_s2_kernel<3, 3>), grid, block, 0, st, dy, wT, g, dx, e);
+  return true;
 }
 
 void dw_fwd_launch(const bf16* x, const float* wT, int N, int H, int W, int C, int Ho, int Wo,

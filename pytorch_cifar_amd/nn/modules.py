@@ -46,6 +46,11 @@ class Conv2d(nn.Conv2d):
         if stats is not None:
             setattr(y, _STATS_ATTR, stats)
             y._pca_stats_src = self
+        elif want_stats and self.groups > 1 and self.groups == self.in_channels and \
+                self.bias is None:
+            # depthwise: no statistics until a fusable BN accepts them (it sets _pca_acc_ok); from
+            # then on the kernel adds them into the accumulator this module passes
+            y._pca_stats_src = self
         return y
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):

@@ -392,13 +392,15 @@ def set_fuse_bn_backward(on: bool) -> None:
 
 
 class _BNSrc:
-    __slots__ = ("y", "mask", "aux", "part", "dx", "acc")
+    __slots__ = ("y", "mask", "aux", "part", "dx", "acc", "act")
 
-    def __init__(self, y, mask, aux, acc=None):
+    def __init__(self, y, mask, aux, acc=None, act=1):
         self.y, self.mask, self.aux = y, mask, aux
         self.part = None
         self.dx = None
         self.acc = acc        # the BN's backward StatAcc (sharded-accumulator mode) or None
+        self.act = act        # 1: ReLU (1-bit mask); 2: swish (z from y and aux scale | shift;
+                              #    only the depthwise dgrad epilogue computes it)
 
 
 # ------------------------------------------------- sharded BatchNorm-sum accumulators
@@ -505,7 +507,7 @@ def _own_stats(bn, role, y_nhwc, stats):
 
 
 def _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add):
-    if src is None:
+    if src is None or src.act != 1 or src.mask is None:
         return C.conv_dgrad(dy, wt, H, W, stride, padding, groups, add)
     acc = src.acc
     if acc is not None:
@@ -679,17 +681,32 @@ class _ConvDirect(torch.autograd.Function):
 
 
 class _ConvDepthwise(torch.autograd.Function):
-    """Depthwise conv (groups == Cin, multiplier Cout/Cin), bandwidth-bound direct kernels."""
+    """Depthwise conv (groups == Cin, multiplier Cout/Cin), bandwidth-bound direct kernels.
+
+    With ``acc`` (the consuming BatchNorm's StatAcc) the forward kernel adds that BN's batch
+    statistics into it (``out[0]`` reports whether it did); with ``bnsrc`` (the producing
+    BN(+ReLU/swish) record) the dgrad kernel adds that BN's backward sums into its accumulator —
+    the two separate passes + finalize launches of each BN around a depthwise conv disappear
+    (mobilenetv2.py:33-36, efficientnet.py:96-103)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, padding):
+    def forward(ctx, x, weight, stride, padding, acc=None, bnsrc=None, out=None):
         C = _C()
         Co, _, KH, KW = weight.shape
         wT = _dw_weight(weight)
-        y = C.dw_fwd(x, wT, KH, KW, stride, padding)
+        if acc is not None:
+            acc.begin()
+            y, ok = C.dw_fwd_stats(x, wT, KH, KW, stride, padding, acc.buf, acc.R)
+            if not int(ok):
+                acc.state = "clean"           # nothing was added
+            elif out is not None:
+                out.append(acc)
+        else:
+            y = C.dw_fwd(x, wT, KH, KW, stride, padding)
         ctx.save_for_backward(x, wT)
         ctx.geom = (stride, padding, KH, KW)
         ctx.weight = weight
+        ctx.bnsrc = bnsrc
         return y
 
     @staticmethod
@@ -699,8 +716,20 @@ class _ConvDepthwise(torch.autograd.Function):
         stride, padding, KH, KW = ctx.geom
         dy = dy.contiguous()
         dx = None
+        src = ctx.bnsrc
+        ctx.bnsrc = None
         if ctx.needs_input_grad[0]:
-            dx = C.dw_dgrad(dy, wT, x.shape[1], x.shape[2], x.shape[3], KH, KW, stride, padding)
+            H, W, Cx = x.shape[1], x.shape[2], x.shape[3]
+            if src is not None and src.acc is not None:
+                src.acc.begin()
+                dx, ok = C.dw_dgrad_bn(dy, wT, H, W, Cx, KH, KW, stride, padding, src.y, src.mask,
+                                       src.aux, src.act, src.acc.buf, src.acc.R)
+                if int(ok):
+                    src.part, src.dx = src.acc.buf, dx   # the BN backward finds its sums filled
+                else:
+                    src.acc.state = "clean"
+            else:
+                dx = C.dw_dgrad(dy, wT, H, W, Cx, KH, KW, stride, padding)
         w = ctx.weight
         dw_ret = None
         if w.requires_grad:
@@ -716,7 +745,15 @@ class _ConvDepthwise(torch.autograd.Function):
                     G.accumulate(w, dw.view(w.shape[0], KH, KW, 1))
                 else:
                     dw_ret = dw.view(w.shape)
-        return dx, dw_ret, None, None
+        return dx, dw_ret, None, None, None, None, None
+
+
+# PCA_DW_BN_FUSE=1: depthwise k3 convs carry the BatchNorm sums of their neighbours in their
+# epilogues (dwconv.hip dwk_epi_*: 2 launches fewer per BN). Off by default: measured same-box,
+# the fused kernels (2-3 waves per SIMD against the plain kernels' 3) cost more than the
+# bandwidth-bound passes + finalize they replace — MobileNetV2 bs1024 13.64 -> 14.52 ms,
+# EfficientNet-B0 bs128 3.93 -> 3.99 ms.
+_DW_BN_FUSE = os.environ.get("PCA_DW_BN_FUSE", "0") == "1"
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False, acc=None):
@@ -739,10 +776,14 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
     Cin = x.shape[1]
     cout_g = Cout // groups
     if groups > 1 and groups == Cin and Cg == 1:
-        y = _ConvDepthwise.apply(to_nhwc(x), weight, stride, padding)
+        got = []
+        fuse = _DW_BN_FUSE and bias is None
+        bnsrc = getattr(x, "_pca_bnsrc", None) if (x.requires_grad and fuse) else None
+        y = _ConvDepthwise.apply(to_nhwc(x), weight, stride, padding,
+                                 acc if (want_stats and fuse) else None, bnsrc, got)
         if bias is not None:
             y = add_bias(y, bias)
-        return to_nchw(y), None
+        return to_nchw(y), (got[0] if got else None)
     if Cg % 8 == 0 and cout_g % 8 == 0:
         slot, owner = _slot_for_conv(x)
         bnsrc = getattr(x, "_pca_bnsrc", None) if x.requires_grad else None
@@ -926,6 +967,10 @@ class _BatchNormAct(torch.autograd.Function):
         # (grad mode is off inside Function.forward: the caller decided it in cfg.src)
         if cfg.src is not None and relu and has_mask and y2 is None:
             ctx.bnsrc = cfg.src = _BNSrc(y, mask, aux, cfg.bacc)
+        elif cfg.src is not None and ACT[cfg.act] == 2 and y2 is None and res is None and \
+                cfg.bacc is not None and aux is not None and aux.numel() >= 4 * y.shape[-1]:
+            # swish: only a depthwise consumer can fuse it (z recomputed from y, aux scale|shift)
+            ctx.bnsrc = cfg.src = _BNSrc(y, None, aux, cfg.bacc, act=2)
         else:
             cfg.src = None
         return out

@@ -434,6 +434,57 @@ def test_depthwise(C, Cin, mult, k, s, H):
     assert rel_err(dw.reshape(Co, 1, k, k), w.grad) < 2e-2
 
 
+@pytest.mark.parametrize("Cin,k,s,H,N", [(96, 3, 1, 16, 4), (144, 3, 2, 16, 3), (240, 3, 1, 8, 4),
+                                          (672, 3, 2, 8, 2), (1152, 3, 1, 4, 8), (40, 3, 2, 9, 2)])
+def test_depthwise_fused_bn_epilogues(C, Cin, k, s, H, N):
+    """Depthwise kernels with the BatchNorm sums fused (sharded accumulator rows): the forward's
+    statistics of its output, and the dgrad's backward reduce of the BN(+ReLU / swish) that
+    produced its input, against fp32 sums of the same kernel's outputs; plain outputs unchanged."""
+    from pytorch_cifar_amd.ops.functional import acc_shards
+
+    torch.manual_seed(8)
+    p = (k - 1) // 2
+    x = bf(torch.randn(N, Cin, H, H, device="cuda"))
+    w = torch.randn(Cin, 1, k, k, device="cuda") * 0.3
+    wT = w.reshape(Cin, k * k).t().contiguous()
+    xn = nhwc(x).bfloat16()
+    R = acc_shards(Cin)
+    acc = torch.zeros(R * 2 * Cin, device="cuda")
+    y, ok = C.dw_fwd_stats(xn, wT, k, k, s, p, acc, R)
+    assert int(ok) == 1
+    # (same arithmetic as the plain kernel; register allocation may contract it differently)
+    assert rel_err(y, C.dw_fwd(xn, wT, k, k, s, p)) < 1e-2
+    sums = acc.view(R, 2, Cin).sum(0)
+    # (the epilogue sums the fp32 results before rounding: compare with the fp32 conv)
+    yf = nhwc(F.conv2d(x.float(), w, stride=s, padding=p, groups=Cin)).reshape(-1, Cin)
+    assert rel_err(sums[0], yf.sum(0)) < 1e-4 and rel_err(sums[1], (yf * yf).sum(0)) < 1e-4
+
+    dy = torch.randn_like(y.float()).bfloat16()
+    dx_ref = C.dw_dgrad(dy, wT, H, H, Cin, k, k, s, p)
+    ybn = torch.randn(N, H, H, Cin, device="cuda").bfloat16()
+    mean, istd = torch.randn(Cin, device="cuda") * 0.1, torch.rand(Cin, device="cuda") + 0.5
+    scale, shift = torch.randn(Cin, device="cuda"), torch.randn(Cin, device="cuda") * 0.2
+    aux = torch.cat([mean, istd, scale, shift])
+    mask_b = torch.rand(N, H, H, Cin, device="cuda") > 0.4
+    bits = (mask_b.reshape(-1, 8).to(torch.int32) << torch.arange(8, device="cuda")).sum(1).to(torch.uint8)
+    xhat = (ybn.float() - mean) * istd
+    for act in (1, 2):
+        acc.zero_()
+        dx, ok = C.dw_dgrad_bn(dy, wT, H, H, Cin, k, k, s, p, ybn, bits if act == 1 else None, aux,
+                               act, acc, R)
+        assert int(ok) == 1
+        assert rel_err(dx, dx_ref) < 1e-2
+        if act == 1:
+            dz = torch.where(mask_b, dx.float(), torch.zeros_like(xhat))
+        else:
+            z = ybn.float() * scale + shift
+            sg = torch.sigmoid(z)
+            dz = dx.float() * (sg + z * sg * (1 - sg))
+        sums = acc.view(R, 2, Cin).sum(0)
+        assert rel_err(sums[0], dz.sum((0, 1, 2))) < 1e-3, act
+        assert rel_err(sums[1], (dz * xhat).sum((0, 1, 2))) < 1e-3, act
+
+
 @pytest.mark.parametrize("Cc,H", [(48, 4), (1152, 2), (96, 32), (20, 4)])
 def test_se_scale(C, Cc, H):
     """Squeeze-excite scale fwd/bwd and the global average pool (fwd/bwd) it uses: vectorized

@@ -2,7 +2,7 @@
 """Per-kernel timeline of ONE training step from a rocprofv3 kernel trace.
 
 Reads ``*_kernel_trace.csv`` (``rocprofv3 --kernel-trace --output-format csv``), cuts the last
-complete step at the per-step optimizer launch (``--marker``, default ``sgd_kernel``) and prints,
+complete step at the per-step optimizer launch (``--marker``, default ``sgd_``: the fused or plain SGD kernel) and prints,
 in dispatch order, each kernel's start offset, duration and the idle gap before it, plus totals:
 busy time (union of kernel intervals), summed kernel time, and idle time. With hipGraph replay or
 a side stream, overlapping kernels show as negative gaps.
@@ -56,7 +56,7 @@ def short(name, n=90):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
-    ap.add_argument("--marker", default="sgd_kernel")
+    ap.add_argument("--marker", default="sgd_")
     ap.add_argument("--step", type=int, default=-2, help="which step window (python index over windows)")
     ap.add_argument("--md", action="store_true")
     ap.add_argument("--categories", action="store_true", help="print only per-phase totals")
