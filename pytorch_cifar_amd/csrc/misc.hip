@@ -1059,6 +1059,191 @@ __global__ __launch_bounds__(256) void se_mlp_bwd_param_kernel(
   else if (do_b1 && t >= kSeWC && t - kSeWC < R) atomicAdd(db1 + t - kSeWC, bacc);
 }
 
+// ---- squeeze-excite in few launches (efficientnet.py:26-36, senet.py:59-66): one block per NB
+// samples does everything that reduces over a sample — forward: pool + both MLP layers
+// (se_fwd_fused_kernel; + se_scale_fwd = 2 launches); backward: the excitation reduce ds and
+// the MLP data path dz, dp (se_bwd_data_kernel; + the parameter kernel + se_dx = 3 launches).
+// The MLP weights stream through each block once per NB samples; NB grows with the batch so
+// large batches do not multiply the weight traffic (NB = 1 at the 8-GPU shard's 128 samples).
+// LDS: vec [NB][C] (pooled / ds) | h [NB][R] | red [256 * 8]
+constexpr int kSeFusedMaxC = 2048, kSeFusedMaxR = 192;
+
+template <int NB>
+__device__ __forceinline__ void se_pool8(const bf16* __restrict__ x, const bf16* __restrict__ dout,
+                                         const float* __restrict__ s, int HW, int C, int n,
+                                         float* red, float* outv) {
+  // outv[c] = mean_hw x (dout == nullptr) or sum_hw dout*x * sig'(s) (excitation gradient)
+  const int G = C >> 3, RW = 256 / G;
+  const int t = threadIdx.x, gi = t % G, r = t / G;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (r < RW) {
+    const size_t base = (size_t)n * HW * C + gi * 8;
+    for (int hw = r; hw < HW; hw += RW) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + base + (size_t)hw * C), f);
+      if (dout) {
+        float d[8];
+        unpack8(*reinterpret_cast<const uint4*>(dout + base + (size_t)hw * C), d);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) a[v] += d[v] * f[v];
+      } else {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) a[v] += f[v];
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < 8; ++v) red[t * 8 + v] = a[v];
+  __syncthreads();
+  if (t < G) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      float acc = 0.f;
+      for (int j = 0; j < RW; ++j) acc += red[(j * G + t) * 8 + v];
+      if (dout) {
+        const float sg = sigmoidf_(s[(size_t)n * C + t * 8 + v]);
+        outv[t * 8 + v] = acc * sg * (1.f - sg);
+      } else {
+        outv[t * 8 + v] = acc / HW;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void se_fwd_fused_kernel(
+    const bf16* __restrict__ x, int N, int HW, int C, int R, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    int act, float* __restrict__ pooled, float* __restrict__ hpre, float* __restrict__ s) {
+  extern __shared__ float sm[];
+  float* vec = sm;                       // [NB][C]
+  float* h = vec + NB * C;               // [NB][R]
+  float* red = h + NB * R;               // [256 * 8]
+  const int n0 = blockIdx.x * NB;
+  const int nb = min(NB, N - n0);
+  for (int k = 0; k < nb; ++k) se_pool8<NB>(x, nullptr, nullptr, HW, C, n0 + k, red, vec + k * C);
+  for (int i = threadIdx.x; i < nb * C; i += 256) pooled[(size_t)n0 * C + i] = vec[i];
+  // layer 1: each wave owns 8 output rows at a time, lanes across C (coalesced W1 rows): the 8
+  // row loads per channel are independent (a wave per single row serialised 12+ load-latency
+  // rounds per block at R = 48)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int r0 = wv * 8; r0 < R; r0 += 32) {
+    float a[NB][8];
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[k][j] = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      float pv[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) pv[k] = vec[k * C + c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float w = r0 + j < R ? w1[(size_t)(r0 + j) * C + c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) a[k][j] += w * pv[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = r0 + j;
+        const float v = wave_sum(a[k][j]) + ((b1 && r < R) ? b1[r] : 0.f);
+        if (lane == 0 && k < nb && r < R) {
+          hpre[(size_t)(n0 + k) * R + r] = v;
+          h[k * R + r] = se_act(v, act);
+        }
+      }
+  }
+  __syncthreads();
+  // layer 2: a thread per channel, its W2 row (R contiguous floats) against the block's h rows
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) a[k] = b2 ? b2[c] : 0.f;
+    const float* wr = w2 + (size_t)c * R;
+    for (int r = 0; r < R; ++r) {
+      const float w = wr[r];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) a[k] += w * h[k * R + r];
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (k < nb) s[(size_t)(n0 + k) * C + c] = a[k];
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void se_bwd_data_kernel(
+    const bf16* __restrict__ dout, const bf16* __restrict__ x, const float* __restrict__ s,
+    int N, int HW, int C, int R, const float* __restrict__ w1, const float* __restrict__ w2,
+    const float* __restrict__ hpre, int act, float* __restrict__ ds, float* __restrict__ dz,
+    float* __restrict__ dp) {
+  extern __shared__ float sm[];
+  float* vec = sm;                       // [NB][C] ds
+  float* h = vec + NB * C;               // [NB][R] dz
+  float* red = h + NB * R;               // [256 * 8]
+  const int n0 = blockIdx.x * NB;
+  const int nb = min(NB, N - n0);
+  for (int k = 0; k < nb; ++k) se_pool8<NB>(x, dout, s, HW, C, n0 + k, red, vec + k * C);
+  for (int i = threadIdx.x; i < nb * C; i += 256) ds[(size_t)n0 * C + i] = vec[i];
+  // dh[r] = sum_c ds[c] W2[c][r]: threads over c read their W2 rows 8 outputs at a time; the 256
+  // partials per output are folded by wave sums + LDS
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int r0 = 0; r0 < R; r0 += 8) {
+    float p[NB][8];
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p[k][j] = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float* wr = w2 + (size_t)c * R + r0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float w = r0 + j < R ? wr[j] : 0.f;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) p[k][j] += w * vec[k * C + c];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = wave_sum(p[k][j]);
+        if (lane == 0) red[(wv * NB + k) * 8 + j] = v;
+      }
+    __syncthreads();
+    if (threadIdx.x < NB * 8) {
+      const int k = threadIdx.x / 8, j = threadIdx.x % 8, r = r0 + j;
+      if (k < nb && r < R) {
+        const float v = red[(0 * NB + k) * 8 + j] + red[(1 * NB + k) * 8 + j] +
+                        red[(2 * NB + k) * 8 + j] + red[(3 * NB + k) * 8 + j];
+        const size_t o = (size_t)(n0 + k) * R + r;
+        const float d = v * se_act_grad(hpre[o], act);
+        dz[o] = d;
+        h[k * R + r] = d;
+      }
+    }
+    __syncthreads();
+  }
+  // dp[c] = sum_r W1[r][c] dz[r] (threads over c: coalesced W1 rows)
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) a[k] = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const float w = w1[(size_t)r * C + c];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) a[k] += w * h[k * R + r];
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (k < nb) dp[(size_t)(n0 + k) * C + c] = a[k];
+  }
+}
+
 // dx = dout * sig(s) + dp / HW   (excitation path + broadcast squeeze-path gradient)
 __global__ __launch_bounds__(256) void se_dx8_kernel(const bf16* __restrict__ dout,
                                                      const float* __restrict__ s,
@@ -1689,6 +1874,10 @@ bool se_mlp_supported(int C, int R) {
 }
 static dim3 se_row_grid(int N, int R) { return dim3(cdiv(N, kSeNB) * cdiv(R, kSeRC)); }
 static dim3 se_col_grid(int N, int C) { return dim3(cdiv(C, 256), cdiv(N, kSeNB)); }
+// the parameter part of se_mlp_bwd_launch alone (dz from se_bwd_data_kernel)
+void se_mlp_bwd_param_launch(const float* ds, const float* dz, const float* hpre,
+                             const float* pooled, int N, int C, int R, int act, float* dw1,
+                             float* db1, float* dw2, float* db2, hipStream_t st);
 void se_mlp_fwd_launch(const float* pooled, int N, int C, int R, const float* w1, const float* b1,
                        const float* w2, const float* b2, int act, float* hpre, float* s,
                        hipStream_t st) {
@@ -1704,6 +1893,11 @@ void se_mlp_bwd_launch(const float* ds, const float* hpre, const float* pooled, 
                      R, w2, nullptr, hpre, act, dz);
   hipLaunchKernelGGL((se_coldot_kernel<false, false>), se_col_grid(N, C), dim3(256), 0, st, dz, N,
                      C, R, w1, nullptr, act, dp);
+  se_mlp_bwd_param_launch(ds, dz, hpre, pooled, N, C, R, act, dw1, db1, dw2, db2, st);
+}
+void se_mlp_bwd_param_launch(const float* ds, const float* dz, const float* hpre,
+                             const float* pooled, int N, int C, int R, int act, float* dw1,
+                             float* db1, float* dw2, float* db2, hipStream_t st) {
   // ~2 blocks per CU: split the samples into chunks over the channel tiles
   const int ct = cdiv(C, kSeWC);
   const int nchunks = std::max(1, std::min(cdiv(N, kSeWN), 512 / ct));
@@ -1721,6 +1915,41 @@ void se_mlp_bwd_launch(const float* ds, const float* hpre, const float* pooled, 
   else PCA_SE_PARAM(64);
 #undef PCA_SE_PARAM
 }
+static int se_fused_nb(int N) { return N >= 1024 ? 4 : N >= 512 ? 2 : 1; }
+static size_t se_fused_lds(int NB, int C, int R) {
+  return ((size_t)NB * C + (size_t)NB * R + 256 * 8) * sizeof(float);
+}
+bool se_fused_supported(int C, int R) {
+  return C % 8 == 0 && C <= kSeFusedMaxC && R >= 1 && R <= kSeFusedMaxR &&
+         se_fused_lds(4, C, R) <= 64 * 1024;
+}
+void se_fwd_fused_launch(const bf16* x, int N, int HW, int C, int R, const float* w1,
+                         const float* b1, const float* w2, const float* b2, int act, float* pooled,
+                         float* hpre, float* s, hipStream_t st) {
+  const int NB = se_fused_nb(N);
+  const dim3 grid(cdiv(N, NB)), block(256);
+  const size_t lds = se_fused_lds(NB, C, R);
+  if (NB == 4)
+    hipLaunchKernelGGL(se_fwd_fused_kernel<4>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2, b2, act, pooled, hpre, s);
+  else if (NB == 2)
+    hipLaunchKernelGGL(se_fwd_fused_kernel<2>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2, b2, act, pooled, hpre, s);
+  else
+    hipLaunchKernelGGL(se_fwd_fused_kernel<1>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2, b2, act, pooled, hpre, s);
+}
+void se_bwd_data_launch(const bf16* dout, const bf16* x, const float* s, int N, int HW, int C,
+                        int R, const float* w1, const float* w2, const float* hpre, int act,
+                        float* ds, float* dz, float* dp, hipStream_t st) {
+  const int NB = se_fused_nb(N);
+  const dim3 grid(cdiv(N, NB)), block(256);
+  const size_t lds = se_fused_lds(NB, C, R);
+  if (NB == 4)
+    hipLaunchKernelGGL(se_bwd_data_kernel<4>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2, hpre, act, ds, dz, dp);
+  else if (NB == 2)
+    hipLaunchKernelGGL(se_bwd_data_kernel<2>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2, hpre, act, ds, dz, dp);
+  else
+    hipLaunchKernelGGL(se_bwd_data_kernel<1>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2, hpre, act, ds, dz, dp);
+}
+
 void se_ds_launch(const bf16* dout, const bf16* x, const float* s, int N, int HW, int C, float* ds,
                   hipStream_t st) {
   hipLaunchKernelGGL(se_scale_bwd8_kernel<false>, dim3(N), dim3(256), 0, st, dout, x, s, HW, C,

@@ -724,6 +724,8 @@ def test_dropout_and_drop_connect(C, unit, dt):
     (33, 8, 512, 32, 1, True),       # SENet18 (ReLU)
     (70, 4, 440, 26, 1, False),      # RegNet-like, no bias, ragged tiles (C % 64, R odd)
     (1024, 4, 1152, 48, 2, True),    # bs1024: several sample chunks per channel tile
+    (600, 2, 240, 10, 2, True),      # fused kernels: 2 samples per block
+    (1030, 2, 96, 4, 1, False),      # fused kernels: 4 samples per block, ragged last block
 ])
 def test_squeeze_excite_matches_fp32(N, H, C, R, act, bias):
     """Native squeeze-excite block (pool + fp32 MLP + sigmoid scale, and its backward with the
