@@ -256,9 +256,23 @@ static float time_launches(F&& f, hipStream_t st, int reps) {
 // the conv once with the trial selection active, allocating its own scratch outputs.
 template <class F>
 static void autotune_conv(int kind, int N, int H, int W, int Cin, int Cout, int KH, int KW,
-                          int stride, int pad, int groups, int Ho, int Wo, F&& run) {
+                          int stride, int pad, int groups, int Ho, int Wo, F&& run,
+                          bool need_bn_fuse = false) {
   auto cands = pca::conv_tune_candidates(kind, N, H, W, Cin, Cout, KH, KW, stride, pad, groups,
                                          Ho, Wo);
+  if (need_bn_fuse) {
+    // a dgrad that should carry the producer BN's backward reduce: candidates that cannot fuse
+    // it (the phased kernel) would leave a separate reduce + finalize + apply behind, which their
+    // trial does not time — keep them only when no candidate can fuse
+    std::vector<std::pair<int, int>> fusable;
+    for (const auto& c : cands) {
+      pca::conv_set_trial(c.first, c.second);
+      if (pca::conv_dgrad_bn_rows(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo) > 0)
+        fusable.push_back(c);
+    }
+    pca::conv_set_trial(-1, -1);
+    if (!fusable.empty()) cands.swap(fusable);
+  }
   if (cands.empty()) return;
   const hipStream_t st = cur_stream();
   float best = 1e30f;
@@ -404,7 +418,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
                              r > 0 ? ptr<bf16>(*bn_y) : nullptr,
                              r > 0 ? bn_mask->data_ptr<uint8_t>() : nullptr,
                              r > 0 ? ptr<float>(*bn_aux) : nullptr, r > 0 ? ptr<float>(pt) : nullptr);
-    });
+    }, want_bn);
   }
   auto dx = at::empty({N, H, W, Cin}, dy.options());
   const int64_t wsn = pca::conv_dgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups,
