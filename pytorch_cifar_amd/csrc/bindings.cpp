@@ -154,6 +154,8 @@ struct CatArgs {
 };
 void cat_nhwc_launch(const CatArgs&, bf16*, int, bool, hipStream_t);
 void interleave2_launch(bf16*, bf16*, bf16*, int, int, bool, hipStream_t);
+void chan_remap_launch(const void*, void*, bool, bool, const int*, const int*, int, int, int, int,
+                       hipStream_t);
 void dpn_merge_fwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, hipStream_t);
 void dpn_merge_bwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, bf16*, hipStream_t);
 void se_scale_bwd_launch(const bf16*, const bf16*, const float*, int, int, int, bf16*, float*,
@@ -1340,6 +1342,40 @@ std::vector<Tensor> split_nhwc(const Tensor& whole, const std::vector<int64_t>& 
   return outs;
 }
 
+// channel remap (group pad / unpad / shuffle and their adjoints): x viewed as [rows, Cin]
+// (Cin = last dim), out [Q, J] with Q = rmap.numel() * K (outer row map) or rows; `acc` (fp32)
+// is added into instead of allocating the output.
+Tensor chan_remap(const Tensor& x, const Tensor& cmap, const optional<Tensor>& rmap, int64_t K,
+                  const optional<Tensor>& acc) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "chan_remap: contiguous GPU input");
+  const bool fp32 = x.scalar_type() == at::kFloat;
+  TORCH_CHECK(fp32 || x.scalar_type() == at::kBFloat16, "chan_remap: bf16 or fp32");
+  TORCH_CHECK(cmap.scalar_type() == at::kInt && cmap.is_cuda() && cmap.dim() == 1, "chan_remap: int32 cmap");
+  const int64_t Cin = x.size(-1);
+  const int64_t rows = Cin ? x.numel() / Cin : 0;
+  const int* rm = optr<int>(rmap);
+  int64_t Q = rows;
+  if (rm) {
+    TORCH_CHECK(rmap->scalar_type() == at::kInt && rmap->is_cuda(), "chan_remap: int32 rmap");
+    TORCH_CHECK(K >= 1 && rows % K == 0, "chan_remap: rows must be a multiple of K");
+    Q = rmap->numel() * K;
+  }
+  const int64_t J = cmap.numel();
+  TORCH_CHECK(Q < (int64_t)1 << 31 && J > 0, "chan_remap: size");
+  Tensor out;
+  if (acc.has_value() && acc->defined()) {
+    TORCH_CHECK(fp32 && acc->scalar_type() == at::kFloat && acc->is_contiguous() && acc->numel() == Q * J,
+                "chan_remap: fp32 accumulator of Q*J elements");
+    out = *acc;
+  } else {
+    out = at::empty({Q, J}, x.options());
+  }
+  if (Q > 0)
+    pca::chan_remap_launch(x.data_ptr(), out.data_ptr(), fp32, acc.has_value() && acc->defined(),
+                           ptr<int>(cmap), rm, (int)Q, (int)(rm ? K : 1), (int)Cin, (int)J, cur_stream());
+  return out;
+}
+
 // shuffle(cat[a, b], 2) for equal widths: a, b [N,H,W,C] -> [N,H,W,2C] interleaved; and back
 Tensor interleave2(const Tensor& a, const Tensor& b) {
   check_bf16(a, "a");
@@ -1681,6 +1717,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dpn_merge_fwd", &dpn_merge_fwd);
   m.def("cat_nhwc", &cat_nhwc);
   m.def("interleave2", &interleave2);
+  m.def("chan_remap", &chan_remap, py::arg("x"), py::arg("cmap"), py::arg("rmap") = py::none(),
+        py::arg("K") = 1, py::arg("acc") = py::none());
   m.def("deinterleave2", &deinterleave2);
   m.def("split_nhwc", &split_nhwc);
   m.def("dpn_merge_bwd", &dpn_merge_bwd);

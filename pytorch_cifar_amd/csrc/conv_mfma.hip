@@ -53,6 +53,7 @@ struct ConvGeom {
   int ksplit;           // split-K factor (1 = off): grid.z = ksplit * groups * classes
   float* ws;            // split-K fp32 partials [ksplit][N*Ho*Wo][Co]
   int mode;             // 0 fwd, 1 dgrad, 2 parity dgrad (autotune cache key)
+  int ilv;              // register-pipelined K loop in the >= 3-stage configs (PCA_IGEMM_ILV)
   // dgrad only: fused backward reduce of the BatchNorm(+ReLU) that produced this conv's input
   // (bn_part != nullptr): per-channel sums of dz = dX * relu'(mask) and dz * xhat into slab rows
   const bf16* bn_y;     // that BN's input y
@@ -352,6 +353,78 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s) issue(kt_begin + s, s);
 
+    if (STAGES >= 3 && g.ilv) {
+      // Register-pipelined K loop (>= 3 LDS stages): the fragments of half-step kk = 1 are read
+      // while the kk = 0 MFMAs run, and those of the NEXT K-step's kk = 0 while the kk = 1 MFMAs
+      // run, one ds_read per MFMA (sched_group_barrier) — the LDS read latency leaves the
+      // critical path instead of sitting between the barrier and the first MFMA of every step.
+      // The barrier moves to mid-step: it publishes the next stage (landed by the counted vmcnt
+      // wait) and, with each wave's own reads of the current stage drained (lgkmcnt(0)), frees
+      // the current stage for the DMA issued at the top of the following step.
+      constexpr int NF = TM + TN;
+      bf16x8 af[2][TM], bfv[2][TN];
+      auto frag = [&](int slot, int kk, int j) {
+        const char* As = smem + slot * STAGE;
+        const char* Bs = As + A_BYTES;
+        const int gsel = kk * 4 + (lane >> 4);
+        if (j < TN) {
+          const int r = wn * WTN + j * 16 + (lane & 15);
+          bfv[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + r * RB + ((gsel ^ (r & 7)) << 4));
+        } else {
+          const int r = wm * WTM + (j - TN) * 16 + (lane & 15);
+          af[kk][j - TN] = *reinterpret_cast<const bf16x8*>(As + r * RB + ((gsel ^ (r & 7)) << 4));
+        }
+      };
+      // one MFMA, one ds_read, ... then the remaining MFMAs (or reads)
+      auto ilv_pattern = [&]() {
+        constexpr int PAIRS = NF < TM * TN ? NF : TM * TN;
+#pragma unroll
+        for (int i = 0; i < PAIRS; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
+        }
+        if constexpr (TM * TN > PAIRS) __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - PAIRS, 0);
+        if constexpr (NF > PAIRS) __builtin_amdgcn_sched_group_barrier(0x100, NF - PAIRS, 0);
+      };
+      wait_vmcnt<(STAGES - 2) * LPS>();
+      raw_barrier();
+#pragma unroll
+      for (int j = 0; j < NF; ++j) frag(0, 0, j);
+      for (int kt = kt_begin; kt < KT; ++kt) {
+        const int rel = kt - kt_begin;
+        const int slot = rel % STAGES;
+        __builtin_amdgcn_sched_barrier(0);
+        issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < NF; ++j) frag(slot, 1, j);
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][mi], bfv[0][ni], acc[mi][ni], 0, 0, 0);
+        ilv_pattern();
+        __builtin_amdgcn_sched_barrier(0);
+        wait_vmcnt<(STAGES - 2) * LPS>();   // stage kt+1 landed (this wave's pieces)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
+        const bool more = kt + 1 < KT;
+        if (more) {
+          const int nslot = (rel + 1) % STAGES;
+#pragma unroll
+          for (int j = 0; j < NF; ++j) frag(nslot, 0, j);
+        }
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][mi], bfv[1][ni], acc[mi][ni], 0, 0, 0);
+        if (more) {
+          ilv_pattern();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else
     for (int kt = kt_begin; kt < KT; ++kt) {
       const int rel = kt - kt_begin;
       wait_vmcnt<(STAGES - 2) * LPS>();
@@ -1330,6 +1403,11 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   g.ksplit = 1;
   g.ws = nullptr;
   g.mode = 0;
+  static const int ilv = [] {
+    const char* e = getenv("PCA_IGEMM_ILV");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  g.ilv = ilv;
   g.bn_y = nullptr;
   g.bn_mask = nullptr;
   g.bn_aux = nullptr;

@@ -1975,4 +1975,87 @@ void weight_prep_launch(const float* w, int G, int Cn, int T, int Cr, bf16* wb, 
                      G, Cn, T, Cr, wb, wt);
 }
 
+// ---- channel remap (K22): out[q][j] = in[src(q)][cmap[j]], 0 where a map entry is -1.
+// src(q) = q, or rmap[q / K] * K + q % K with an outer row map (conv weights [Cout][KH*KW][Cg]:
+// K = KH*KW). One kernel covers the per-group zero padding of odd-width grouped convs (input,
+// weight, bias) and its inverse slice (output, BN statistics), ShuffleNet's channel shuffle
+// (shufflenet.py:10-19), and every backward of those — the adjoint of an injective remap is the
+// remap with the inverse maps. ACC adds into `out` (fp32 parameter gradients in the arena).
+// The channel map is staged in LDS once per block; each thread writes V consecutive output
+// channels with one vector store (the gathered reads hit the same input row, L1/L2-resident).
+template <typename T, int V, bool ACC>
+__global__ __launch_bounds__(256) void chan_remap_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                         const int* __restrict__ cmap,
+                                                         const int* __restrict__ rmap, int Q, int K,
+                                                         int Cin, int J, int map_in_lds) {
+  extern __shared__ int smap[];
+  const int* mp = cmap;
+  if (map_in_lds) {
+    for (int j = threadIdx.x; j < J; j += blockDim.x) smap[j] = cmap[j];
+    __syncthreads();
+    mp = smap;
+  }
+  struct alignas(sizeof(T) * V) Vec { T v[V]; };
+  const int G = J / V;
+  const int64_t total = (int64_t)Q * G;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(i / G), gi = (int)(i - (int64_t)q * G);
+    int64_t srow = q;
+    if (rmap) {
+      const int r = q / K;
+      const int s = rmap[r];
+      srow = s < 0 ? -1 : (int64_t)s * K + (q - r * K);
+    }
+    const T* row = in + srow * Cin;
+    Vec o;
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int c = mp[gi * V + u];
+      o.v[u] = (srow >= 0 && c >= 0) ? row[c] : T(0.f);
+    }
+    Vec* dst = reinterpret_cast<Vec*>(out + (int64_t)q * J + gi * V);
+    if constexpr (ACC) {
+      Vec a = *dst;
+#pragma unroll
+      for (int u = 0; u < V; ++u) a.v[u] = a.v[u] + o.v[u];
+      *dst = a;
+    } else {
+      *dst = o;
+    }
+  }
+}
+
+template <typename T, bool ACC>
+static void chan_remap_dispatch(const T* in, T* out, const int* cmap, const int* rmap, int Q, int K,
+                                int Cin, int J, hipStream_t st) {
+  constexpr int VMAX = 16 / sizeof(T);
+  int V = VMAX;
+  while (V > 1 && (J % V)) V >>= 1;
+  const int lds_ok = J <= 16384 ? 1 : 0;
+  const size_t lds = lds_ok ? (size_t)J * sizeof(int) : 0;
+  const dim3 grid(grid_cap((size_t)Q * (J / V))), block(256);
+#define PCA_REMAP(VV)                                                                           \
+  if (V == VV) {                                                                                \
+    hipLaunchKernelGGL((chan_remap_kernel<T, VV, ACC>), grid, block, lds, st, in, out, cmap, rmap, \
+                       Q, K, Cin, J, lds_ok);                                                   \
+    return;                                                                                     \
+  }
+  if constexpr (VMAX >= 8) { PCA_REMAP(8) }
+  PCA_REMAP(4) PCA_REMAP(2) PCA_REMAP(1)
+#undef PCA_REMAP
+}
+
+void chan_remap_launch(const void* in, void* out, bool fp32, bool accumulate, const int* cmap,
+                       const int* rmap, int Q, int K, int Cin, int J, hipStream_t st) {
+  if (fp32) {
+    if (accumulate)
+      chan_remap_dispatch<float, true>((const float*)in, (float*)out, cmap, rmap, Q, K, Cin, J, st);
+    else
+      chan_remap_dispatch<float, false>((const float*)in, (float*)out, cmap, rmap, Q, K, Cin, J, st);
+  } else {
+    chan_remap_dispatch<bf16, false>((const bf16*)in, (bf16*)out, cmap, rmap, Q, K, Cin, J, st);
+  }
+}
+
 }  // namespace pca

@@ -818,29 +818,59 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
 _GROUP_PAD = os.environ.get("PCA_GROUP_PAD", "1") != "0"
 
 
+def _group_pad_remap(groups, n, npad):
+    """[groups * npad] <- [groups * n]: each group's n channels followed by npad - n zeros."""
+    def build():
+        return Remap([(j // npad) * n + j % npad if j % npad < n else -1
+                      for j in range(groups * npad)], groups * n)
+    return Remap.get(("gpad", groups, n, npad), build)
+
+
+def _group_unpad_remap(groups, n, npad):
+    """[groups * n] <- [groups * npad] (the slice back to the logical channels)."""
+    def build():
+        return Remap([(j // n) * npad + j % n for j in range(groups * n)], groups * npad)
+    return Remap.get(("gunpad", groups, n, npad), build)
+
+
+def _weight_pad_remap(groups, cout_g, op, Cg, cp, K):
+    """Conv weight [G*cout_g][K][Cg] -> [G*op][K][cp]: zero output rows and input channels."""
+    def build():
+        cmap = [c if c < Cg else -1 for c in range(cp)]
+        rmap = [(r // op) * cout_g + r % op if r % op < cout_g else -1 for r in range(groups * op)]
+        return Remap(cmap, Cg, rmap, groups * cout_g, K)
+    return Remap.get(("wpad", groups, cout_g, op, Cg, cp, K), build)
+
+
 def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
+    """Odd-width grouped conv on the MFMA kernels: the per-group zero padding of the input,
+    weight and bias and the slice of the output / BN statistics are native channel remaps
+    (one launch each way, gradients of the weight and bias added into the arena)."""
     Cout, Cg, KH, KW = weight.shape
     cout_g = Cout // groups
     cp, op = _round8(Cg), _round8(cout_g)
     xn = to_nhwc(x)
     N, H, W, _ = xn.shape
     if cp != Cg:
-        xn = F.pad(xn.view(N, H, W, groups, Cg), (0, cp - Cg)).reshape(N, H, W, groups * cp)
+        xn = _RemapFn.apply(xn, _group_pad_remap(groups, Cg, cp), (N, H, W, groups * cp), None)
     # weight [Cout, Cg, KH, KW] -> [G*op, cp, KH, KW], channels_last (the MFMA B layout)
-    wp = weight.view(groups, cout_g, Cg, KH, KW)
-    wp = F.pad(wp, (0, 0, 0, 0, 0, cp - Cg, 0, op - cout_g)).reshape(groups * op, cp, KH, KW)
-    wp = wp.contiguous(memory_format=torch.channels_last)
+    if cp != Cg or op != cout_g:
+        wr = _weight_pad_remap(groups, cout_g, op, Cg, cp, KH * KW)
+        wp = to_nchw(_remap_param(weight, wr, (groups * op, KH, KW, cp)))
+    else:
+        wp = weight
     bp = None
     if bias is not None:
-        bp = F.pad(bias.view(groups, cout_g), (0, op - cout_g)).reshape(groups * op)
+        bp = bias if op == cout_g else _remap_param(bias, _group_pad_remap(groups, cout_g, op),
+                                                    (groups * op,))
     y, stats = _ConvMFMA.apply(xn, wp, bp, stride, padding, groups, want_stats, 0)
     if op != cout_g:
         Ho, Wo = y.shape[1], y.shape[2]
-        # (.contiguous: with groups == 1 the reshape of the slice is a strided view, not a copy)
-        y = y.view(N, Ho, Wo, groups, op)[..., :cout_g].reshape(N, Ho, Wo, Cout).contiguous()
+        unpad = _group_unpad_remap(groups, cout_g, op)
+        y = _RemapFn.apply(y, unpad, (N, Ho, Wo, Cout), None)
         if want_stats and stats is not None and stats.numel():
             R = stats.shape[0]
-            stats = stats.view(R, 2, groups, op)[..., :cout_g].reshape(R, 2, Cout).contiguous()
+            stats = unpad.apply(stats.contiguous()).view(R, 2, Cout)
     return to_nchw(y), (stats if want_stats and stats is not None and stats.numel() else None)
 
 
@@ -1567,13 +1597,109 @@ def drop_connect(x, drop_ratio, owner=None):
     return _dropout_units(x, x[0].numel(), drop_ratio, owner if owner is not None else drop_connect)
 
 
+class Remap:
+    """An injective channel remap ``out[q][j] = in[src(q)][cmap[j]]`` (-1 = zero) and its adjoint.
+
+    ``cmap`` has J entries indexing the Cin input channels; ``rmap`` (optional) maps output rows
+    to input rows of K-row blocks (conv weights [Cout][KH*KW][Cg], K = KH*KW). The adjoint of an
+    injective remap is the remap with the inverse maps, so forward and backward are both one
+    launch of ``chan_remap`` (csrc/misc.hip). Device maps are built once per (key, device) — before
+    hipGraph capture, on the warm-up steps — and reused by every replay."""
+
+    _cache = {}
+
+    def __init__(self, cmap, cin, rmap=None, rin=None, K=1):
+        self.cmap, self.cin, self.rmap, self.rin, self.K = list(cmap), cin, rmap, rin, K
+        inv = [-1] * cin
+        for j, c in enumerate(self.cmap):
+            if c >= 0:
+                inv[c] = j
+        self.icmap = inv
+        self.irmap = None
+        if rmap is not None:
+            inv_r = [-1] * rin
+            for r, s in enumerate(rmap):
+                if s >= 0:
+                    inv_r[s] = r
+            self.irmap = inv_r
+        self._dev = {}
+
+    @classmethod
+    def get(cls, key, build):
+        m = cls._cache.get(key)
+        if m is None:
+            m = build()
+            cls._cache[key] = m
+        return m
+
+    def maps(self, device):
+        d = self._dev.get(device)
+        if d is None:
+            def t(v):
+                return None if v is None else torch.tensor(v, dtype=torch.int32, device=device)
+            d = (t(self.cmap), t(self.rmap), t(self.icmap), t(self.irmap))
+            self._dev[device] = d
+        return d
+
+    def apply(self, x, inverse=False, acc=None):
+        """Remap the contiguous ``x`` (last dim = channels) -> flat [Q, J] (or add into ``acc``)."""
+        cm, rm, icm, irm = self.maps(x.device)
+        if inverse:
+            cm, rm = icm, irm
+        return _C().chan_remap(x, cm, rm, self.K, acc)
+
+
+class _RemapFn(torch.autograd.Function):
+    """Differentiable channel remap of a physical-order tensor; ``leaf`` (a parameter whose
+    physical view is ``x``) gets its gradient added straight into its arena buffer."""
+
+    @staticmethod
+    def forward(ctx, x, remap, out_shape, leaf):
+        ctx.remap, ctx.in_shape, ctx.leaf = remap, x.shape, leaf
+        return remap.apply(x).view(out_shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        leaf = ctx.leaf
+        if leaf is not None:
+            buf = G.grad_buffer(leaf)
+            if buf is not None and tuple(buf.shape) == tuple(ctx.in_shape):
+                ctx.remap.apply(dy, inverse=True, acc=buf)
+                G.fire(leaf)
+                return None, None, None, None
+        return ctx.remap.apply(dy, inverse=True).view(ctx.in_shape), None, None, None
+
+
+def _remap_param(p, remap, phys_shape):
+    """Remapped copy of parameter ``p`` in physical order; its gradient flows back natively."""
+    phys = G.physical(p)
+    leaf = p if (p.is_leaf and p.requires_grad and phys.is_contiguous()) else None
+    if not phys.is_contiguous():
+        phys = phys.contiguous()
+    return _RemapFn.apply(phys, remap, phys_shape, leaf)
+
+
+def _shuffle_remap(C, groups):
+    # out channel j = i * groups + g  <-  in channel g * (C / groups) + i
+    def build():
+        cpg = C // groups
+        return Remap([(j % groups) * cpg + j // groups for j in range(C)], C)
+    return Remap.get(("shuffle", C, groups), build)
+
+
 def channel_shuffle(x, groups):
-    """[N,C,H,W] -> [N,g,C/g,H,W] -> transpose -> [N,C,H,W] (shufflenet*.py ShuffleBlock)."""
+    """[N,C,H,W] -> [N,g,C/g,H,W] -> transpose -> [N,C,H,W] (shufflenet*.py ShuffleBlock): on the
+    GPU one native channel-remap pass each way (NHWC, the channel dim is innermost) instead of a
+    transposing stock copy."""
     N, C, H, W = x.shape
-    out = x.reshape(N, groups, C // groups, H, W).transpose(1, 2).reshape(N, C, H, W)
-    if not _ref(out):
-        out = out.contiguous(memory_format=torch.channels_last)
-    return out
+    if _ref(x) or x.dtype != COMPUTE_DTYPE:
+        out = x.reshape(N, groups, C // groups, H, W).transpose(1, 2).reshape(N, C, H, W)
+        if not _ref(out):
+            out = out.contiguous(memory_format=torch.channels_last)
+        return out
+    xn = to_nhwc(x)
+    return to_nchw(_RemapFn.apply(xn, _shuffle_remap(C, groups), xn.shape, None))
 
 
 class _CatNHWC(torch.autograd.Function):

@@ -345,6 +345,79 @@ def test_group_padded_conv_matches_fp32(Cin, Cout, G, k, s):
     assert rel(wn.grad, w.grad) < 2e-2
 
 
+@pytest.mark.parametrize("Cin,Cout,G", [(200, 50, 2), (12, 44, 1), (96, 75, 3)])
+def test_group_padded_conv_bias_and_native_remaps(Cin, Cout, G):
+    """The padded grouped conv's pad / slice are native remaps (no stock pad / slice kernels):
+    a biased conv's output, dX, dW, db vs fp32, with dW / db added into existing gradients."""
+    import torch.nn.functional as F
+    from pytorch_cifar_amd.ops import functional as OF
+
+    torch.manual_seed(17)
+    x = torch.randn(3, Cin, 9, 9, device="cuda").bfloat16().float().requires_grad_(True)
+    w = (torch.randn(Cout, Cin // G, 3, 3, device="cuda") * 0.2).requires_grad_(True)
+    b = torch.randn(Cout, device="cuda").requires_grad_(True)
+    ref = F.conv2d(x, w, b, 1, 1, 1, G)
+    dy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(dy)
+    wn = w.detach().clone().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    bn = b.detach().clone().requires_grad_(True)
+    wn.grad = torch.ones_like(wn)            # accumulation into an existing gradient buffer
+    bn.grad = torch.ones_like(bn)
+    xn = x.detach().bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    with torch.autograd.profiler.profile(use_device="cuda") as prof:
+        y, _ = OF.conv2d(xn, wn, bn, 1, 1, G, False)
+        y.backward(dy.to(y.dtype).contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+    assert rel(y, ref) < 1e-2
+    assert rel(xn.grad, x.grad) < 2e-2
+    assert rel(wn.grad - 1, w.grad) < 2e-2
+    assert rel(bn.grad - 1, b.grad) < 2e-2
+    names = " ".join(e.name for e in prof.function_events)
+    assert "constant_pad" not in names and "aten::slice_backward" not in names, names
+
+
+@pytest.mark.parametrize("C,g", [(200, 2), (240, 3), (64, 4), (30, 3)])
+def test_channel_shuffle_native(C, g):
+    """ShuffleNet channel shuffle as a native remap (fwd + bwd) vs the reshape/transpose oracle."""
+    from pytorch_cifar_amd.ops import functional as OF
+
+    torch.manual_seed(18)
+    x = torch.randn(2, C, 5, 7, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xr = x.float().requires_grad_(True)
+    ref = xr.reshape(2, g, C // g, 5, 7).transpose(1, 2).reshape(2, C, 5, 7)
+    xn = x.clone().requires_grad_(True)
+    y = OF.channel_shuffle(xn, g)
+    assert torch.equal(y.float(), ref.detach())
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    y.backward(dy.contiguous(memory_format=torch.channels_last))
+    assert torch.equal(xn.grad.float(), xr.grad)
+
+
+def test_chan_remap_row_map_and_accumulate():
+    """chan_remap with an outer row map (conv weight padding) and fp32 accumulation vs indexing."""
+    from pytorch_cifar_amd import _native
+
+    C = _native.lib()
+    torch.manual_seed(19)
+    K, Cin = 9, 13
+    x = torch.randn(6 * K, Cin, device="cuda")
+    cmap = [c if c < Cin else -1 for c in range(16)]
+    rmap = [0, 1, -1, 2, 3, 4, 5, -1]
+    out = C.chan_remap(x, torch.tensor(cmap, dtype=torch.int32, device="cuda"),
+                       torch.tensor(rmap, dtype=torch.int32, device="cuda"), K)
+    xv = x.view(6, K, Cin)
+    ref = torch.zeros(8, K, 16, device="cuda")
+    for r, s in enumerate(rmap):
+        if s >= 0:
+            ref[r, :, :Cin] = xv[s]
+    assert torch.equal(out.view(8, K, 16), ref)
+    acc = torch.ones(8 * K, 16, device="cuda")
+    C.chan_remap(x, torch.tensor(cmap, dtype=torch.int32, device="cuda"),
+                 torch.tensor(rmap, dtype=torch.int32, device="cuda"), K, acc)
+    assert torch.allclose(acc.view(8, K, 16), ref + 1)
+
+
 def test_dpn_merge_matches_torch():
     """Native DPN dual-path join vs relu(cat[x[:d] + o[:d], x[d:], o[d:]]) and its gradients."""
     from pytorch_cifar_amd.ops import functional as OF
