@@ -56,6 +56,7 @@ void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int,
                        const float* bn_aux = nullptr, float* bn_part = nullptr);
 int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
+void conv_set_bn_dual(const bf16* y2, const float* aux2);
 void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
                        int Cin, int Cout, int KH, int KW, int stride, int pad, int groups, int Ho,
                        int Wo, hipStream_t st);
@@ -373,7 +374,9 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
                                     const optional<Tensor>& bn_y, const optional<Tensor>& bn_mask,
                                     const optional<Tensor>& bn_aux,
                                     const optional<Tensor>& bn_acc = c10::nullopt,
-                                    int acc_rows = 0) {
+                                    int acc_rows = 0,
+                                    const optional<Tensor>& bn_y2 = c10::nullopt,
+                                    const optional<Tensor>& bn_aux2 = c10::nullopt) {
   check_bf16(dy, "dy");
   check_bf16(wt, "wt");
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
@@ -400,6 +403,26 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
     check_f32(*bn_aux, "bn_aux");
     TORCH_CHECK(bn_aux->numel() >= 2 * Cin, "bn_aux [mean|istd|...][C]");
   }
+  // dual BN (projection-shortcut block tail): third sum dz * xhat2, accumulator mode only
+  const bool dual = want_bn && bn_y2.has_value() && bn_y2->defined() && bn_acc.has_value() &&
+                    bn_acc->defined();
+  if (dual) {
+    check_bf16(*bn_y2, "bn_y2");
+    TORCH_CHECK(bn_y2->numel() == bn_y->numel(), "bn_y2 must match dx (NHWC)");
+    TORCH_CHECK(bn_aux2.has_value() && bn_aux2->defined(), "bn_aux2 required");
+    check_f32(*bn_aux2, "bn_aux2");
+    TORCH_CHECK(bn_aux2->numel() >= 2 * Cin, "bn_aux2 [mean|istd|...][C]");
+  }
+  const int NS = dual ? 3 : 2;
+  struct DualScope {
+    bool on;
+    DualScope(bool d, const bf16* y2, const float* a2) : on(d) {
+      if (on) pca::conv_set_bn_dual(y2, a2);
+    }
+    ~DualScope() {
+      if (on) pca::conv_set_bn_dual(nullptr, nullptr);
+    }
+  } dual_scope(dual, dual ? ptr<bf16>(*bn_y2) : nullptr, dual ? ptr<float>(*bn_aux2) : nullptr);
   if (g_autotune && !stream_capturing(cur_stream()) &&
       pca::conv_needs_tune(1, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, false)) {
     // trials run the call as issued: with the fused BN-backward reduce when it is requested
@@ -413,7 +436,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
       const int r = want_bn ? pca::conv_dgrad_bn_rows(N, H, W, Cin, Cout, KH, KW, stride, pad,
                                                       groups, Ho, Wo)
                             : 0;
-      if (r > 0) pt = at::empty({r, 2, Cin}, dy.options().dtype(at::kFloat));
+      if (r > 0) pt = at::empty({r, NS, Cin}, dy.options().dtype(at::kFloat));
       pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dxt), N, H, W, Cin, Cout, KH,
                              KW, stride, pad, groups, Ho, Wo, cur_stream(), add,
                              n > 0 ? ptr<float>(wst) : nullptr,
@@ -433,7 +456,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
                            : 0;
   const bool use_acc = rows > 0 && bn_acc.has_value() && bn_acc->defined();
   if (use_acc) {
-    check_acc(*bn_acc, acc_rows, 2, Cin);
+    check_acc(*bn_acc, acc_rows, NS, Cin);
     part = *bn_acc;
   } else if (rows > 0) {
     part = at::empty({rows, 2, Cin}, dy.options().dtype(at::kFloat));
@@ -1623,8 +1646,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_bn", &conv_dgrad_impl, py::arg("dy"), py::arg("wt"), py::arg("H"),
         py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend"),
         py::arg("bn_y"), py::arg("bn_mask"), py::arg("bn_aux"), py::arg("bn_acc") = py::none(),
-        py::arg("acc_rows") = 0,
-        "dgrad + fused backward reduce of the producing BN+ReLU -> (dx, partial[rows][2][C])");
+        py::arg("acc_rows") = 0, py::arg("bn_y2") = py::none(), py::arg("bn_aux2") = py::none(),
+        "dgrad + fused backward reduce of the producing BN+ReLU -> (dx, partial[rows][2][C]); "
+        "with bn_y2 / bn_aux2 (dual BN, accumulator mode) the accumulator gets [R][3][C] sums");
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
   m.def("conv_autotune_enabled", []() { return g_autotune; });

@@ -59,7 +59,11 @@ struct ConvGeom {
   const bf16* bn_y;     // that BN's input y
   const uint8_t* bn_mask;
   const float* bn_aux;  // [mean | istd | ...][Co]
-  float* bn_part;       // [rows][2][Co]
+  float* bn_part;       // [rows][NS][Co]
+  // dual BN (projection-shortcut block tail act(BN(y) + BN2(y2))): the third sum dz * xhat2
+  // (accumulator mode only; NS = 3)
+  const bf16* bn_y2;
+  const float* bn_aux2;
   int shards;           // BN partial sums (stats / bn_part): 0 = slab rows, >0 = sharded atomics
 };
 
@@ -78,12 +82,26 @@ __device__ __forceinline__ void bn_fuse_acc(const uint4& v, const bf16* y, uint8
   }
 }
 
+// dual-BN third sum: dz * xhat2 of the projection-shortcut BN input y2
+__device__ __forceinline__ void bn_fuse_acc3(const uint4& v, const bf16* y2, uint8_t m,
+                                             const float* aux2, int ch, int Co, float* s3) {
+  float f[8], yy[8];
+  unpack8(v, f);
+  unpack8(*reinterpret_cast<const uint4*>(y2), yy);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
+    s3[q] += dz * (yy[q] - aux2[ch + q]) * aux2[Co + ch + q];
+  }
+}
+
 // block reduction of the per-thread (s1, s2) of channel group c8 = tid % CG (NT % CG == 0) into
-// slab row `row`; channel base ch0 of group 0 (red: NT * 16 floats of LDS)
+// slab row `row`; channel base ch0 of group 0 (red: NT * 16 floats of LDS); NS = row stride in
+// units of Co (2, or 3 for a dual BN's accumulator)
 template <int NT>
 __device__ __forceinline__ void bn_fuse_flush(float* red, const float* s1, const float* s2,
                                               int CG, int ch0, int cvalid, int Co, float* part,
-                                              int row, int shards) {
+                                              int row, int shards, int NS = 2) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -100,9 +118,30 @@ __device__ __forceinline__ void bn_fuse_flush(float* red, const float* s1, const
       for (int q = 0; q < 16; ++q) a[q] += red[j * 16 + q];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      stat_out(part, row, shards, 2 * Co, ch0 + tid * 8 + q, a[q]);
-      stat_out(part, row, shards, 2 * Co, Co + ch0 + tid * 8 + q, a[8 + q]);
+      stat_out(part, row, shards, NS * Co, ch0 + tid * 8 + q, a[q]);
+      stat_out(part, row, shards, NS * Co, Co + ch0 + tid * 8 + q, a[8 + q]);
     }
+  }
+}
+
+// per-tile flush of the dual third sum (accumulator mode: atomics into shard row % shards)
+template <int NT>
+__device__ __forceinline__ void bn_fuse_flush3(float* red, const float* s3, int CG, int ch0,
+                                               int cvalid, int Co, float* part, int row,
+                                               int shards) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[tid * 8 + q] = s3[q];
+  __syncthreads();
+  if (tid < CG && tid * 8 < cvalid) {
+    float a[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] = 0.f;
+    for (int j = tid; j < NT; j += CG)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] += red[j * 8 + q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) stat_out(part, row, shards, 3 * Co, 2 * Co + ch0 + tid * 8 + q, a[q]);
   }
 }
 
@@ -531,6 +570,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         }
     __syncthreads();
     constexpr int CG = BN / 8;
+    float bs3[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bs3[q] = 0.f;
+    const bool dual = bnf && g.bn_y2 != nullptr;
 #pragma unroll
     for (int it = 0; it < (BM * CG) / NT; ++it) {
       const int idx = tid + it * NT;
@@ -557,17 +600,25 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
           v = pack8(a);
         }
         if (bnf) bn_fuse_acc(v, g.bn_y + o, g.bn_mask[o >> 3], bmean, bistd, bs1, bs2);
+        if (dual) bn_fuse_acc3(v, g.bn_y2 + o, g.bn_mask[o >> 3], g.bn_aux2, grp * g.Cn + gc, g.Co, bs3);
         *reinterpret_cast<uint4*>(Y + o) = v;
       }
     }
     __syncthreads();   // the C tile aliases the ring the next tile's prologue refills
+    if constexpr (DGRAD && !SPLITK) {
+      if (dual) {   // (epilogue-local: no accumulator registers live across the K loop)
+        bn_fuse_flush3<NT>(reinterpret_cast<float*>(smem), bs3, CG_, grp * g.Cn + n0, g.Cn - n0,
+                           g.Co, g.bn_part, (int)blockIdx.x, g.shards);
+        __syncthreads();
+      }
+    }
   }
 
   if constexpr (DGRAD && !SPLITK) {
     if (bnf) {   // slab row per (M-walker, parity class); channels of this block's N tile
       const int row = PARITY ? (int)blockIdx.x * 4 + cls : (int)blockIdx.x;
       bn_fuse_flush<NT>(reinterpret_cast<float*>(smem), bs1, bs2, CG_, grp * g.Cn + n0,
-                        g.Cn - n0, g.Co, g.bn_part, row, g.shards);
+                        g.Cn - n0, g.Co, g.bn_part, row, g.shards, g.bn_y2 ? 3 : 2);
     }
   }
   if constexpr (STATS && !SPLITK) {
@@ -1289,8 +1340,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                            const uint8_t* __restrict__ bn_mask,
                                                            const float* __restrict__ bn_aux,
                                                            float* __restrict__ bn_part,
-                                                           int shards) {
-  __shared__ float red[2 * 2048];
+                                                           int shards,
+                                                           const bf16* __restrict__ bn_y2,
+                                                           const float* __restrict__ bn_aux2) {
+  __shared__ float red[3 * 2048];
+  const int NSB = bn_y2 ? 3 : 2;      // fused BN sums per channel (3: dual BN)
   const int CG = Co >> 3;             // 8-channel groups per row (Co <= 2048: CG <= 256)
   const int RP = 256 / CG;            // rows per pass
   const int tid = threadIdx.x;
@@ -1304,10 +1358,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
   const size_t plane = (size_t)M * Co;
-  float bs1[8], bs2[8], bmean[8], bistd[8];
+  float bs1[8], bs2[8], bs3[8], bmean[8], bistd[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    bs1[q] = bs2[q] = 0.f;
+    bs1[q] = bs2[q] = bs3[q] = 0.f;
     bmean[q] = bn_part && active ? bn_aux[cg * 8 + q] : 0.f;
     bistd[q] = bn_part && active ? bn_aux[Co + cg * 8 + q] : 0.f;
   }
@@ -1338,6 +1392,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       }
       const uint4 pv = pack8(a);
       if (bn_part) bn_fuse_acc(pv, bn_y + o, bn_mask[o >> 3], bmean, bistd, bs1, bs2);
+      if (bn_part && bn_y2) bn_fuse_acc3(pv, bn_y2 + o, bn_mask[o >> 3], bn_aux2, cg * 8, Co, bs3);
       *reinterpret_cast<uint4*>(Y + o) = pv;
     }
   }
@@ -1345,18 +1400,21 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      red[(rr * Co + cg * 8 + q) * 2 + 0] = active ? bs1[q] : 0.f;
-      red[(rr * Co + cg * 8 + q) * 2 + 1] = active ? bs2[q] : 0.f;
+      red[(rr * Co + cg * 8 + q) * 3 + 0] = active ? bs1[q] : 0.f;
+      red[(rr * Co + cg * 8 + q) * 3 + 1] = active ? bs2[q] : 0.f;
+      red[(rr * Co + cg * 8 + q) * 3 + 2] = active ? bs3[q] : 0.f;
     }
     __syncthreads();
     for (int c = tid; c < Co; c += 256) {
-      float s0 = 0.f, q0 = 0.f;
+      float s0 = 0.f, q0 = 0.f, t0 = 0.f;
       for (int k = 0; k < RP; ++k) {
-        s0 += red[(k * Co + c) * 2 + 0];
-        q0 += red[(k * Co + c) * 2 + 1];
+        s0 += red[(k * Co + c) * 3 + 0];
+        q0 += red[(k * Co + c) * 3 + 1];
+        t0 += red[(k * Co + c) * 3 + 2];
       }
-      stat_out(bn_part, blockIdx.x, shards, 2 * Co, c, s0);
-      stat_out(bn_part, blockIdx.x, shards, 2 * Co, Co + c, q0);
+      stat_out(bn_part, blockIdx.x, shards, NSB * Co, c, s0);
+      stat_out(bn_part, blockIdx.x, shards, NSB * Co, Co + c, q0);
+      if (NSB == 3) stat_out(bn_part, blockIdx.x, shards, NSB * Co, 2 * Co + c, t0);
     }
     return;
   }
@@ -1412,6 +1470,8 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   g.bn_mask = nullptr;
   g.bn_aux = nullptr;
   g.bn_part = nullptr;
+  g.bn_y2 = nullptr;
+  g.bn_aux2 = nullptr;
   g.shards = stat_shards();
   return g;
 }
@@ -1559,10 +1619,10 @@ static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, co
     const int gx = splitk_reduce_grid(M, g.Co, &rpb);
     if (stats)
       hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
-                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards);
+                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2);
     else
       hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
-                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards);
+                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2);
     return;
   }
   const ConvGeom& g = g0;
@@ -1836,10 +1896,22 @@ static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int K
   return g;
 }
 
+// Dual-BN request of the next dgrad launch(es) (bindings scope it around one call): the fused
+// reduce also adds dz * xhat2 of the projection-shortcut BN (y2, aux2) — generic igemm / split-K
+// stride-1 dgrads into a sharded accumulator only.
+static const bf16* g_dual_y2 = nullptr;
+static const float* g_dual_aux2 = nullptr;
+void conv_set_bn_dual(const bf16* y2, const float* aux2) {
+  g_dual_y2 = y2;
+  g_dual_aux2 = aux2;
+}
+
 // slab rows the fused BN-backward reduce of this dgrad launch writes (its grid / reduce grid),
-// or 0 when the selected kernel cannot fuse it (the phased 256-row kernel)
+// or 0 when the selected kernel cannot fuse it (the phased 256-row kernel; with a dual-BN request
+// every kernel but the generic igemm / split-K stride-1 dgrad)
 int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo) {
+  const bool dual = g_dual_y2 != nullptr;
   // the layer-1 c64 kernel prefetches the fused reduce's y / mask (and the residual addend) at
   // tile start so they hide under its MFMA loop (read in its one-workgroup-per-CU epilogue they
   // cost +116 us per call at bs1024); PCA_C64_BN_FUSE=0 keeps the separate reduce for layer 1
@@ -1848,9 +1920,10 @@ int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
     return !(e && e[0] == '0');
   }();
   if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
-    return c64_fuse ? conv_c64_stat_rows(N, H) : 0;
+    return c64_fuse && !dual ? conv_c64_stat_rows(N, H) : 0;
   const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   if (g.Co % 8 != 0) return 0;
+  if (dual && (g.mode != 1 || ph_cfg<1>(g) >= 0 || use_hx<1>(g))) return 0;
   if (g.mode == 2) {
     if (use_hx<2>(g)) return hx_grid<2>(g);   // one slab row per (tile group, class-channel block)
     if (igemm_ws_floats<2>(g) > 0) {
@@ -1981,6 +2054,10 @@ void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, i
   g.bn_mask = bn_mask;
   g.bn_aux = bn_aux;
   g.bn_part = bn_part;
+  if (bn_part && g_dual_y2 && g.mode == 1 && ph_cfg<1>(g) < 0 && !use_hx<1>(g)) {
+    g.bn_y2 = g_dual_y2;
+    g.bn_aux2 = g_dual_aux2;
+  }
   if (g.mode == 2) {
     igemm_dispatch<2>(dy, wt, dx, nullptr, nullptr, g, st, addend, ws);
   } else {

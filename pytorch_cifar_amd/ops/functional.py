@@ -383,6 +383,14 @@ def _prepped_weight(weight, groups, w_phys, need_dx):
 # incoming gradient IS that dgrad's output (same storage): any other gradient contribution makes
 # autograd produce a new tensor and the BN falls back to its own reduce.
 _FUSE_BN_BWD = os.environ.get("PCA_FUSE_BN_BWD", "1") != "0"
+# the same for a dual BN (act(BN(y) + BN2(y2)), the projection-shortcut block tail): generic
+# igemm / split-K stride-1 dgrads add the third sum dz * xhat2 (PCA_DUAL_BN_FUSE=0: separate pass)
+_DUAL_BN_FUSE = os.environ.get("PCA_DUAL_BN_FUSE", "1") != "0"
+
+
+def set_dual_bn_fuse(on: bool) -> None:
+    global _DUAL_BN_FUSE
+    _DUAL_BN_FUSE = bool(on)
 
 
 def set_fuse_bn_backward(on: bool) -> None:
@@ -392,10 +400,11 @@ def set_fuse_bn_backward(on: bool) -> None:
 
 
 class _BNSrc:
-    __slots__ = ("y", "mask", "aux", "part", "dx", "acc", "act")
+    __slots__ = ("y", "mask", "aux", "part", "dx", "acc", "act", "y2", "aux2")
 
-    def __init__(self, y, mask, aux, acc=None, act=1):
+    def __init__(self, y, mask, aux, acc=None, act=1, y2=None, aux2=None):
         self.y, self.mask, self.aux = y, mask, aux
+        self.y2, self.aux2 = y2, aux2   # dual BN (projection-shortcut tail): NS = 3 sums
         self.part = None
         self.dx = None
         self.acc = acc        # the BN's backward StatAcc (sharded-accumulator mode) or None
@@ -507,13 +516,13 @@ def _own_stats(bn, role, y_nhwc, stats):
 
 
 def _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add):
-    if src is None or src.act != 1 or src.mask is None:
+    if src is None or src.act != 1 or src.mask is None or (src.y2 is not None and src.acc is None):
         return C.conv_dgrad(dy, wt, H, W, stride, padding, groups, add)
     acc = src.acc
     if acc is not None:
         acc.begin()
         dx, part = C.conv_dgrad_bn(dy, wt, H, W, stride, padding, groups, add, src.y, src.mask,
-                                   src.aux, acc.buf, acc.R)
+                                   src.aux, acc.buf, acc.R, src.y2, src.aux2)
     else:
         dx, part = C.conv_dgrad_bn(dy, wt, H, W, stride, padding, groups, add, src.y, src.mask,
                                    src.aux)
@@ -997,6 +1006,11 @@ class _BatchNormAct(torch.autograd.Function):
         # (grad mode is off inside Function.forward: the caller decided it in cfg.src)
         if cfg.src is not None and relu and has_mask and y2 is None:
             ctx.bnsrc = cfg.src = _BNSrc(y, mask, aux, cfg.bacc)
+        elif cfg.src is not None and relu and has_mask and _DUAL_BN_FUSE and \
+                cfg.bacc is not None and cfg.bacc.NS >= 3 and aux2 is not None:
+            # projection-shortcut tail: the consumer dgrad adds all three sums (dz, dz*xhat,
+            # dz*xhat2) into the accumulator — no separate reduce + finalize launches
+            ctx.bnsrc = cfg.src = _BNSrc(y, mask, aux, cfg.bacc, y2=y2, aux2=aux2)
         elif cfg.src is not None and ACT[cfg.act] == 2 and y2 is None and res is None and \
                 cfg.bacc is not None and aux is not None and aux.numel() >= 4 * y.shape[-1]:
             # swish: only a depthwise consumer can fuse it (z recomputed from y, aux scale|shift)

@@ -316,6 +316,73 @@ def test_bn_backward_reduce_fusion_matches_separate_pass():
     assert not bad, bad
 
 
+@pytest.mark.parametrize("N,H,C", [(16, 4, 512), (128, 4, 512), (64, 16, 128), (32, 8, 256)])
+def test_conv_dgrad_dual_bn_sums(N, H, C):
+    """conv_dgrad_bn with a dual-BN request: dX and the three accumulator sums (dz, dz*xhat,
+    dz*xhat2 with dz = dX * mask) against torch on the same bf16 dX."""
+    from pytorch_cifar_amd import _native
+    from pytorch_cifar_amd.ops import functional as PF
+
+    Cn = _native.lib()
+    torch.manual_seed(23)
+    dy = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = torch.randn(C, C, 3, 3, device="cuda") * 0.05
+    wb, wt = Cn.weight_prep(w.permute(0, 2, 3, 1).contiguous(), 1, True)
+    y = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    y2 = (torch.randn(N, H, H, C, device="cuda") * 2 + 0.5).bfloat16()
+    mask_bits = torch.rand(N * H * H * C, device="cuda") > 0.4
+    mask = (mask_bits.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1).to(torch.uint8)
+    aux = torch.cat([torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5,
+                     torch.zeros(2 * C, device="cuda")])
+    aux2 = torch.cat([torch.randn(C, device="cuda") * 0.3 + 0.5, torch.rand(C, device="cuda") + 0.5,
+                      torch.zeros(2 * C, device="cuda")])
+    R = PF.acc_shards(C)
+    acc = torch.zeros(R * 3 * C, device="cuda")
+    dx, part = Cn.conv_dgrad_bn(dy, wt, H, H, 1, 1, 1, None, y, mask, aux, acc, R, y2, aux2)
+    ref = torch.nn.functional.conv_transpose2d(dy.permute(0, 3, 1, 2).float(), w, padding=1)
+    assert rel(dx.permute(0, 3, 1, 2).float(), ref) < 1e-2
+    if part.numel() == 0:
+        pytest.skip("selected dgrad kernel cannot fuse a dual BN")
+    dz = dx.float().reshape(-1, C) * mask_bits.view(-1, C).float()
+    xh = (y.float().reshape(-1, C) - aux[:C]) * aux[C:2 * C]
+    xh2 = (y2.float().reshape(-1, C) - aux2[:C]) * aux2[C:2 * C]
+    got = acc.view(R, 3, C).sum(0)
+    assert rel(got[0], dz.sum(0)) < 1e-3
+    assert rel(got[1], (dz * xh).sum(0)) < 1e-3
+    assert rel(got[2], (dz * xh2).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("batch", [128, 256])
+def test_dual_bn_backward_reduce_fusion(batch):
+    """Projection-shortcut block tails act(BN(y) + BN2(y2)): the three backward sums reduced in
+    the consumer conv's dgrad epilogue (igemm) or split-K reduce equal the separate reduce pass —
+    every parameter gradient after one step (a second step is not comparable: fp32-atomic BN sums
+    make its forward differ at bf16-rounding level, amplified through 20 layers)."""
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.ops import functional as PF
+
+    torch.manual_seed(3)
+    base = models.ResNet18().cuda()
+    x = torch.randn(batch, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (batch,), device="cuda")
+    grads = []
+    try:
+        for fuse in (False, True):
+            PF.set_dual_bn_fuse(fuse)
+            m = copy.deepcopy(base)
+            PF.cross_entropy(m(x), y).backward()
+            torch.cuda.synchronize()
+            grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    finally:
+        PF.set_dual_bn_fuse(True)
+    bad = []
+    for n, g0 in grads[0].items():
+        e = rel(grads[1][n], g0)
+        if e > 2e-2:
+            bad.append((n, round(e, 4)))
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("Cin,Cout,G,k,s", [(200, 50, 2, 1, 1), (50, 176, 2, 1, 1), (96, 96, 32, 3, 2),
                                            (128, 128, 32, 3, 1), (12, 44, 1, 3, 1), (3, 6, 1, 5, 1)])
 def test_group_padded_conv_matches_fp32(Cin, Cout, G, k, s):
