@@ -37,7 +37,7 @@ def _grid(r):
 def _window(rows):
     """rows (dispatch_id, ...) sorted; keep the last complete step (after the second-to-last
     sgd_kernel up to and including the last one)."""
-    sgd = [r[0] for r in rows if "sgd_kernel" in r[1]]
+    sgd = [r[0] for r in rows if "sgd_kernel" in r[1] or "sgd_prep_kernel" in r[1]]
     if len(sgd) >= 2:
         lo, hi = sgd[-2], sgd[-1]
         rows = [r for r in rows if lo < r[0] <= hi]
@@ -104,6 +104,12 @@ def main():
     total = sum(r[0] for r in rows)
     hdr = f"{'us/step':>9} {'n':>3} {'MFMA%':>6} {'HBM GB/s':>9} {'LDSconf%':>8}  kernel"
     print(f"step kernels: {total:.1f} us (min over passes per kernel), {len(rows)} distinct kernels")
+    # whole-step traffic past L2 (the same FETCH/WRITE estimate as the per-kernel column)
+    tb = sum((2 * e["c"].get("FETCH_SIZE", 0.0) + e["c"].get("WRITE_SIZE", 0.0)) * 1024
+             for e in agg.values())
+    if tb > 0 and total > 0:
+        print(f"step traffic past L2: {tb / 1e9:.2f} GB -> {tb / (total * 1e3):.0f} GB/s averaged over "
+              f"the step's kernel time")
     print(hdr)
     for us, n, mfma, gbs, conf, lds, name in rows[: a.top if a.top > 0 else None]:
         cp = f"{100.0 * conf / lds:8.1f}" if conf is not None and lds else f"{'-':>8}"
