@@ -120,7 +120,8 @@ bool head_batch_supported(int N, int K);
 void head_fwd_launch(const bf16*, int, int, int, const float*, const float*, int, float*, float*,
                      float, int64_t*, uint8_t*, hipStream_t);
 void head_bwd_launch(const float*, const float*, const float*, int, int, int, int, bf16*, float*,
-                     float*, float, const uint8_t*, hipStream_t);
+                     float*, float, const uint8_t*, hipStream_t, const bf16* bn_y,
+                     const uint8_t* bn_mask, const float* bn_aux, float* bn_acc, int bn_R);
 void dropout_fwd_launch(const void*, bool, size_t, int64_t, float, int64_t*, uint8_t*, void*,
                         hipStream_t);
 void dropout_bwd_launch(const void*, bool, size_t, int64_t, float, const uint8_t*, void*,
@@ -1061,7 +1062,11 @@ Tensor dropout_bwd(const Tensor& dy, const Tensor& mask, double p, int64_t unit_
 // the given accumulators (gradient-arena views) when present, else fresh zero-based tensors
 std::vector<Tensor> head_bwd(const Tensor& dl, const Tensor& w, const Tensor& pooled, int H, int W,
                              const optional<Tensor>& dw_acc, const optional<Tensor>& db_acc,
-                             bool want_db, double p, const optional<Tensor>& dmask) {
+                             bool want_db, double p, const optional<Tensor>& dmask,
+                             const optional<Tensor>& bn_y = c10::nullopt,
+                             const optional<Tensor>& bn_mask = c10::nullopt,
+                             const optional<Tensor>& bn_aux = c10::nullopt,
+                             const optional<Tensor>& bn_acc = c10::nullopt, int acc_rows = 0) {
   check_f32(dl, "dlogits");
   check_f32(w, "weight");
   check_f32(pooled, "pooled");
@@ -1079,9 +1084,24 @@ std::vector<Tensor> head_bwd(const Tensor& dl, const Tensor& w, const Tensor& po
     TORCH_CHECK(dmask->scalar_type() == at::kByte && dmask->numel() == (int64_t)N * C && p > 0.0 &&
                     p < 1.0,
                 "dropout mask [N, C] uint8 and p in (0, 1)");
+  // fused backward sums of the BN(+ReLU) that produced the pooled features (see head_bwd_kernel)
+  const bool bnf = bn_acc.has_value() && bn_acc->defined();
+  if (bnf) {
+    TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "head_bwd BN fusion: 256 % (C/8) == 0");
+    check_bf16(*bn_y, "bn_y");
+    TORCH_CHECK(bn_y->numel() == (int64_t)N * H * W * C, "bn_y must match dx");
+    TORCH_CHECK(bn_mask.has_value() && bn_mask->defined() && bn_mask->scalar_type() == at::kByte &&
+                    bn_mask->numel() * 8 == bn_y->numel(), "bn_mask: one bit per element");
+    check_f32(*bn_aux, "bn_aux");
+    TORCH_CHECK(bn_aux->numel() >= 2 * C, "bn_aux [mean|istd|...][C]");
+    check_acc(*bn_acc, acc_rows, 2, C);
+  }
   pca::head_bwd_launch(ptr<float>(dl), ptr<float>(w), ptr<float>(pooled), N, H * W, C, K,
                        ptr<bf16>(dx), ptr<float>(dw), db.defined() ? ptr<float>(db) : nullptr,
-                       (float)p, drop ? ptr<uint8_t>(*dmask) : nullptr, cur_stream());
+                       (float)p, drop ? ptr<uint8_t>(*dmask) : nullptr, cur_stream(),
+                       bnf ? ptr<bf16>(*bn_y) : nullptr, bnf ? bn_mask->data_ptr<uint8_t>() : nullptr,
+                       bnf ? ptr<float>(*bn_aux) : nullptr, bnf ? ptr<float>(*bn_acc) : nullptr,
+                       bnf ? acc_rows : 0);
   return {dx, dw, db};
 }
 
@@ -1714,7 +1734,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fused global-average-pool [+ Philox dropout] + Linear -> (logits, pooled, keep mask)");
   m.def("head_bwd", &head_bwd, py::arg("dl"), py::arg("w"), py::arg("pooled"), py::arg("H"),
         py::arg("W"), py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none(),
-        py::arg("want_db") = true, py::arg("p") = 0.0, py::arg("dmask") = py::none());
+        py::arg("want_db") = true, py::arg("p") = 0.0, py::arg("dmask") = py::none(),
+        py::arg("bn_y") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_aux") = py::none(),
+        py::arg("bn_acc") = py::none(), py::arg("acc_rows") = 0);
   m.def("dropout_fwd", &dropout_fwd, "Philox dropout / drop-connect -> (y, keep mask per unit)");
   m.def("dropout_bwd", &dropout_bwd, "dropout / drop-connect gradient from the keep mask");
   m.def("head_supported", [](int N, int C, int K) {

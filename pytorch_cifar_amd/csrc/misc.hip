@@ -1660,6 +1660,18 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ 
   if (drop) drop_advance(rng);
 }
 
+// Optional fused backward reduce of the BatchNorm(+ReLU) that produced the pooled features
+// (ResNet / PreAct block tails): the per-sample blocks also add sum dz and sum dz * xhat of
+// dz = dX * relu'(mask) into that BN's sharded accumulator (one launch fewer for its reduce and
+// one for its finalize). Needs 256 % (C / 8) == 0 (a thread's channel group is fixed).
+struct HeadBnFuse {
+  const bf16* y;
+  const uint8_t* mask;
+  const float* aux;   // [mean | istd | ...][C]
+  float* acc;         // [R][2][C]
+  int R;
+};
+
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dl,
                                                        const float* __restrict__ w,
                                                        const float* __restrict__ pooled, int N,
@@ -1667,7 +1679,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
                                                        bf16* __restrict__ dx,
                                                        float* __restrict__ dw,
                                                        float* __restrict__ db, float p,
-                                                       const uint8_t* __restrict__ dmask) {
+                                                       const uint8_t* __restrict__ dmask,
+                                                       HeadBnFuse bf) {
   extern __shared__ float hs[];
   const int tid = threadIdx.x;
   if ((int)blockIdx.x < N) {
@@ -1689,9 +1702,58 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     __syncthreads();
     const int CG = C >> 3;
     bf16* dxn = dx + (size_t)n * HW * C;
+    if (!bf.acc) {
+      for (int i = tid; i < HW * CG; i += 256) {
+        const int g = i % CG;
+        *reinterpret_cast<uint4*>(dxn + (size_t)i * 8) = pack8(hs + g * 8);
+      }
+      return;
+    }
+    // fused BN-backward sums: this thread's channel group g = tid % CG is fixed (256 % CG == 0)
+    const int g = tid % CG;
+    float mean[8], istd[8], s1[8], s2[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      mean[q] = bf.aux[g * 8 + q];
+      istd[q] = bf.aux[C + g * 8 + q];
+      s1[q] = s2[q] = 0.f;
+    }
+    const uint4 v = pack8(hs + g * 8);   // every pixel of the sample carries the same dX row
+    float f[8];
+    unpack8(v, f);
+    const size_t base = (size_t)n * HW * C;
     for (int i = tid; i < HW * CG; i += 256) {
-      const int g = i % CG;
-      *reinterpret_cast<uint4*>(dxn + (size_t)i * 8) = pack8(hs + g * 8);
+      const size_t o = base + (size_t)i * 8;
+      *reinterpret_cast<uint4*>(dx + o) = v;
+      float yy[8];
+      unpack8(*reinterpret_cast<const uint4*>(bf.y + o), yy);
+      const uint8_t m = bf.mask[o >> 3];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
+        s1[q] += dz;
+        s2[q] += dz * (yy[q] - mean[q]) * istd[q];
+      }
+    }
+    __syncthreads();                     // hs (the dX row) is no longer read
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      hs[tid * 16 + q] = s1[q];
+      hs[tid * 16 + 8 + q] = s2[q];
+    }
+    __syncthreads();
+    if (tid < CG) {
+      float a[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a[q] = 0.f;
+      for (int j = tid; j < 256; j += CG)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) a[q] += hs[j * 16 + q];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        stat_out(bf.acc, n, bf.R, 2 * C, tid * 8 + q, a[q]);
+        stat_out(bf.acc, n, bf.R, 2 * C, C + tid * 8 + q, a[8 + q]);
+      }
     }
     return;
   }
@@ -1756,11 +1818,14 @@ void head_fwd_launch(const bf16* x, int N, int HW, int C, const float* w, const 
 
 void head_bwd_launch(const float* dl, const float* w, const float* pooled, int N, int HW, int C,
                      int K, bf16* dx, float* dw, float* db, float p, const uint8_t* dmask,
-                     hipStream_t st) {
-  const size_t lds = std::max<size_t>((size_t)C, (size_t)kHeadMaxK * 4 * 64) * sizeof(float);
+                     hipStream_t st, const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux,
+                     float* bn_acc, int bn_R) {
+  HeadBnFuse bf{bn_y, bn_mask, bn_aux, bn_acc, bn_R};
+  size_t lds = std::max<size_t>((size_t)C, (size_t)kHeadMaxK * 4 * 64) * sizeof(float);
+  if (bn_acc) lds = std::max<size_t>(lds, 256 * 16 * sizeof(float));
   const int wblocks = cdiv(C, 64) * cdiv(N, kHeadSamples);
   hipLaunchKernelGGL(head_bwd_kernel, dim3(N + wblocks), dim3(256), lds, st, dl, w, pooled, N,
-                     HW, C, K, dx, dw, db, p, dmask);
+                     HW, C, K, dx, dw, db, p, dmask, bf);
 }
 
 void gap_fwd_launch(const bf16* x, int N, int HW, int C, float* y, hipStream_t st) {

@@ -1275,12 +1275,17 @@ class _PoolLinear(torch.autograd.Function):
     """Global average pool [+ dropout] + Linear in one kernel each way (csrc/misc.hip head_*)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, p=0.0, rng=None):
+    def forward(ctx, x, weight, bias, p=0.0, rng=None, bnsrc=None):
         logits, pooled, dmask = _C().head_fwd(x, weight, bias, p, rng)
         ctx.save_for_backward(weight, pooled, dmask if p > 0 else None)
         ctx.hw = (x.shape[1], x.shape[2])
         ctx.params = (weight, bias)
         ctx.p = p
+        # the producing BN+ReLU (block tail): its backward sums are added by the head backward
+        C = x.shape[-1]
+        ok = (bnsrc is not None and bnsrc.act == 1 and bnsrc.mask is not None and bnsrc.y2 is None
+              and bnsrc.acc is not None and C % 8 == 0 and 256 % (C // 8) == 0)
+        ctx.bnsrc = bnsrc if ok else None
         return logits
 
     @staticmethod
@@ -1290,8 +1295,17 @@ class _PoolLinear(torch.autograd.Function):
         ctx.params = None
         wbuf = G.grad_buffer(w) if (w.requires_grad and w.is_leaf) else None
         bbuf = G.grad_buffer(b) if (b is not None and b.requires_grad and b.is_leaf) else None
-        dx, dw, db = _C().head_bwd(dl.float().contiguous(), weight, pooled, ctx.hw[0], ctx.hw[1],
-                                   wbuf, bbuf, b is not None, ctx.p, dmask)
+        src = ctx.bnsrc
+        ctx.bnsrc = None
+        if src is not None:
+            src.acc.begin()
+            dx, dw, db = _C().head_bwd(dl.float().contiguous(), weight, pooled, ctx.hw[0],
+                                       ctx.hw[1], wbuf, bbuf, b is not None, ctx.p, dmask,
+                                       src.y, src.mask, src.aux, src.acc.buf, src.acc.R)
+            src.part, src.dx = src.acc.buf, dx   # the BN backward finds its sums filled
+        else:
+            dx, dw, db = _C().head_bwd(dl.float().contiguous(), weight, pooled, ctx.hw[0],
+                                       ctx.hw[1], wbuf, bbuf, b is not None, ctx.p, dmask)
         dw_ret = db_ret = None
         if w.requires_grad:
             if wbuf is not None:
@@ -1307,7 +1321,7 @@ class _PoolLinear(torch.autograd.Function):
                 G.accumulate(b, db)
             else:
                 db_ret = db
-        return dx, dw_ret, db_ret, None, None
+        return dx, dw_ret, db_ret, None, None, None
 
 
 def rng_state(owner, device):
@@ -1358,7 +1372,8 @@ def pool_linear(x, kernel_size, linear, dropout_p=0.0, training=False):
             out = dropout(out, p, True, owner=linear)
         return linear(out)
     rng = rng_state(linear, x.device) if p > 0 else None
-    return _PoolLinear.apply(to_nhwc(x), w, b, p, rng)
+    src = getattr(x, "_pca_bnsrc", None) if torch.is_grad_enabled() else None
+    return _PoolLinear.apply(to_nhwc(x), w, b, p, rng, src)
 
 
 class _AvgPool(torch.autograd.Function):
