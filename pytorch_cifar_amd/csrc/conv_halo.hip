@@ -90,12 +90,15 @@ template <int W, int MB, int KP>
 constexpr int halo_stage_bytes() {
   return HaloShape<W, KP>::HBYTES + MB * KP * 128 + 1024;
 }
-template <int W, int MB, int KP>
+template <int W, int MB, int KP, int ST = 3>
 constexpr bool halo_fits() {
-  return 3 * halo_stage_bytes<W, MB, KP>() <= 160 * 1024;
+  return ST * halo_stage_bytes<W, MB, KP>() <= 160 * 1024;
 }
 
-template <int W, int MB, int WM, int WN, int KP, int TG = 9>
+// ST = LDS stages in the ring (ST - 1 stages in flight): the small-image shapes of the 8-GPU
+// shard (layer 4 at bs128: 96 tiles, 32 short stages per tile, DMA-latency bound with 2 stages in
+// flight) take 6 stages of 32 pixels instead of 3 of 64.
+template <int W, int MB, int WM, int WN, int KP, int TG = 9, int ST = 3>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wgrad_halo_kernel(const bf16* __restrict__ X,
                                                                   const bf16* __restrict__ DY,
                                                                   float* __restrict__ out,
@@ -104,7 +107,8 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   constexpr int NW = WM * WN;
   constexpr int KS = KP / 32;                    // MFMA K-steps per stage
   constexpr int DYI = KP / 8;                    // DMA instructions per 64-channel dY block
-  constexpr int STAGES = 3;
+  constexpr int STAGES = ST;
+  static_assert(ST >= 3, "stages");
   constexpr int A_OFF = SH::HBYTES;              // dY blocks follow the halo image
   constexpr int J_OFF = A_OFF + MB * KP * 128;   // junk KiB for the padding DMA slots
   constexpr int STAGE = J_OFF + 1024;
@@ -238,12 +242,12 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
   typedef short i16x8 __attribute__((ext_vector_type(8)));
   const int KT = p_end > p_begin ? cdiv(p_end - p_begin, KP) : 0;
-  issue(p_begin, 0);
-  issue(p_begin + KP, 1);
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) issue(p_begin + s * KP, s);
   for (int kt = 0; kt < KT; ++kt) {
-    wait_vmcnt<SLOTS>();            // stage kt landed (stage kt+1 may still be in flight)
+    wait_vmcnt<(STAGES - 2) * SLOTS>();   // stage kt landed (the STAGES - 2 after it may not have)
     raw_barrier();
-    issue(p_begin + (kt + 2) * KP, (kt + 2) % STAGES);
+    issue(p_begin + (kt + STAGES - 1) * KP, (kt + STAGES - 1) % STAGES);
     if (g.ablate & 2) continue;
     const char* S = smem + (kt % STAGES) * STAGE;
 #pragma unroll
@@ -431,25 +435,30 @@ static int halo_cus() {
   return n;
 }
 
-// X(cfg, MB, WM, WN, KP, TG)
-#define PCA_HALO_CFGS(X)    \
-  X(0, 1, 1, 4, 32, 9)      \
-  X(1, 2, 2, 4, 32, 9)      \
-  X(2, 1, 2, 4, 32, 9)      \
-  X(3, 1, 2, 4, 64, 9)      \
-  X(4, 2, 2, 4, 64, 9)      \
-  X(5, 1, 2, 4, 128, 9)     \
-  X(6, 1, 1, 4, 64, 9)      \
-  X(7, 1, 2, 4, 64, 3)      \
-  X(8, 1, 1, 4, 64, 3)      \
-  X(9, 2, 2, 4, 64, 3)
-constexpr int kHaloCfgs = 10;
+// X(cfg, MB, WM, WN, KP, TG, ST)
+#define PCA_HALO_CFGS(X)       \
+  X(0, 1, 1, 4, 32, 9, 3)      \
+  X(1, 2, 2, 4, 32, 9, 3)      \
+  X(2, 1, 2, 4, 32, 9, 3)      \
+  X(3, 1, 2, 4, 64, 9, 3)      \
+  X(4, 2, 2, 4, 64, 9, 3)      \
+  X(5, 1, 2, 4, 128, 9, 3)     \
+  X(6, 1, 1, 4, 64, 9, 3)      \
+  X(7, 1, 2, 4, 64, 3, 3)      \
+  X(8, 1, 1, 4, 64, 3, 3)      \
+  X(9, 2, 2, 4, 64, 3, 3)      \
+  X(10, 2, 2, 4, 32, 3, 6)     \
+  X(11, 1, 2, 4, 32, 3, 6)     \
+  X(12, 1, 1, 4, 32, 3, 6)     \
+  X(13, 1, 2, 4, 32, 9, 6)     \
+  X(14, 2, 2, 4, 64, 3, 4)
+constexpr int kHaloCfgs = 15;
 
-template <int W, int MB, int WM, int WN, int KP, int TG>
+template <int W, int MB, int WM, int WN, int KP, int TG, int ST>
 static int halo_occupancy() {
   static int occ = 0;
   if (occ == 0) {
-    occ = blocks_per_cu((const void*)wgrad_halo_kernel<W, MB, WM, WN, KP, TG>, WM * WN * 64,
+    occ = blocks_per_cu((const void*)wgrad_halo_kernel<W, MB, WM, WN, KP, TG, ST>, WM * WN * 64,
                         "wgrad_halo");
   }
   return occ;
@@ -515,10 +524,10 @@ static int halo_select(const HaloGeom& g) {
   return g.cout_g <= 64 ? 0 : 1;
 }
 
-template <int W, int MB, int WM, int WN, int KP, int TG>
+template <int W, int MB, int WM, int WN, int KP, int TG, int ST>
 static int64_t halo_plan(HaloGeom& g) {
   const int tiles = cdiv(g.cout_g, 64 * MB) * (g.cin_g / 64) * (9 / TG) * g.groups;
-  const int slots = halo_occupancy<W, MB, WM, WN, KP, TG>() * halo_cus();
+  const int slots = halo_occupancy<W, MB, WM, WN, KP, TG, ST>() * halo_cus();
   int splits = std::max(1, slots / tiles);
   splits = std::min(splits, std::max(1, cdiv(g.P, 256)));
   const int forced = wgrad_split_force();
@@ -533,18 +542,18 @@ static int64_t halo_plan(HaloGeom& g) {
   static const bool verbose = getenv("PCA_CONV_VERBOSE") != nullptr;
   if (verbose)
     fprintf(stderr, "[pca] halo wgrad W=%d MB=%d waves=%d KP=%d: occ=%d cus=%d tiles=%d splits=%d chunk=%d atomic=%d\n",
-            W, MB, WM * WN, KP, halo_occupancy<W, MB, WM, WN, KP, TG>(), halo_cus(), tiles, splits,
+            W, MB, WM * WN, KP, halo_occupancy<W, MB, WM, WN, KP, TG, ST>(), halo_cus(), tiles, splits,
             chunk, g.atomic);
   if (g.atomic) return 0;
   return slab_ws_floats(splits, (int64_t)tiles * (64 * MB) * (TG * 64));
 }
 
-template <int W, int MB, int WM, int WN, int KP, int TG>
+template <int W, int MB, int WM, int WN, int KP, int TG, int ST>
 static void launch_halo(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom g,
                         hipStream_t st) {
-  halo_plan<W, MB, WM, WN, KP, TG>(g);
+  halo_plan<W, MB, WM, WN, KP, TG, ST>(g);
   dim3 grid(cdiv(g.cout_g, 64 * MB), (g.cin_g / 64) * (9 / TG), g.splits * g.groups);
-  hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP, TG>), grid, dim3(WM * WN * 64), 0, st, x,
+  hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP, TG, ST>), grid, dim3(WM * WN * 64), 0, st, x,
                      dy, g.atomic ? dw : ws, g);
   if (g.atomic) return;
   constexpr int BM = 64 * MB, BN = TG * 64;
@@ -574,13 +583,13 @@ template <int W>
 static int64_t halo_dispatch_w(const bf16* x, const bf16* dy, float* dw, float* ws, HaloGeom& g,
                                hipStream_t st, bool plan_only) {
   switch (halo_select(g)) {
-#define PCA_CASE(C, MB, WM, WN, KP, TG)                                \
-    case C:                                                            \
-      if constexpr (halo_fits<W, MB, KP>()) {                          \
-        if (plan_only) return halo_plan<W, MB, WM, WN, KP, TG>(g);     \
-        launch_halo<W, MB, WM, WN, KP, TG>(x, dy, dw, ws, g, st);      \
-        return 0;                                                      \
-      }                                                                \
+#define PCA_CASE(C, MB, WM, WN, KP, TG, ST)                              \
+    case C:                                                              \
+      if constexpr (halo_fits<W, MB, KP, ST>()) {                        \
+        if (plan_only) return halo_plan<W, MB, WM, WN, KP, TG, ST>(g);   \
+        launch_halo<W, MB, WM, WN, KP, TG, ST>(x, dy, dw, ws, g, st);    \
+        return 0;                                                        \
+      }                                                                  \
       break;
     PCA_HALO_CFGS(PCA_CASE)
 #undef PCA_CASE
@@ -588,8 +597,8 @@ static int64_t halo_dispatch_w(const bf16* x, const bf16* dy, float* dw, float* 
       break;
   }
   // (a configuration whose LDS stages do not fit this image width falls back to cfg 0)
-  if (plan_only) return halo_plan<W, 1, 1, 4, 32, 9>(g);
-  launch_halo<W, 1, 1, 4, 32, 9>(x, dy, dw, ws, g, st);
+  if (plan_only) return halo_plan<W, 1, 1, 4, 32, 9, 3>(g);
+  launch_halo<W, 1, 1, 4, 32, 9, 3>(x, dy, dw, ws, g, st);
   return 0;
 }
 

@@ -2280,7 +2280,13 @@ std::vector<std::pair<int, int>> wgrad_tune_candidates(int N, int H, int W, int 
                                                        int groups) {
   std::vector<int> cfgs;
   const bool halo = wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) >= 0;
+  // (42-46: the 4-6 stage halo configs; PCA_HALO_DEEP=0 leaves them out of the search)
+  static const bool deep = [] {
+    const char* e = getenv("PCA_HALO_DEEP");
+    return !(e && e[0] == '0');
+  }();
   if (halo) cfgs.insert(cfgs.end(), {32, 33, 34, 35, 36, 37, 38, 39, 40, 41});
+  if (halo && deep) cfgs.insert(cfgs.end(), {42, 43, 44, 45, 46});
   const int cin_g = Cin / groups, cout_g = Cout / groups;
   if (cin_g % 64 == 0 && cout_g % 64 == 0) cfgs.insert(cfgs.end(), {16, 17, 18, 19, 20, 21});
   cfgs.insert(cfgs.end(), {0, 1, 2, 3, 6, 7});

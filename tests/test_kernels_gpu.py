@@ -241,7 +241,7 @@ def test_wgrad_autotune_candidates(C, case):
     assert not bad, bad
 
 
-WGRAD_CFGS = list(range(8)) + list(range(16, 22)) + list(range(32, 42))   # 39-41: one kernel row (3 taps) per halo tile
+WGRAD_CFGS = list(range(8)) + list(range(16, 22)) + list(range(32, 47))   # 39-41: one kernel row (3 taps) per halo tile; 42-46: 4-6 LDS stages
 
 
 @pytest.mark.parametrize("case", [(3, 64, 16, 64, 3, 1, 1, 1), (2, 128, 8, 256, 3, 2, 1, 1),
