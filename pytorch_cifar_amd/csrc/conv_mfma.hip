@@ -1577,8 +1577,15 @@ static int igemm_ksplit_t(const ConvGeom& g) {
 }
 
 static int splitk_reduce_grid(int M, int Co, int* rows_per_block) {
+  // every block adds its BN sums into the R shard rows of the accumulator at the end: the grid
+  // cap also bounds those same-address atomics (PCA_SPLITK_RED_CAP blocks; default 2 per CU)
+  static const int cap = [] {
+    const char* e = getenv("PCA_SPLITK_RED_CAP");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 0;
+  }();
   const int RP = 256 / (Co / 8);
-  int gx = std::min(cdiv(M, RP), 2 * num_cus());
+  int gx = std::min(cdiv(M, RP), cap > 0 ? cap : 2 * num_cus());
   const int rpb = cdiv(M, gx);
   *rows_per_block = rpb;
   return cdiv(M, rpb);

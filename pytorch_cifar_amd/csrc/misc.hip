@@ -2091,9 +2091,78 @@ __global__ __launch_bounds__(256) void chan_remap_kernel(const T* __restrict__ i
   }
 }
 
+// Row-staged form for activations (no row map): a block loads RB whole input rows into LDS with
+// 16-byte (or the widest dividing) loads, then writes RB output rows gathering from LDS — every
+// global access coalesced and vectorized (the per-element gather above issues V scalar loads
+// per output vector: slower than a stock pad on DPN / RegNet's padded groups).
+template <typename T, int VIN, int V>
+__global__ __launch_bounds__(256) void chan_remap_rows_kernel(const T* __restrict__ in,
+                                                              T* __restrict__ out,
+                                                              const int* __restrict__ cmap, int Q,
+                                                              int Cin, int J, int RB) {
+  extern __shared__ __attribute__((aligned(16))) char rsm[];
+  int* smap = reinterpret_cast<int*>(rsm);
+  T* rows = reinterpret_cast<T*>(rsm + ((J * (int)sizeof(int) + 15) & ~15));
+  for (int j = threadIdx.x; j < J; j += blockDim.x) smap[j] = cmap[j];
+  struct alignas(sizeof(T) * VIN) VecI { T v[VIN]; };
+  struct alignas(sizeof(T) * V) VecO { T v[V]; };
+  const int ci = Cin / VIN, jo = J / V;
+  for (int r0 = blockIdx.x * RB; r0 < Q; r0 += gridDim.x * RB) {
+    const int nr = min(RB, Q - r0);
+    __syncthreads();   // (map staged / previous rows consumed)
+    const VecI* src = reinterpret_cast<const VecI*>(in + (int64_t)r0 * Cin);
+    VecI* dst = reinterpret_cast<VecI*>(rows);
+    for (int i = threadIdx.x; i < nr * ci; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    VecO* o = reinterpret_cast<VecO*>(out + (int64_t)r0 * J);
+    for (int i = threadIdx.x; i < nr * jo; i += blockDim.x) {
+      const int r = i / jo, gi = i - r * jo;
+      VecO v;
+#pragma unroll
+      for (int u = 0; u < V; ++u) {
+        const int c = smap[gi * V + u];
+        v.v[u] = c >= 0 ? rows[r * Cin + c] : T(0.f);
+      }
+      o[i] = v;
+    }
+  }
+}
+
+template <typename T>
+static bool chan_remap_rows(const T* in, T* out, const int* cmap, int Q, int Cin, int J,
+                            hipStream_t st) {
+  constexpr int VMAX = 16 / sizeof(T);
+  int vin = VMAX, v = VMAX;
+  while (vin > 1 && (Cin % vin)) vin >>= 1;
+  while (v > 1 && (J % v)) v >>= 1;
+  const size_t map_bytes = ((size_t)J * sizeof(int) + 15) & ~(size_t)15;
+  const size_t row_bytes = (size_t)Cin * sizeof(T);
+  if (map_bytes + row_bytes > 48 * 1024) return false;
+  int RB = (int)((48 * 1024 - map_bytes) / row_bytes);
+  RB = std::max(1, std::min(RB, 64));
+  const size_t lds = map_bytes + (size_t)RB * row_bytes;
+  const int blocks = (int)std::min<int64_t>(cdiv64(Q, RB), 4096);
+#define PCA_RR(VI, VO)                                                                       \
+  if (vin == VI && v == VO) {                                                                \
+    hipLaunchKernelGGL((chan_remap_rows_kernel<T, VI, VO>), dim3(blocks), dim3(256), lds, st, \
+                       in, out, cmap, Q, Cin, J, RB);                                        \
+    return true;                                                                             \
+  }
+  if constexpr (VMAX == 8) {
+    PCA_RR(8, 8) PCA_RR(8, 4) PCA_RR(8, 2) PCA_RR(8, 1) PCA_RR(4, 8) PCA_RR(2, 8) PCA_RR(1, 8)
+  }
+  PCA_RR(4, 4) PCA_RR(4, 2) PCA_RR(4, 1) PCA_RR(2, 4) PCA_RR(2, 2) PCA_RR(2, 1) PCA_RR(1, 4)
+  PCA_RR(1, 2) PCA_RR(1, 1)
+#undef PCA_RR
+  return false;
+}
+
 template <typename T, bool ACC>
 static void chan_remap_dispatch(const T* in, T* out, const int* cmap, const int* rmap, int Q, int K,
                                 int Cin, int J, hipStream_t st) {
+  if constexpr (!ACC) {
+    if (!rmap && chan_remap_rows<T>(in, out, cmap, Q, Cin, J, st)) return;
+  }
   constexpr int VMAX = 16 / sizeof(T);
   int V = VMAX;
   while (V > 1 && (J % V)) V >>= 1;
