@@ -729,7 +729,7 @@ class _ConvDepthwise(torch.autograd.Function):
         ctx.bnsrc = None
         if ctx.needs_input_grad[0]:
             H, W, Cx = x.shape[1], x.shape[2], x.shape[3]
-            if src is not None and src.acc is not None:
+            if src is not None and src.acc is not None and src.y2 is None:   # (no dual-BN sums)
                 src.acc.begin()
                 dx, ok = C.dw_dgrad_bn(dy, wT, H, W, Cx, KH, KW, stride, padding, src.y, src.mask,
                                        src.aux, src.act, src.acc.buf, src.acc.R)
