@@ -1,7 +1,7 @@
 """Host-side AddressSanitizer + UBSan run of the kernel library's launch planners (SURVEY §5:
 race / fault detection; the reference has none). GPU ASan and XNACK runs are not available on the
 MI355X pool, so the host logic that sizes workspaces, BatchNorm slab rows and persistent grids,
-and the autotuner's candidate lists, is built with -fsanitize=address,undefined (host side only)
+and the autotuner's candidate lists, is built with the address + undefined-behaviour sanitizers (host side only)
 and driven over the zoo's conv census at batch 1-1024 and every tuning candidate
 (tools/sanitize/host_plan_check.cpp). CPU only; takes ~3 minutes (the kernels' device code is
 compiled too). PCA_SKIP_SANITIZE=1 skips it."""

@@ -18,6 +18,6 @@ done
 wait
 $HIPCC -x hip --offload-arch=gfx950 -O1 -g -std=c++17 -Xarch_host -fsanitize=address \
   -Xarch_host -fsanitize=undefined -I"$CSRC" -c "$ROOT/tools/sanitize/host_plan_check.cpp" -o "$OUT/main.o"
-$HIPCC -fsanitize=address -fsanitize=undefined "$OUT/main.o" "${objs[@]}" -o "$OUT/host_plan_check" \
+$HIPCC -fno-gpu-sanitize -fsanitize=address -fsanitize=undefined "$OUT/main.o" "${objs[@]}" -o "$OUT/host_plan_check" \
   -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 ASAN_OPTIONS=detect_leaks=0:abort_on_error=0 UBSAN_OPTIONS=print_stacktrace=1 "$OUT/host_plan_check"
