@@ -77,11 +77,13 @@ def _apply_runtime_flags(args, loaders):
             ld.fp32 = True
 
 def _data_parallel_ranks(args):
+    # torch.cuda.device_count() alone (amdsmi on ROCm) decides: torch.cuda.is_available() would
+    # start the HIP runtime in this launcher parent, which must stay off the GPU
     if args.nproc:
         return args.nproc
-    if args.cpu or not torch.cuda.is_available():
+    if args.cpu:
         return 1
-    return torch.cuda.device_count()
+    return max(1, torch.cuda.device_count())
 
 
 def main(argv=None):

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -256,6 +257,15 @@ static float time_launches(F&& f, hipStream_t st, int reps) {
   return ms / reps;
 }
 
+// PCA_TUNE_LOG=1: print every autotune trial (tools/gpu sweeps read it from stderr)
+static bool tune_log() {
+  static const bool on = [] {
+    const char* e = std::getenv("PCA_TUNE_LOG");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // time every candidate (cfg, split) of a conv geometry and record the fastest. `run` launches
 // the conv once with the trial selection active, allocating its own scratch outputs.
 template <class F>
@@ -284,6 +294,10 @@ static void autotune_conv(int kind, int N, int H, int W, int Cin, int Cout, int 
   for (const auto& c : cands) {
     pca::conv_set_trial(c.first, c.second);
     const float t = time_launches(run, st, 3);
+    if (tune_log())
+      fprintf(stderr, "[tune] %s N=%d H=%d W=%d Cin=%d Cout=%d k=%dx%d s=%d g=%d bnfuse=%d cfg=%d split=%d %.1f us\n",
+              kind == 0 ? "fwd" : "dgrad", N, H, W, Cin, Cout, KH, KW, stride, groups, (int)need_bn_fuse,
+              c.first, c.second, t * 1e3f);
     if (t < best) {
       best = t;
       pick = c;
@@ -519,6 +533,9 @@ Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride,
                                n > 0 ? ptr<float>(wst) : nullptr, N, H, W, Cin, Cout, KH, KW,
                                stride, pad, groups, Ho, Wo, cur_stream());
       }, cur_stream(), 3);
+      if (tune_log())
+        fprintf(stderr, "[tune] wgrad N=%d H=%d W=%d Cin=%d Cout=%d k=%dx%d s=%d g=%d cfg=%d split=%d %.1f us\n",
+                N, H, W, Cin, Cout, KH, KW, stride, groups, c.first, c.second, t * 1e3f);
       if (t < best) {
         best = t;
         pick = c;

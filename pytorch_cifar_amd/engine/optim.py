@@ -37,7 +37,9 @@ class SGD(torch.optim.Optimizer):
         self._tables = {}
         self.capturing = False
         # arena step only: clear each gradient after reading it (the trainer then skips the next
-        # zero_grad fill); _zeroed_grads reports whether the last step did
+        # zero_grad fill); _zeroed_grads reports whether the last step did. While this is set,
+        # step() leaves every arena .grad reading ZERO (gradient-norm logging or hooks must read
+        # the gradients before step()); a TrainStep sets it for its lifetime and close() restores it.
         self.zero_grad_in_step = False
         self._zeroed_grads = False
 

@@ -27,7 +27,8 @@ class NonFiniteLossError(FloatingPointError):
 
 
 class TrainStep:
-    def __init__(self, net, optimizer, loader, batch_size, ddp=None, graph=False, metrics=None):
+    def __init__(self, net, optimizer, loader, batch_size, ddp=None, graph=False, metrics=None,
+                 clear_grads_in_step=None):
         self.net = net
         self.opt = optimizer
         self.loader = loader
@@ -42,9 +43,15 @@ class TrainStep:
                     and os.environ.get("PCA_FUSED_SGD_PREP", "1") != "0":
                 optimizer.attach_weight_prep(inner.__dict__["_pca_wplan"])
         # the arena step clears the gradients it consumed, so the next step needs no zero_grad
-        # fill (one launch and a full gradient-arena write per step)
+        # fill (one launch and a full gradient-arena write per step). This changes what the
+        # optimizer's step() does to .grad (it reads zero afterwards), so it is an explicit
+        # opt-in of this TrainStep: ``clear_grads_in_step`` (default on, PCA_SGD_ZERO_GRAD=0 off),
+        # and close() puts the optimizer's previous setting back.
+        self._prev_zero_in_step = getattr(optimizer, "zero_grad_in_step", None)
+        if clear_grads_in_step is None:
+            clear_grads_in_step = os.environ.get("PCA_SGD_ZERO_GRAD", "1") != "0"
         if getattr(optimizer, "arena", None) is not None and hasattr(optimizer, "zero_grad_in_step") \
-                and os.environ.get("PCA_SGD_ZERO_GRAD", "1") != "0":
+                and clear_grads_in_step:
             optimizer.zero_grad_in_step = True
         self._grads_clean = False
         self.ddp = ddp
@@ -55,6 +62,12 @@ class TrainStep:
         self.static_idx = torch.zeros(batch_size, dtype=torch.int64, device=self.device)
         self.last_loss = None
         self.graph_error = None
+
+    def close(self):
+        """Give the optimizer back its own gradient semantics (step() leaves .grad as computed)."""
+        if self._prev_zero_in_step is not None:
+            self.opt.zero_grad_in_step = self._prev_zero_in_step
+        self._grads_clean = False
 
     # one eager step on a given index batch
     def _body(self, idx):
@@ -135,6 +148,16 @@ class TrainStep:
             if first is not None:
                 self.opt._arena_first = first
 
+        def born_in_warmup():
+            # state created by the warm-ups themselves (the dropout Philox states appear on the
+            # first training forward): roll it back to its creation value {seed, step 0, tickets 0}
+            from ..ops.functional import rng_states
+
+            with torch.no_grad():
+                for r in rng_states(getattr(self.net, "module", self.net)):
+                    if id(r) not in known:
+                        r[1:].zero_()
+
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -145,8 +168,10 @@ class TrainStep:
         except BaseException:
             torch.cuda.current_stream().wait_stream(s)
             restore()
+            born_in_warmup()
             raise
         restore()
+        born_in_warmup()
         self._fresh_operands()   # (the restore rewrote the masters: the capture sees current operands)
         # If this is the run's first step, the restored momenta are zero and the captured
         # steady-state rule buf = 0.9 * buf + d equals the first-step rule buf = d (dampening 0),

@@ -16,10 +16,11 @@ def swish(x):
     return F.swish(x)
 
 
-def drop_connect(x, drop_ratio):
+def drop_connect(x, drop_ratio, owner=None):
     """Per-sample drop-connect (efficientnet.py:16-22): native Philox keep byte per sample on the
-    GPU (ops/functional.py drop_connect), Bernoulli mask on the CPU reference path."""
-    return F.drop_connect(x, drop_ratio)
+    GPU (ops/functional.py drop_connect), Bernoulli mask on the CPU reference path. ``owner``
+    (the block) holds the Philox state, so the trainer's state snapshot sees it."""
+    return F.drop_connect(x, drop_ratio, owner=owner)
 
 
 class SE(tnn.Module):
@@ -61,7 +62,7 @@ class Block(tnn.Module):
         y = self.conv3(out)
         if self.has_skip:
             if self.training and self.drop_rate > 0:
-                return F.add_act(drop_connect(self.bn3(y), self.drop_rate), x)
+                return F.add_act(drop_connect(self.bn3(y), self.drop_rate, owner=self), x)
             return self.bn3(y, residual=x)
         return self.bn3(y)
 

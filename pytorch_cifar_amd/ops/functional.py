@@ -1346,11 +1346,22 @@ def rng_state(owner, device):
 _RNG_SEQ = [0]
 
 
+class _OrphanRng:
+    """Holder of the Philox states of dropout / drop-connect calls made without an owner module
+    (one process-wide object: those calls share it, and :func:`rng_states` always reports it, so
+    a training-step snapshot covers them too)."""
+
+
+_ORPHAN_RNG = _OrphanRng()
+
+
 def rng_states(model):
-    """Every dropout rng state tensor attached to ``model``'s modules (training-step state)."""
+    """Every dropout rng state tensor attached to ``model``'s modules (training-step state), plus
+    the owner-less calls' states."""
     out = []
     for m in model.modules():
         out += list(m.__dict__.get("_pca_rng", {}).values())
+    out += list(_ORPHAN_RNG.__dict__.get("_pca_rng", {}).values())
     return out
 
 
@@ -1615,7 +1626,7 @@ def dropout(x, p, training, owner=None):
         return x
     if _ref(x):
         return F.dropout(x, p=p, training=True)
-    return _dropout_units(x, 1, p, owner if owner is not None else _dropout_units)
+    return _dropout_units(x, 1, p, owner if owner is not None else _ORPHAN_RNG)
 
 
 def drop_connect(x, drop_ratio, owner=None):
@@ -1627,7 +1638,7 @@ def drop_connect(x, drop_ratio, owner=None):
         keep = 1.0 - drop_ratio
         mask = torch.empty([x.shape[0], 1, 1, 1], dtype=x.dtype, device=x.device).bernoulli_(keep)
         return x / keep * mask
-    return _dropout_units(x, x[0].numel(), drop_ratio, owner if owner is not None else drop_connect)
+    return _dropout_units(x, x[0].numel(), drop_ratio, owner if owner is not None else _ORPHAN_RNG)
 
 
 class Remap:
