@@ -37,10 +37,11 @@ def parse():
     ap.add_argument("--model", default="ResNet18")
     ap.add_argument("--batch", type=int, default=1024, help="global batch")
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (1/0)")
-    # 4 MiB buckets (not DDP's 25): on xGMI the all-reduce of a bucket only overlaps backward if
-    # the bucket closes early; with 25 MiB, ResNet-18's last bucket holds ~18 MiB that can only
-    # start after the stem's wgrad, fully exposed. 4 MiB keeps the exposed tail to layers 1-2.
+    # 4 MiB buckets (not DDP's 25): only the last bucket's all-reduce is exposed after the
+    # backward; arithmetic in parallel/ddp.py (25 MiB: ~11 MB exposed, 4 MiB: ~4 MB)
     ap.add_argument("--bucket-mb", type=float, default=4.0)
+    ap.add_argument("--grad-compress", default="none", choices=["none", "bf16", "bf16_tail"],
+                    help="opt-in bf16 gradient all-reduce (off: exact fp32 DDP semantics)")
     ap.add_argument("--baseline", action="store_true",
                     help="run the stock PyTorch-ROCm comparator step instead (MIOpen/hipBLASLt, autocast bf16)")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -71,7 +72,8 @@ def main():
     from pytorch_cifar_amd.engine.trainer import build_bench_step
 
     step, meta = build_bench_step(args.model, per_rank, device, ctx, graph=bool(args.graph),
-                                  baseline=args.baseline, bucket_mb=args.bucket_mb)
+                                  baseline=args.baseline, bucket_mb=args.bucket_mb,
+                                  grad_compress=args.grad_compress)
 
     # (CPU runs — the gloo contract test in tests/test_cli_cpu.py — have nothing to synchronize)
     sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)

@@ -62,6 +62,8 @@ parser.add_argument('--graph', default=1, type=int)
 parser.add_argument('--max_steps', default=None, type=int)
 parser.add_argument('--bucket_mb', default=4.0, type=float,
                     help='gradient all-reduce bucket size (MiB); small buckets overlap backward on xGMI')
+parser.add_argument('--grad_compress', default='none', choices=['none', 'bf16', 'bf16_tail'],
+                    help='opt-in bf16 gradient all-reduce (every bucket, or only the exposed last one)')
 parser.add_argument('--log_every', default=20, type=int)
 parser.add_argument('--no_broadcast_buffers', action='store_true')
 parser.add_argument('--cpu', action='store_true', help='gloo/CPU ranks (tests)')
@@ -161,7 +163,8 @@ def main_worker(ctx, args):
     if ctx.world > 1:
         arena = ParamArena(model.parameters())
         ddp = DistributedDataParallel(model, ctx, bucket_cap_mb=args.bucket_mb, arena=arena,
-                                      broadcast_buffers=not args.no_broadcast_buffers)
+                                      broadcast_buffers=not args.no_broadcast_buffers,
+                                      grad_compress=args.grad_compress)
         net = ddp
     else:
         if device.type == 'cuda':

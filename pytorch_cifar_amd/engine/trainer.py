@@ -229,7 +229,7 @@ def read_metrics(metrics: torch.Tensor, reset: bool = True):
 
 
 def build_bench_step(model_name, per_rank_batch, device, ctx, graph=True, baseline=False,
-                     bucket_mb=25.0, n_images=50000):
+                     bucket_mb=25.0, n_images=50000, grad_compress=None):
     """Closure running one timed training step of the headline benchmark + metadata."""
     from ..data.loader import DeviceLoader
     from ..data.synthetic import synthetic_cifar10
@@ -253,7 +253,8 @@ def build_bench_step(model_name, per_rank_batch, device, ctx, graph=True, baseli
     if ctx.world > 1:
         from ..parallel.ddp import DistributedDataParallel
 
-        ddp = DistributedDataParallel(model, ctx, bucket_cap_mb=bucket_mb, arena=arena)
+        ddp = DistributedDataParallel(model, ctx, bucket_cap_mb=bucket_mb, arena=arena,
+                                      grad_compress=grad_compress)
         net = ddp
     loader = DeviceLoader(images, labels, per_rank_batch, device, train=True, crop_pad=4, flip=True,
                           world=ctx.world, rank=ctx.rank, seed=0, drop_last=True)

@@ -25,9 +25,28 @@ Re-implements what main_dist.py:140-144 gets from ``torch.nn.parallel.Distribute
   copies between a step's forward and the next forward differ (they already hold rank 0's);
 * the initial rank-0 parameters and buffers are broadcast at construction (C3).
 
-xGMI is point-to-point (7 links/GPU); RCCL's ring/tree channels stripe a large message over the
-links, so a few large buckets beat many small ones: 25 MiB default buckets keep ResNet-18 (44.7 MB
-of fp32 grads) at two or three collectives per step.
+Bucket size on xGMI (why the launchers default to 4 MiB, not DDP's 25). xGMI is point-to-point
+(7 links per GPU, ~150 GB/s each way per link); an 8-rank ring all-reduce of S bytes moves
+2(N-1)/N * S = 1.75 S through every GPU. At the 8-GPU shard (bs128 per rank) ResNet-18's backward
+is ~1.2 ms and produces its 44.7 MB of fp32 gradients back to front: layer 4 (33.6 MB) in the first
+~0.35 ms, layers 3-1 and the stem (11.1 MB) in the remaining ~0.85 ms. What the step cannot hide is
+the all-reduce of the LAST bucket, which only starts after the stem's weight gradient:
+  * 25 MiB buckets: the last bucket holds layers 1-3 (~11 MB) -> 1.75 * 11 MB / ~150 GB/s (one
+    ring's per-link rate; more channels only help until the per-message latency dominates) ~ 130 us
+    exposed per step (7 % of a 1.88 ms step);
+  * 4 MiB buckets: the last bucket is ~4 MB -> ~47 us exposed, and the earlier buckets (each
+    ~20-30 us of RCCL launch/latency) still finish under the backward (11 collectives in ~1 ms of
+    backward leave the link idle >70 % of the time);
+  * 1 MiB buckets: ~45 collectives per step; their fixed per-call cost (~20 us) adds up to most of
+    the backward, so the pipeline no longer drains behind the last gradient.
+Hence ``bucket_cap_mb`` defaults to DDP's 25 MiB in this class (API parity) and to 4 MiB in
+bench.py / main_dist.py (``--bucket_mb``). The first bucket is capped at 1 MiB like DDP.
+
+``grad_compress`` (opt-in, off by default = exact DDP semantics): "bf16" all-reduces every bucket
+as bf16 (compressed into a persistent bf16 copy on the communication stream, decompressed into the
+fp32 arena after the collective: half the link bytes, the sum rounded to bf16 — what torch's
+``bf16_compress_hook`` does); "bf16_tail" compresses only the last bucket, the one whose all-reduce
+is exposed after the backward (see above).
 
 The communicator is the native :class:`RcclComm` on GPU ranks; a torch.distributed fallback
 (gloo) runs the same logic in the CPU multi-process tests.
@@ -56,21 +75,26 @@ class _TorchDistComm:
 
 
 class Bucket:
-    __slots__ = ("index", "start", "end", "params", "pending", "launched", "view")
+    __slots__ = ("index", "start", "end", "params", "pending", "launched", "view", "low")
 
     def __init__(self, index, start, end, params, flat):
         self.index, self.start, self.end, self.params = index, start, end, params
         self.view = flat[start:end]
         self.pending = len(params)
         self.launched = False
+        self.low = None       # persistent bf16 copy (grad_compress)
 
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, ctx, bucket_cap_mb: float = 25.0,
                  first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  find_unused_parameters: bool = True, arena: ParamArena | None = None,
-                 force_collectives: bool = False, overlap_buffer_broadcast: bool = True):
+                 force_collectives: bool = False, overlap_buffer_broadcast: bool = True,
+                 grad_compress: str | None = None):
         super().__init__()
+        if grad_compress not in (None, "none", "bf16", "bf16_tail"):
+            raise ValueError(f"grad_compress must be None, 'bf16' or 'bf16_tail', not {grad_compress!r}")
+        self.grad_compress = None if grad_compress == "none" else grad_compress
         self.module = module
         self.ctx = ctx
         self.world = ctx.world
@@ -128,6 +152,9 @@ class DistributedDataParallel(nn.Module):
             self.buckets[0].start = 0
             self.buckets[0].view = flat[0: self.buckets[0].end]
         self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
+        for b in self.buckets:
+            if self.grad_compress == "bf16" or (self.grad_compress == "bf16_tail" and b is self.buckets[-1]):
+                b.low = torch.empty(b.end - b.start, dtype=torch.bfloat16, device=flat.device)
 
     def bucket_sizes_mib(self):
         return [round((b.end - b.start) * 4 / 2 ** 20, 3) for b in self.buckets]
@@ -224,7 +251,13 @@ class DistributedDataParallel(nn.Module):
             return
         self._fork()
         with self._stream_ctx():
-            self.comm.all_reduce(b.view, "avg", self._sid())
+            if b.low is not None:
+                # compressed bucket: bf16 over the links, fp32 back into the arena (comm stream)
+                b.low.copy_(b.view)
+                self.comm.all_reduce(b.low, "avg", self._sid())
+                b.view.copy_(b.low)
+            else:
+                self.comm.all_reduce(b.view, "avg", self._sid())
 
     def _finish_pass(self):
         unused = []

@@ -158,3 +158,70 @@ def test_shard_sampler_matches_torch_distributed_sampler():
                 a.set_epoch(epoch)
                 b.set_epoch(epoch)
                 assert a.indices().tolist() == list(iter(b))
+
+
+def _train_steps(ctx, compress=None, steps=5):
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.engine.optim import SGD
+    from pytorch_cifar_amd.ops.functional import cross_entropy
+    from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(100 + ctx.rank)   # rank 0's initial state must win (C3)
+    model = models.LeNet()
+    ddp = DistributedDataParallel(model, ctx, bucket_cap_mb=0.01, first_bucket_mb=0.01,
+                                  grad_compress=compress)
+    opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    g = torch.Generator().manual_seed(11)
+    init = {n: p.detach().clone() for n, p in model.named_parameters()}
+    batches = []
+    for _ in range(steps):
+        x = torch.randn(8, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (8,), generator=g)
+        batches.append((x, y))
+        opt.zero_grad()
+        cross_entropy(ddp(x[ctx.rank * 4:(ctx.rank + 1) * 4]), y[ctx.rank * 4:(ctx.rank + 1) * 4]).backward()
+        opt.step()
+    return {"init": init, "params": {n: p.detach().clone() for n, p in model.named_parameters()},
+            "batches": batches}
+
+
+def _train_steps_bf16(ctx):
+    return _train_steps(ctx, compress="bf16")
+
+
+def test_ddp_steps_bitwise_equal_across_ranks_and_match_single_process():
+    """N optimizer steps of 2-rank DDP (LeNet, no BatchNorm): both ranks hold bitwise-identical
+    parameters (every rank applies the same averaged gradient), and they match one process
+    training on the concatenated batch (reference main_dist.py:140-144 DDP semantics)."""
+    r0, r1 = run_ranks(_train_steps)
+    for n in r0["params"]:
+        assert torch.equal(r0["params"][n], r1["params"][n]), n
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.engine.optim import SGD
+    from pytorch_cifar_amd.ops.functional import cross_entropy
+
+    m = models.LeNet()
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            p.copy_(r0["init"][n])
+    opt = SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    for x, y in r0["batches"]:
+        opt.zero_grad()
+        cross_entropy(m(x), y).backward()
+        opt.step()
+    for n, p in m.named_parameters():
+        torch.testing.assert_close(r0["params"][n], p.detach(), rtol=2e-5, atol=1e-6)
+
+
+def test_ddp_bf16_compressed_buckets():
+    """Opt-in bf16 bucket all-reduce: ranks stay bitwise identical, and the trajectory stays within
+    bf16 rounding of the exact fp32 one."""
+    c0, c1 = run_ranks(_train_steps_bf16)
+    e0, _ = run_ranks(_train_steps)
+    ds = []
+    for n in c0["params"]:
+        assert torch.equal(c0["params"][n], c1["params"][n]), n
+        d = ((c0["params"][n] - e0["params"][n]).norm() / e0["params"][n].norm()).item()
+        assert d < 1e-2, (n, d)
+        ds.append(d)
+    assert max(ds) > 0, "the bf16 path was not taken"
