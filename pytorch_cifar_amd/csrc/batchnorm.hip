@@ -20,6 +20,9 @@ namespace pca {
 static int g_stat_shards = 0;
 int stat_shards() { return g_stat_shards; }
 void set_stat_shards(int shards) { g_stat_shards = shards; }
+static const float* g_stat_shift = nullptr;
+const float* stat_shift() { return g_stat_shift; }
+void set_stat_shift(const float* k) { g_stat_shift = k; }
 
 // Row-parallel geometry for an [M][C] NHWC matrix: TPR threads cover a row's granules
 // (VEC channels each), RPP rows are processed per pass by one 256-thread block.
@@ -71,28 +74,36 @@ __device__ __forceinline__ void store_vec(bf16* p, const float* f) {
 }
 
 // ---- per-channel sum / sumsq partials of a bare tensor: partial[P][2][C] ----
+// centered (krow != nullptr): sums of x - K with K[c] = x[0][c] (the first row: a value within a
+// few standard deviations of the channel mean, the same for every block), K published in krow
+// for the finalize / fold (robust variance, see common.h stat_shift)
 template <int VEC>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ x, int M,
                                                        RowPar rp, int rows_per_block,
-                                                       float* __restrict__ partial, int shards) {
+                                                       float* __restrict__ partial, int shards,
+                                                       float* __restrict__ krow) {
   __shared__ float red[256 * VEC * 2];
   const int t = threadIdx.x;
   const int gx = t % rp.TPR, ry = t / rp.TPR;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
+  if (krow && blockIdx.x == 0)
+    for (int c = t; c < rp.C; c += 256) krow[c] = bf2f(x[c]);
   for (int gbase = 0; gbase < rp.G; gbase += rp.TPR) {
     const int gi = gbase + gx;
-    float s[VEC], q[VEC];
+    float s[VEC], q[VEC], k[VEC];
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) s[v] = q[v] = 0.f;
+    for (int v = 0; v < VEC; ++v) s[v] = q[v] = k[v] = 0.f;
+    if (krow && gi < rp.G) load_vec<VEC>(x + gi * VEC, k);
     if (ry < rp.RPP && gi < rp.G) {
       for (int r = r0 + ry; r < r1; r += rp.RPP) {
         float f[VEC];
         load_vec<VEC>(x + (size_t)r * rp.C + gi * VEC, f);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
-          s[v] += f[v];
-          q[v] += f[v] * f[v];
+          const float d = f[v] - k[v];
+          s[v] += d;
+          q[v] += d * d;
         }
       }
     }
@@ -166,11 +177,14 @@ void bias_grad_fold_launch(const float* stat, int R, int C, int accumulate, floa
 // ---- forward finalize: stat[R][2][C] -> aux[4][C] = {mean, invstd, scale, shift} ----
 // One 1024-thread block per 64 channels: 16 row-lanes fold the R (<= 1024) partial rows in
 // parallel (coalesced 256-byte row segments), then lane-row 0 combines them in fp64.
+// kin: the shift K[c] the producer subtracted (its K row / the pilot it read; nullptr = 0);
+// pilot_out: receives the batch mean (the next step's K; may alias kin — one thread per channel
+// reads K before writing the mean)
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     const float* __restrict__ stat, int R, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     int64_t* __restrict__ nbt, float momentum, float eps, int training, int update_running,
-    float* __restrict__ aux) {
+    float* __restrict__ aux, const float* kin, float* pilot_out) {
   __shared__ float red[16][64][2];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -194,11 +208,12 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
       ds += red[k][cl][0];
       dq += red[k][cl][1];
     }
-    const double m = ds / count;
+    const double m = ds / count;          // mean of x - K
     double v = dq / count - m * m;
     if (v < 0.0) v = 0.0;
-    mean = (float)m;
+    mean = (float)(m + (kin ? (double)kin[c] : 0.0));
     var = (float)v;
+    if (pilot_out) pilot_out[c] = mean;
     if (update_running) {
       const double unb = count > 1.0 ? v * count / (count - 1.0) : v;
       rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
@@ -705,6 +720,8 @@ struct BnFin {
   float* dbeta;
   float* zero;           // block 0 zeroes [zero, zero + zero_n) (the other pass's accumulator)
   int zero_n;
+  const float* krow;     // forward: the shift K the producers subtracted (acc K row), or nullptr
+  float* pilot;          // forward: block 0 writes the batch mean here (the next step's K)
 };
 
 // The fold of the R shard rows is spread over the block: TPC lanes (consecutive threads, a
@@ -740,10 +757,10 @@ __device__ __forceinline__ void bn_fin_forward(const BnFin& f, int C, float* sc,
     float sum[2];
     fin_fold<2>(f.acc, f.R, 2, C, c, j, tpc, c < C, sum);
     if (j != 0 || c >= C) continue;
-    const double m = (double)sum[0] / f.count;
+    const double m = (double)sum[0] / f.count;     // mean of x - K (shifted sums)
     double v = (double)sum[1] / f.count - m * m;
     if (v < 0.0) v = 0.0;
-    const float mean = (float)m;
+    const float mean = (float)(m + (f.krow ? (double)f.krow[c] : 0.0));
     const float istd = rsqrtf((float)v + f.eps);
     const float gm = f.gamma ? f.gamma[c] : 1.f;
     const float bt = f.beta ? f.beta[c] : 0.f;
@@ -754,6 +771,7 @@ __device__ __forceinline__ void bn_fin_forward(const BnFin& f, int C, float* sc,
       f.aux[C + c] = istd;
       f.aux[2 * C + c] = gm * istd;
       f.aux[3 * C + c] = bt - mean * gm * istd;
+      if (f.pilot) f.pilot[c] = mean;   // (the other blocks read K from the K row, not here)
       if (f.rmean) {
         const double unb = f.count > 1.f ? v * f.count / (f.count - 1.0) : v;
         f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * mean;
@@ -865,13 +883,14 @@ int bn_row_blocks(int M, int C) {
   return P;
 }
 
-void bn_stats_launch(const bf16* x, int M, int C, float* partial, int P, hipStream_t st) {
+void bn_stats_launch(const bf16* x, int M, int C, float* partial, int P, hipStream_t st,
+                     float* krow) {
   const int rows = cdiv(M, P);
   switch (bn_vec(C)) {
 #define PCA_STATS(V)                                                                              \
   case V: {                                                                                       \
     RowPar rp = make_rowpar(C, V);                                                                \
-    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial, g_stat_shards); \
+    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial, g_stat_shards, krow); \
     break;                                                                                        \
   }
     PCA_STATS(8) PCA_STATS(4) PCA_STATS(2) PCA_STATS(1)
@@ -892,9 +911,10 @@ int colsum_launch(const float* in, int R, int L, float* out, hipStream_t st) {
 void bn_finalize_launch(const float* stat, int R, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, int64_t* nbt,
                         float momentum, float eps, int training, int update_running, float* aux,
-                        hipStream_t st) {
+                        hipStream_t st, const float* kin, float* pilot_out) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C, count,
-                     gamma, beta, rmean, rvar, nbt, momentum, eps, training, update_running, aux);
+                     gamma, beta, rmean, rvar, nbt, momentum, eps, training, update_running, aux,
+                     kin, pilot_out);
 }
 
 void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const bf16* res,
@@ -1024,14 +1044,17 @@ bool bn_apply_acc_launch(const bf16* y, int C, int M, float count, float* acc, i
                          const float* gamma2, const float* beta2, float* rmean2, float* rvar2,
                          int64_t* nbt2, float momentum2, float eps2, float* aux2, const bf16* res,
                          const bf16* y2, int act, bf16* out, uint8_t* mask, float* zero,
-                         int zero_n, hipStream_t st) {
+                         int zero_n, hipStream_t st, bool shifted, float* pilot, bool shifted2,
+                         float* pilot2) {
   if (!(rows_enabled() && C % 8 == 0 && C <= 2048 &&
         (act == ACT_RELU || act == ACT_NONE || (act == ACT_SWISH && !res && !y2)) && !(res && y2)))
     return false;
+  // K rows of shifted accumulators follow their [R][2][C] sums
   BnFin f{acc, R, count, gamma, beta, rmean, rvar, nbt, momentum, eps, aux, nullptr, nullptr, nullptr,
-          zero, zero_n};
+          zero, zero_n, shifted ? acc + (size_t)R * 2 * C : nullptr, pilot};
   BnFin f2{acc2, R2, count, gamma2, beta2, rmean2, rvar2, nbt2, momentum2, eps2, aux2, nullptr,
-           nullptr, nullptr, nullptr, 0};
+           nullptr, nullptr, nullptr, 0, (shifted2 && acc2) ? acc2 + (size_t)R2 * 2 * C : nullptr,
+           pilot2};
   const dim3 gr(acc_rows_grid(M, C)), bl(256);
   const size_t lds = (size_t)(y2 ? 4 : 2) * C * sizeof(float);
 #define PCA_APPLY(R_, D, A) \

@@ -65,11 +65,12 @@ int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int
                              int pad, int groups, int Ho, int Wo);
 // batchnorm.hip
 int bn_row_blocks(int M, int C);
-void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t);
+void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t, float* krow = nullptr);
 int colsum_launch(const float*, int, int, float*, hipStream_t);
 void bias_grad_fold_launch(const float*, int, int, int, float*, hipStream_t);
 void bn_finalize_launch(const float*, int, int, double, const float*, const float*, float*, float*,
-                        int64_t*, float, float, int, int, float*, hipStream_t);
+                        int64_t*, float, float, int, int, float*, hipStream_t,
+                        const float* kin = nullptr, float* pilot_out = nullptr);
 void bn_apply_launch(const bf16*, const float*, int, size_t, const bf16*, const bf16*,
                      const float*, int, bf16*, uint8_t*, hipStream_t);
 void bn_bwd_reduce_launch(const bf16*, const bf16*, const uint8_t*, const bf16*, const float*,
@@ -83,13 +84,16 @@ void bn_bwd_apply_launch(const bf16*, const bf16*, const uint8_t*, const bf16*, 
                          hipStream_t);
 int stat_shards();
 void set_stat_shards(int shards);
+const float* stat_shift();
+void set_stat_shift(const float* k);
 bool bn_apply_acc_launch(const bf16* y, int C, int M, float count, float* acc, int R,
                          const float* gamma, const float* beta, float* rmean, float* rvar,
                          int64_t* nbt, float momentum, float eps, float* aux, float* acc2, int R2,
                          const float* gamma2, const float* beta2, float* rmean2, float* rvar2,
                          int64_t* nbt2, float momentum2, float eps2, float* aux2, const bf16* res,
                          const bf16* y2, int act, bf16* out, uint8_t* mask, float* zero,
-                         int zero_n, hipStream_t st);
+                         int zero_n, hipStream_t st, bool shifted = false, float* pilot = nullptr,
+                         bool shifted2 = false, float* pilot2 = nullptr);
 bool bn_bwd_apply_acc_launch(const bf16* dout, const uint8_t* mask, const bf16* y, int C, int M,
                              float count, float* acc, int R, const float* aux, const float* gamma,
                              float* dgamma, float* dbeta, const float* aux2, const float* gamma2,
@@ -321,9 +325,17 @@ void check_acc(const Tensor& acc, int R, int NS, int C) {
   TORCH_CHECK(R >= 1 && acc.numel() >= (int64_t)R * NS * C, "stat accumulator must hold R*NS*C floats");
 }
 
+// RAII: the shift K (pilot mean) the producer launches in scope subtract from their BN sums
+struct ShiftScope {
+  const float* prev;
+  explicit ShiftScope(const float* k) : prev(pca::stat_shift()) { pca::set_stat_shift(k); }
+  ~ShiftScope() { pca::set_stat_shift(prev); }
+};
+
 std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<Tensor>& bias,
                              int stride, int pad, int groups, bool want_stats,
-                             const optional<Tensor>& stat_acc, int acc_rows) {
+                             const optional<Tensor>& stat_acc, int acc_rows,
+                             const optional<Tensor>& stat_shift) {
   check_bf16(x, "x");
   check_bf16(wb, "weight");
   TORCH_CHECK(x.dim() == 4 && wb.dim() == 4, "conv_fwd expects x[N,H,W,C], w[Cout,KH,KW,Cin/G]");
@@ -365,6 +377,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
     stats = at::empty({gm, 2, Cout}, x.options().dtype(at::kFloat));
   }
   ShardScope shards(use_acc ? acc_rows : 0);
+  const bool shift = want_stats && stat_shift.has_value() && stat_shift->defined();
+  if (shift) {
+    check_f32(*stat_shift, "stat_shift");
+    TORCH_CHECK(stat_shift->numel() == Cout, "stat_shift [Cout]");
+    if (use_acc)
+      TORCH_CHECK(stats.numel() >= (int64_t)acc_rows * 2 * Cout + Cout,
+                  "shifted accumulator needs its K row");
+  }
+  ShiftScope shift_scope(shift ? ptr<float>(*stat_shift) : nullptr);
   if (bias.has_value() && bias->defined()) {
     check_f32(*bias, "bias");
     TORCH_CHECK(bias->numel() == Cout, "bias size");
@@ -586,6 +607,19 @@ Tensor bn_stats(const Tensor& x) {
   return partial;
 }
 
+// centered form (robust variance): sums of x - K with K = x's first row, K returned alongside
+// -> {partial [P][2][C], K [C]} (the finalize's kin)
+std::vector<Tensor> bn_stats_centered(const Tensor& x) {
+  check_bf16(x, "x");
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  const int P = pca::bn_row_blocks(M, C);
+  auto buf = at::empty({(int64_t)P * 2 * C + C}, x.options().dtype(at::kFloat));
+  float* k = ptr<float>(buf) + (size_t)P * 2 * C;
+  pca::bn_stats_launch(ptr<bf16>(x), M, C, ptr<float>(buf), P, cur_stream(), k);
+  return {buf.narrow(0, 0, (int64_t)P * 2 * C).view({P, 2, C}), buf.narrow(0, (int64_t)P * 2 * C, C)};
+}
+
 // Reduce-kernel grid when it adds into an R-row sharded accumulator: at most kAccDepth
 // workgroups per shard row, so the same-address fp32 atomics stay shallow (deeper queues — 1024
 // blocks into 16 rows — cost more than the finalize launch they remove).
@@ -637,10 +671,13 @@ Tensor bias_grad(const Tensor& dy, const optional<Tensor>& accum) {
 }
 
 // partial [R, 2, C] (or undefined in eval) -> aux [4, C] = {mean, invstd, scale, shift}
+// kin: the shift K the producer subtracted from its sums (pilot / centred stats), or none;
+// pilot_out: receives the batch mean (may be kin itself)
 Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional<Tensor>& gamma,
                    const optional<Tensor>& beta, const Tensor& rmean, const Tensor& rvar,
                    const optional<Tensor>& nbt, double momentum, double eps, bool training,
-                   bool update_running) {
+                   bool update_running, const optional<Tensor>& kin,
+                   const optional<Tensor>& pilot_out) {
   const int C = rmean.numel();
   auto aux = at::empty({4, C}, rmean.options());
   const float* stat = nullptr;
@@ -659,10 +696,19 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
       stat = ptr<float>(folded);
     }
   }
+  if (kin.has_value() && kin->defined()) {
+    check_f32(*kin, "kin");
+    TORCH_CHECK(kin->numel() == C, "kin [C]");
+  }
+  if (pilot_out.has_value() && pilot_out->defined()) {
+    check_f32(*pilot_out, "pilot_out");
+    TORCH_CHECK(pilot_out->numel() == C, "pilot_out [C]");
+  }
   pca::bn_finalize_launch(stat, R, C, count, optr<float>(gamma), optr<float>(beta),
                           ptr<float>(rmean), ptr<float>(rvar), optr<int64_t>(nbt), (float)momentum,
                           (float)eps, training ? 1 : 0, update_running ? 1 : 0, ptr<float>(aux),
-                          cur_stream());
+                          cur_stream(), training ? optr<float>(kin) : nullptr,
+                          training ? optr<float>(pilot_out) : nullptr);
   return aux;
 }
 
@@ -704,11 +750,20 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
                                  const optional<Tensor>& gamma2, const optional<Tensor>& beta2,
                                  const optional<Tensor>& rmean2, const optional<Tensor>& rvar2,
                                  const optional<Tensor>& nbt2, double momentum2, double eps2,
-                                 int act, bool want_mask, const optional<Tensor>& zero) {
+                                 int act, bool want_mask, const optional<Tensor>& zero,
+                                 bool shifted, const optional<Tensor>& pilot, bool shifted2,
+                                 const optional<Tensor>& pilot2) {
   check_bf16(y, "y");
   const int C = y.size(-1);
   const int M = y.numel() / C;
   check_acc(acc, R, 2, C);
+  // shifted accumulators carry the producers' K row after the sums; the pilots get the means
+  TORCH_CHECK(!shifted || acc.numel() >= (int64_t)R * 2 * C + C, "shifted accumulator needs its K row");
+  for (const auto* pt : {&pilot, &pilot2})
+    if (pt->has_value() && (*pt)->defined()) {
+      check_f32(**pt, "pilot");
+      TORCH_CHECK((*pt)->numel() == C, "pilot [C]");
+    }
   const bool dual = y2.has_value() && y2->defined();
   if (dual) {
     check_bf16(*y2, "y2");
@@ -716,6 +771,8 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
     TORCH_CHECK(acc2.has_value() && acc2->defined() && rmean2.has_value() && rvar2.has_value(),
                 "dual BN needs the second accumulator and running stats");
     check_acc(*acc2, R2, 2, C);
+    TORCH_CHECK(!shifted2 || acc2->numel() >= (int64_t)R2 * 2 * C + C,
+                "shifted accumulator needs its K row");
   }
   if (res.has_value() && res->defined()) {
     check_bf16(*res, "res");
@@ -727,6 +784,8 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
   if (want_mask && act == 1 && C % 8 == 0)
     mask = at::empty({(int64_t)(y.numel() / 8)}, y.options().dtype(at::kByte));
   auto aux = at::empty({4, C}, fopt);
+  const float* k1 = shifted ? ptr<float>(acc) + (size_t)R * 2 * C : nullptr;
+  const float* k2 = (dual && shifted2) ? ptr<float>(*acc2) + (size_t)R2 * 2 * C : nullptr;
   Tensor aux2;
   if (dual) aux2 = at::empty({4, C}, fopt);
   const auto st = cur_stream();
@@ -739,16 +798,18 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
       optr<float>(beta2), optr<float>(rmean2), optr<float>(rvar2), optr<int64_t>(nbt2),
       (float)momentum2, (float)eps2, dual ? ptr<float>(aux2) : nullptr, optr<bf16>(res),
       optr<bf16>(y2), act, ptr<bf16>(out), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr,
-      has_zero ? ptr<float>(*zero) : nullptr, has_zero ? (int)zero->numel() : 0, st);
+      has_zero ? ptr<float>(*zero) : nullptr, has_zero ? (int)zero->numel() : 0, st, shifted,
+      optr<float>(pilot), shifted2, optr<float>(pilot2));
   if (!fused) {
     pca::bn_finalize_launch(ptr<float>(acc), R, C, count, optr<float>(gamma), optr<float>(beta),
                             ptr<float>(rmean), ptr<float>(rvar), optr<int64_t>(nbt),
-                            (float)momentum, (float)eps, 1, 1, ptr<float>(aux), st);
+                            (float)momentum, (float)eps, 1, 1, ptr<float>(aux), st, k1,
+                            optr<float>(pilot));
     if (dual)
       pca::bn_finalize_launch(ptr<float>(*acc2), R2, C, count, optr<float>(gamma2),
                               optr<float>(beta2), ptr<float>(*rmean2), ptr<float>(*rvar2),
                               optr<int64_t>(nbt2), (float)momentum2, (float)eps2, 1, 1,
-                              ptr<float>(aux2), st);
+                              ptr<float>(aux2), st, k2, optr<float>(pilot2));
     if (has_zero) zero->zero_();
     pca::bn_apply_launch(ptr<bf16>(y), ptr<float>(aux), C, y.numel(), optr<bf16>(res),
                          optr<bf16>(y2), dual ? ptr<float>(aux2) : nullptr, act, ptr<bf16>(out),
@@ -1677,7 +1738,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "hipGetLastError() of this thread as a string ('' = no error); clears it");
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wb"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("groups"), py::arg("want_stats"), py::arg("stat_acc") = py::none(),
-        py::arg("acc_rows") = 0);
+        py::arg("acc_rows") = 0, py::arg("stat_shift") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend") = py::none());
   m.def("conv_dgrad_bn", &conv_dgrad_impl, py::arg("dy"), py::arg("wt"), py::arg("H"),
@@ -1717,11 +1778,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weight_prep", &weight_prep);
   m.def("weight_prep_multi", &weight_prep_multi);
   m.def("bn_stats", &bn_stats);
+  m.def("bn_stats_centered", &bn_stats_centered,
+        "BN sums of x - x[0] (robust variance) -> (partial [P][2][C], K [C])");
   m.def("bn_acc_max_elems", &acc_max_elems,
         "largest tensor whose BN sums a separate pass adds into an accumulator");
   m.def("bn_stats_acc", &bn_stats_acc, "BN sums of a bare tensor into a sharded accumulator");
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("accum") = py::none());
-  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_finalize", &bn_finalize, py::arg("partial"), py::arg("count"), py::arg("gamma"),
+        py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("momentum"),
+        py::arg("eps"), py::arg("training"), py::arg("update_running"), py::arg("kin") = py::none(),
+        py::arg("pilot_out") = py::none());
   m.def("bn_apply", &bn_apply);
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("mask"), py::arg("y"),
         py::arg("aux"), py::arg("gamma"), py::arg("y2"), py::arg("aux2"), py::arg("gamma2"),
@@ -1735,7 +1801,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("nbt"), py::arg("momentum"), py::arg("eps"), py::arg("res"), py::arg("y2"),
         py::arg("acc2"), py::arg("R2"), py::arg("gamma2"), py::arg("beta2"), py::arg("rmean2"),
         py::arg("rvar2"), py::arg("nbt2"), py::arg("momentum2"), py::arg("eps2"), py::arg("act"),
-        py::arg("want_mask"), py::arg("zero") = py::none(),
+        py::arg("want_mask"), py::arg("zero") = py::none(), py::arg("shifted") = false,
+        py::arg("pilot") = py::none(), py::arg("shifted2") = false, py::arg("pilot2") = py::none(),
         "training BN(+act/+res/+BN2) with the finalize folded in from sharded accumulators");
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("nhwc_to_nchw", &nhwc_to_nchw);

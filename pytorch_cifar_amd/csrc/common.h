@@ -99,6 +99,25 @@ __device__ __forceinline__ void stat_out(float* base, int row, int shards, size_
 int stat_shards();
 void set_stat_shards(int shards);
 
+// Shifted BatchNorm forward sums (robust variance). A producer of forward statistics sums
+// d = v - K[c] and d*d, where K is the consuming BN's pilot mean (its previous batch mean): the
+// fold's E[d^2] - E[d]^2 then has no catastrophic cancellation once K is near the batch mean
+// (fp32 E[x^2] - E[x]^2 loses (mean/std)^2 * eps of the variance). K comes from stat_shift() (set
+// by the bindings around a launch, like stat_shards; nullptr = unshifted, K = 0). With a sharded
+// accumulator the producer also publishes the K it used in the accumulator's K row
+// base[shards * rowlen + c] (every block stores the same values; block 0 does), which is what
+// the fold reads — the fold's block 0 may overwrite the pilot itself while other blocks fold.
+const float* stat_shift();
+void set_stat_shift(const float* k);
+
+__device__ __forceinline__ float shift_of(const float* k, int c) { return k ? k[c] : 0.f; }
+
+__device__ __forceinline__ void stat_krow(float* base, int shards, size_t rowlen, const float* k,
+                                          int C) {
+  if (k && shards > 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+    for (int c = threadIdx.x; c < C; c += blockDim.x) base[(size_t)shards * rowlen + c] = k[c];
+}
+
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_SIGMOID = 3 };
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }

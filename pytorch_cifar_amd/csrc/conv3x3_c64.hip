@@ -33,6 +33,7 @@ struct C64Geom {
   float* bn_part;   // [gridDim.x][2][64]
   int shards;       // stats / bn_part: 0 = slab rows, >0 = sharded atomic accumulator
   int64_t* prof;    // diagnostics: per-wave shader-clock stamps (c64_set_prof), else nullptr
+  const float* kshift;   // forward stats: per-channel shift K (common.h stat_shift), or nullptr
 };
 
 namespace c64 {
@@ -135,10 +136,14 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
     boff[ni] = nn * 1152 + ((kq ^ (nn & 7)) << 4);
   }
 
-  // per-lane BatchNorm sums of channels q*16 + e, accumulated over every tile (forward)
-  float st_s[16], st_q[16];
+  // per-lane BatchNorm sums of channels q*16 + e, accumulated over every tile (forward; shifted
+  // by kk = the consumer BN's pilot mean when given)
+  float st_s[16], st_q[16], kk[16];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) st_s[e] = st_q[e] = 0.f;
+  for (int e = 0; e < 16; ++e) {
+    st_s[e] = st_q[e] = 0.f;
+    kk[e] = (STATS && g.kshift) ? g.kshift[q * 16 + e] : 0.f;
+  }
   // fused BN-backward reduce (dgrad): sums of dz and dz * xhat of channels q*16 + e
   const bool bnf = DGRAD && g.bn_part != nullptr;
   float bs1[16], bs2[16], bmean[16], bistd[16];
@@ -183,7 +188,7 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
     if constexpr (STATS) {
 #pragma unroll
       for (int e = 0; e < 16; e += 2) {   // packed f32 adds / FMAs (no MFMA to share issue with)
-        f32x2 x = {v[e], v[e + 1]};
+        f32x2 x = {v[e] - kk[e], v[e + 1] - kk[e + 1]};
         f32x2 s2 = {st_s[e], st_s[e + 1]}, q2 = {st_q[e], st_q[e + 1]};
         s2 += x;
         q2 += x * x;
@@ -382,6 +387,7 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
       stat_out(dst, blockIdx.x, g.shards, 128, tid, a);
       stat_out(dst, blockIdx.x, g.shards, 128, 64 + tid, b);
     }
+    if constexpr (STATS) stat_krow(stats, g.shards, 128, g.kshift, 64);
   }
 }
 
@@ -536,15 +542,17 @@ void conv3x3_c64_v1_kernel(const bf16* __restrict__ A, const bf16* __restrict__ 
     // ---- epilogue ----
     if constexpr (STATS) {
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
+      for (int ni = 0; ni < 4; ++ni) {
+        const float kc = g.kshift ? g.kshift[ni * 16 + (lane & 15)] : 0.f;
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float v = acc[mi][ni][j];
+            const float v = acc[mi][ni][j] - kc;
             st_s[ni] += v;
             st_q[ni] += v * v;
           }
+      }
     }
     raw_barrier();                                // every wave is done reading this halo
     bf16* Cs = reinterpret_cast<bf16*>(smem + buf * HBYTES);
@@ -619,6 +627,7 @@ void conv3x3_c64_v1_kernel(const bf16* __restrict__ A, const bf16* __restrict__ 
       stat_out(stats, blockIdx.x, g.shards, 128, tid, s);
       stat_out(stats, blockIdx.x, g.shards, 128, 64 + tid, q);
     }
+    stat_krow(stats, g.shards, 128, g.kshift, 64);
   } else {
     wait_vmcnt<0>();
     if (bnf) {
@@ -691,6 +700,7 @@ void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const 
   g.bn_aux = bn_aux;
   g.bn_part = dgrad ? bn_part : nullptr;
   g.shards = stat_shards();
+  g.kshift = (!dgrad && stats) ? stat_shift() : nullptr;
   g.prof = nullptr;
   const dim3 grid(c64_grid(g.tiles)), block(256);
   static const int ver = [] {

@@ -39,7 +39,23 @@ struct HxGeom {
   const uint8_t* bn_mask;
   const float* bn_aux;
   float* bn_part;
+  // MODE 3 (stride-1 dgrad of a projection-shortcut block tail act(BN(y) + BN2(y2))): the third
+  // sum dz * xhat2 (accumulator rows of 3 sums)
+  const bf16* bn_y2;
+  const float* bn_aux2;
+  const float* kshift;   // forward stats: per-channel shift K (common.h stat_shift), or nullptr
 };
+
+// dgrad: prefetch the fused BN reduce's y during the last tap (true) or load it at the epilogue
+// (false: 36 fewer registers live across the MFMA loop; the 8-wave dgrads spilled with it)
+#ifndef PCA_HX_PREFETCH_Y
+#define PCA_HX_PREFETCH_Y 0
+#endif
+constexpr bool kHxPrefetchY = PCA_HX_PREFETCH_Y != 0;
+// MODE 3 (dual-BN third sum) is compiled out: its 48 per-lane sums spill the 8-wave variants
+// (180+ registers); the dual-BN block-tail dgrads stay on the generic igemm
+constexpr bool kHxDual = false;
+bool conv_hx_dual() { return kHxDual; }
 
 __device__ __forceinline__ int hx_perm(int n) { return ((n >> 2) & 3) * 16 + (n >> 4) * 4 + (n & 3); }
 
@@ -56,7 +72,7 @@ struct HxShape {
   static constexpr int BPC = BN / 8;                  // weight pieces per tap
   static constexpr int BS = BPC / NW;                 // ... per wave
   static constexpr int BBYTES = BN * 128;
-  static constexpr int LDS = 2 * HBYTES + 2 * BBYTES + 1024 + BN * 8;
+  static constexpr int LDS = 2 * HBYTES + 2 * BBYTES + 1024 + BN * 16;
   static_assert(IMGS * W * W == BM, "a tile is whole images");
   static_assert(BPC % NW == 0, "weight pieces split evenly over the waves");
   // halo piece k is issued during tap k % (TAPS-1) (the last tap stages the next chunk's weights)
@@ -67,7 +83,8 @@ struct HxShape {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-// MODE 0: forward (3x3 taps); 1: stride-1 dgrad (mirrored taps, fused dgrad epilogue);
+// MODE 0: forward (3x3 taps); 1: stride-1 dgrad (mirrored taps, fused dgrad epilogue); 3: MODE 1
+// whose fused BN-backward reduce also sums dz * xhat2 of a dual-BN block tail;
 // 2: stride-2 dgrad as a 2x2 convolution over dY producing the four output parity classes as
 // 4 x Cin channels (weights pre-arranged by hx_s2_weight_kernel, zero where a class does not meet
 // a tap), written depth-to-space: class (ph, pw) of dY pixel (y, x) is dX pixel (2y+ph, 2x+pw).
@@ -81,6 +98,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
                        const HxGeom g) {
   constexpr bool DGRAD = MODE != 0;
   constexpr bool D2S = MODE == 2;
+  constexpr bool DUAL = MODE == 3;
   constexpr int KS = D2S ? 2 : 3, TAPS = KS * KS;
   using SH = HxShape<W, IMGS, WM, WN, TAPS>;
   constexpr int NW = SH::NW, BM = SH::BM, BN = SH::BN, W2 = SH::W2;
@@ -89,7 +107,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
   char* const Hs = smem;                       // [2][HBYTES] halo ring
   char* const Bs = smem + 2 * HB;              // [2][BBYTES] weight ring
   char* const dummy = smem + 2 * HB + 2 * BB;  // landing place of padding DMA slots
-  float* const auxs = reinterpret_cast<float*>(dummy + 1024);   // dgrad: BN mean | istd
+  float* const auxs = reinterpret_cast<float*>(dummy + 1024);   // dgrad: BN mean | istd [| 2]
 
   typedef __attribute__((address_space(3))) const char lds_char;
   typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
@@ -136,7 +154,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
     b_row[k] = (ch * KA + (((lane & 7) ^ (r & 7)) << 3)) * 2;
   }
   auto b_tile = [&](int tap, int ch, int bb) {
-    const int src_tap = MODE == 1 ? 8 - tap : tap;
+    const int src_tap = (MODE == 1 || MODE == 3) ? 8 - tap : tap;
     const int delta = (src_tap * g.CA + ch * 64) * 2;
 #pragma unroll
     for (int k = 0; k < SH::BS; ++k)
@@ -162,16 +180,26 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
 
   // per-lane BatchNorm sums of channels nb0 + wn*64 + q*16 + e (forward stats / dgrad reduce)
   const bool bnf = DGRAD && g.bn_part != nullptr;
-  float s1[16], s2[16];
+  // per-lane sums of its 16 channels, accumulated over every tile (forward statistics / dgrad
+  // fused BN-backward reduce; MODE 3 a third one)
+  float s1[16], s2[16], s3[DUAL ? 16 : 1];
 #pragma unroll
   for (int e = 0; e < 16; ++e) s1[e] = s2[e] = 0.f;
+#pragma unroll
+  for (int e = 0; e < (DUAL ? 16 : 1); ++e) s3[e] = 0.f;
   const int ch_lane = nb0 + wn * 64 + q * 16;  // first of this lane's 16 produced channels
+  float kk[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) kk[e] = (STATS && g.kshift) ? g.kshift[ch_lane + e] : 0.f;
   // its output-tensor channel (depth-to-space: class ch / COUT, channel ch % COUT)
   const int co_lane = D2S ? ch_lane % g.COUT : ch_lane;
   const int cls_lane = D2S ? ch_lane / g.COUT : 0;
   if (bnf) {   // the block's BN mean / istd once into LDS (read per element in the epilogue)
     for (int i = tid; i < 2 * BN; i += NW * 64)
       auxs[i] = g.bn_aux[(i >= BN ? g.COUT : 0) + (nb0 + (i % BN)) % g.COUT];
+    if constexpr (DUAL)
+      for (int i = tid; i < 2 * BN; i += NW * 64)
+        auxs[2 * BN + i] = g.bn_aux2[(i >= BN ? g.COUT : 0) + (nb0 + (i % BN)) % g.COUT];
     __syncthreads();
   }
   // output pixel of tile pixel p (the dY-resolution pixel for D2S, shifted to its class)
@@ -247,8 +275,10 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
                 pre_a[mi][1] = *reinterpret_cast<const uint4*>(addend + o + 8);
               }
               if (bnf) {
-                pre_y[mi][0] = *reinterpret_cast<const uint4*>(g.bn_y + o);
-                pre_y[mi][1] = *reinterpret_cast<const uint4*>(g.bn_y + o + 8);
+                if constexpr (kHxPrefetchY) {
+                  pre_y[mi][0] = *reinterpret_cast<const uint4*>(g.bn_y + o);
+                  pre_y[mi][1] = *reinterpret_cast<const uint4*>(g.bn_y + o + 8);
+                }
                 pre_m[mi] = *reinterpret_cast<const uint16_t*>(g.bn_mask + (o >> 3));
               }
             }
@@ -280,6 +310,18 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
     }
 
     // ---- epilogue: lane holds channels ch_lane + [0,16) of tile pixel wm*64 + mi*16 + lane&15 ----
+    if constexpr (DGRAD && !kHxPrefetchY) {
+      // the BN input y of the fused reduce, loaded now for all four rows at once (prefetched
+      // during the last tap it held 32 more registers across the MFMA loop: 256 + spills)
+      if (bnf) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const size_t o = out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
+          pre_y[mi][0] = *reinterpret_cast<const uint4*>(g.bn_y + o);
+          pre_y[mi][1] = *reinterpret_cast<const uint4*>(g.bn_y + o + 8);
+        }
+      }
+    }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       float v[16];
@@ -292,8 +334,9 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
       if constexpr (STATS) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          s1[e] += v[e];
-          s2[e] += v[e] * v[e];
+          const float d = v[e] - kk[e];   // shifted sums (kk = 0 unshifted)
+          s1[e] += d;
+          s2[e] += d * d;
         }
       }
       uint4 o0 = pack8(v), o1 = pack8(v + 8);
@@ -323,6 +366,17 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
             const int c = ch_lane - nb0 + e;
             s2[e] += dz * (yy[e] - auxs[c]) * auxs[BN + c];   // (aux of channel c % COUT)
           }
+          if constexpr (DUAL) {   // (y2 read here: no prefetch registers for it)
+            const size_t o = out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
+            unpack8(*reinterpret_cast<const uint4*>(g.bn_y2 + o), yy);
+            unpack8(*reinterpret_cast<const uint4*>(g.bn_y2 + o + 8), yy + 8);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
+              const int c = ch_lane - nb0 + e;
+              s3[e] += dz * (yy[e] - auxs[2 * BN + c]) * auxs[3 * BN + c];
+            }
+          }
         }
       }
       bf16* dst = Y + out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
@@ -333,22 +387,25 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
 
   // ---- per-block channel sums: the 16 lanes of a group share channels; WM waves per column ----
   if (STATS || bnf) {
+    constexpr int NSR = DUAL ? 3 : 2;             // sums per channel
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
 #pragma unroll
       for (int x = 1; x < 16; x <<= 1) {
         s1[e] += __shfl_xor(s1[e], x, 64);
         s2[e] += __shfl_xor(s2[e], x, 64);
+        if constexpr (DUAL) s3[e] += __shfl_xor(s3[e], x, 64);
       }
     }
     wait_vmcnt<0>();
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][NSR]
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        red[(wm * BN + wn * 64 + q * 16 + e) * 2 + 0] = s1[e];
-        red[(wm * BN + wn * 64 + q * 16 + e) * 2 + 1] = s2[e];
+        red[(wm * BN + wn * 64 + q * 16 + e) * NSR + 0] = s1[e];
+        red[(wm * BN + wn * 64 + q * 16 + e) * NSR + 1] = s2[e];
+        if constexpr (DUAL) red[(wm * BN + wn * 64 + q * 16 + e) * NSR + 2] = s3[e];
       }
     }
     __syncthreads();
@@ -356,12 +413,13 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
     // parity classes of the stride-2 dgrad); slab row per (M walker, N block) for D2S
     const int nco = D2S ? (BN < g.COUT ? BN : g.COUT) : BN;
     if (tid < nco) {
-      float a = 0.f, b = 0.f;
+      float a = 0.f, b = 0.f, d3 = 0.f;
       for (int j = tid; j < BN; j += (D2S ? g.COUT : BN)) {
 #pragma unroll
         for (int w = 0; w < WM; ++w) {   // fixed order: deterministic per block
-          a += red[(w * BN + j) * 2 + 0];
-          b += red[(w * BN + j) * 2 + 1];
+          a += red[(w * BN + j) * NSR + 0];
+          b += red[(w * BN + j) * NSR + 1];
+          if constexpr (DUAL) d3 += red[(w * BN + j) * NSR + 2];
         }
       }
       float* dst = STATS ? stats : g.bn_part;
@@ -370,9 +428,11 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
       const int cb = D2S && g.COUT > BN ? g.COUT / BN : 1;
       const int row = D2S ? (int)(blockIdx.x * (gridDim.y / cb) + blockIdx.y / cb) : (int)blockIdx.x;
       const int col = (nb0 + tid) % g.COUT;
-      stat_out(dst, row, g.shards, 2 * g.COUT, col, a);
-      stat_out(dst, row, g.shards, 2 * g.COUT, g.COUT + col, b);
+      stat_out(dst, row, g.shards, NSR * g.COUT, col, a);
+      stat_out(dst, row, g.shards, NSR * g.COUT, g.COUT + col, b);
+      if constexpr (DUAL) stat_out(dst, row, g.shards, NSR * g.COUT, 2 * g.COUT + col, d3);
     }
+    if constexpr (STATS) stat_krow(stats, g.shards, 2 * g.COUT, g.kshift, g.COUT);
   }
 }
 
@@ -380,6 +440,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
 // host side
 // ---------------------------------------------------------------------------------------
 int stat_shards();
+const float* stat_shift();
 
 static int hx_cus() {
   static int n = 0;
@@ -432,7 +493,10 @@ static int hx_run(const bf16* a, const bf16* b, bf16* y, float* stats, const bf1
   const int gx = hx_grid_x<W, IMGS, WM, WN, MODE>(g, nblocks);
   if (launch) {
     const dim3 grid(gx, nblocks), block(WM * WN * 64);
-    if (MODE != 0)
+    if (kHxDual && MODE == 1 && g.bn_part && g.bn_y2)
+      hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, kHxDual ? 3 : 1, false>), grid, block,
+                         0, st, a, b, y, nullptr, addend, nullptr, g);
+    else if (MODE != 0)
       hipLaunchKernelGGL((conv3x3_hx_kernel<W, IMGS, WM, WN, MODE, false>), grid, block, 0, st, a, b,
                          y, nullptr, addend, nullptr, g);
     else if (stats)
@@ -461,7 +525,7 @@ static int hx_dispatch(const bf16* a, const bf16* b, bf16* y, float* stats, cons
 int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
                    const float* bias, int N, int H, int CA, int CO, int mode, hipStream_t st,
                    const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
-                   bool launch) {
+                   bool launch, const bf16* bn_y2, const float* bn_aux2) {
   HxGeom g;
   g.N = N;
   g.CA = CA;
@@ -475,6 +539,9 @@ int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf
   g.bn_mask = bn_mask;
   g.bn_aux = bn_aux;
   g.bn_part = mode != 0 ? bn_part : nullptr;
+  g.bn_y2 = mode == 1 && bn_part ? bn_y2 : nullptr;   // (accumulator mode: rows of 3 sums)
+  g.bn_aux2 = g.bn_y2 ? bn_aux2 : nullptr;
+  g.kshift = mode == 0 && stats ? stat_shift() : nullptr;
   if (mode == 0) return hx_dispatch<0>(a, b, y, stats, addend, bias, g, H, st, launch);
   if (mode == 1) return hx_dispatch<1>(a, b, y, stats, addend, bias, g, H, st, launch);
   return hx_dispatch<2>(a, b, y, stats, addend, bias, g, H, st, launch);

@@ -65,6 +65,7 @@ struct ConvGeom {
   const bf16* bn_y2;
   const float* bn_aux2;
   int shards;           // BN partial sums (stats / bn_part): 0 = slab rows, >0 = sharded atomics
+  const float* kshift;  // forward stats: per-channel shift K (common.h stat_shift), or nullptr
 };
 
 // dz = dX * relu'(y), accumulated as (sum dz, sum dz * xhat) for 8 channels
@@ -546,16 +547,33 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       }
     }
     if constexpr (STATS) {
+      if (g.kshift) {   // shifted sums (robust variance): rows past M must not contribute -K
 #pragma unroll
-      for (int ni = 0; ni < TN; ++ni)
+        for (int ni = 0; ni < TN; ++ni) {
+          const int c = n0 + wn * WTN + ni * 16 + (lane & 15);
+          const float kc = c < g.Cn ? g.kshift[grp * g.Cn + c] : 0.f;
 #pragma unroll
-        for (int mi = 0; mi < TM; ++mi)
+          for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float v = acc[mi][ni][j];   // rows past M are exact zeros (zero-filled A)
-            st_s[ni] += v;
-            st_q[ni] += v * v;
-          }
+            for (int j = 0; j < 4; ++j) {
+              const int r = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + j;
+              const float d = r < Mrows ? acc[mi][ni][j] - kc : 0.f;
+              st_s[ni] += d;
+              st_q[ni] += d * d;
+            }
+        }
+      } else {
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float v = acc[mi][ni][j];   // rows past M are exact zeros (zero-filled A)
+              st_s[ni] += v;
+              st_q[ni] += v * v;
+            }
+      }
     }
     bf16* Cs = reinterpret_cast<bf16*>(smem);
 #pragma unroll
@@ -650,6 +668,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         stat_out(stats, blockIdx.x, g.shards, 2 * g.Co, g.Co + grp * g.Cn + c, q);
       }
     }
+    stat_krow(stats, g.shards, 2 * g.Co, g.kshift, g.Co);
   }
 }
 
@@ -922,15 +941,21 @@ __global__ __launch_bounds__(WAVES * 64) void conv_igemm_ph_kernel(const bf16* _
     }
     if constexpr (STATS) {
 #pragma unroll
-      for (int ni = 0; ni < TN; ++ni)
+      for (int ni = 0; ni < TN; ++ni) {
+        const int c = n0 + wn * WTN + ni * 16 + (lane & 15);
+        const float kc = (g.kshift && c < g.Cn) ? g.kshift[grp * g.Cn + c] : 0.f;
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float v = acc[mi][ni][j];   // rows past M are exact zeros (zero-filled A)
-            st_s[ni] += v;
-            st_q[ni] += v * v;
+            // rows past M are exact zeros (zero-filled A): unshifted they add nothing, shifted
+            // they must not add -K
+            const int r = m0 + wm * 128 + mi * 16 + (lane >> 4) * 4 + j;
+            const float d = r < Mrows ? acc[mi][ni][j] - kc : 0.f;
+            st_s[ni] += d;
+            st_q[ni] += d * d;
           }
+      }
     }
     constexpr int CRB = BN * 2;   // bytes per staged C row
 #pragma unroll
@@ -993,6 +1018,7 @@ __global__ __launch_bounds__(WAVES * 64) void conv_igemm_ph_kernel(const bf16* _
         stat_out(stats, blockIdx.x, g.shards, 2 * g.Co, g.Co + grp * g.Cn + c, q);
       }
     }
+    stat_krow(stats, g.shards, 2 * g.Co, g.kshift, g.Co);
   }
 }
 
@@ -1342,7 +1368,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                            float* __restrict__ bn_part,
                                                            int shards,
                                                            const bf16* __restrict__ bn_y2,
-                                                           const float* __restrict__ bn_aux2) {
+                                                           const float* __restrict__ bn_aux2,
+                                                           const float* __restrict__ kshift) {
   __shared__ float red[3 * 2048];
   const int NSB = bn_y2 ? 3 : 2;      // fused BN sums per channel (3: dual BN)
   const int CG = Co >> 3;             // 8-channel groups per row (Co <= 2048: CG <= 256)
@@ -1355,6 +1382,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   for (int q = 0; q < 8; ++q) sm[q] = sq[q] = 0.f;
 #pragma unroll
   for (int q = 0; q < 8; ++q) b[q] = bias ? bias[cg * 8 + q] : 0.f;
+  float kk[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) kk[q] = (STATS && kshift && active) ? kshift[cg * 8 + q] : 0.f;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
   const size_t plane = (size_t)M * Co;
@@ -1380,8 +1410,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       if constexpr (STATS) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          sm[q] += a[q];
-          sq[q] += a[q] * a[q];
+          const float d = a[q] - kk[q];   // shifted sums (kk = 0 unshifted)
+          sm[q] += d;
+          sq[q] += d * d;
         }
       }
       if (addend) {
@@ -1436,6 +1467,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       stat_out(stats, blockIdx.x, shards, 2 * Co, c, s0);
       stat_out(stats, blockIdx.x, shards, 2 * Co, Co + c, q0);
     }
+    stat_krow(stats, shards, 2 * Co, kshift, Co);
   }
 }
 
@@ -1473,6 +1505,7 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   g.bn_y2 = nullptr;
   g.bn_aux2 = nullptr;
   g.shards = stat_shards();
+  g.kshift = stat_shift();
   return g;
 }
 
@@ -1627,10 +1660,12 @@ static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, co
     const int gx = splitk_reduce_grid(M, g.Co, &rpb);
     if (stats)
       hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
-                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2);
+                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2,
+                         g.kshift);
     else
       hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
-                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2);
+                         rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2,
+                         nullptr);
     return;
   }
   const ConvGeom& g = g0;
@@ -1725,9 +1760,10 @@ bool conv_hx_applicable(int N, int H, int W, int CA, int CO, int KH, int KW, int
 int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
                    const float* bias, int N, int H, int CA, int CO, int mode, hipStream_t st,
                    const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
-                   bool launch);
+                   bool launch, const bf16* bn_y2 = nullptr, const float* bn_aux2 = nullptr);
 bool conv_hx_s2_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                            int pad, int groups, int Ho, int Wo);
+bool conv_hx_dual();
 void conv_hx_s2_weights(const bf16* wt, int Cin, int Cout, bf16* w2, hipStream_t st);
 // (for a dgrad geometry g: Hs/Ws/Cs = dY, Ho/Wo/Co = dX)
 static bool hx_ok(const ConvGeom& g, int mode) {
@@ -1806,7 +1842,7 @@ static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, 
       Bw = w2;
     }
     conv_hx_launch(A, Bw, Y, stats, addend, bias, g.N, g.Hs, g.Cs, MODE == 2 ? 4 * g.Co : g.Co,
-                   MODE, st, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, true);
+                   MODE, st, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, true, g.bn_y2, g.bn_aux2);
     return;
   }
   switch (igemm_select(g)) {
@@ -1931,7 +1967,7 @@ int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
     return c64_fuse && !dual ? conv_c64_stat_rows(N, H) : 0;
   const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   if (g.Co % 8 != 0) return 0;
-  if (dual && (g.mode != 1 || ph_cfg<1>(g) >= 0 || use_hx<1>(g))) return 0;
+  if (dual && (g.mode != 1 || ph_cfg<1>(g) >= 0 || (use_hx<1>(g) && !conv_hx_dual()))) return 0;
   if (g.mode == 2) {
     if (use_hx<2>(g)) return hx_grid<2>(g);   // one slab row per (tile group, class-channel block)
     if (igemm_ws_floats<2>(g) > 0) {
@@ -2062,7 +2098,7 @@ void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, i
   g.bn_mask = bn_mask;
   g.bn_aux = bn_aux;
   g.bn_part = bn_part;
-  if (bn_part && g_dual_y2 && g.mode == 1 && ph_cfg<1>(g) < 0 && !use_hx<1>(g)) {
+  if (bn_part && g_dual_y2 && g.mode == 1 && ph_cfg<1>(g) < 0 && (!use_hx<1>(g) || conv_hx_dual())) {
     g.bn_y2 = g_dual_y2;
     g.bn_aux2 = g_dual_aux2;
   }

@@ -246,7 +246,8 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
                                                        const bf16* __restrict__ w,
                                                        const float* __restrict__ bias,
                                                        bf16* __restrict__ y, int N, int H,
-                                                       float* __restrict__ stats, int shards) {
+                                                       float* __restrict__ stats, int shards,
+                                                       const float* __restrict__ kshift) {
   constexpr int NT = CO / 16;
   constexpr int CST = CO + 8;                      // staged C row pitch (bf16)
   __shared__ __attribute__((aligned(16))) bf16 halo[kFHP * kSCS];
@@ -278,9 +279,12 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
     tok[ks] = tap < 9;
     toff[ks] = tok[ks] ? (tap / 3) * kFW2 + tap % 3 : 0;
   }
-  float st_s[NT], st_q[NT];
+  float st_s[NT], st_q[NT], kk[NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) st_s[nt] = st_q[nt] = 0.f;
+  for (int nt = 0; nt < NT; ++nt) {
+    st_s[nt] = st_q[nt] = 0.f;
+    kk[nt] = kshift ? kshift[nt * 16 + (lane & 15)] : 0.f;
+  }
 
   // halo of a chunk: rows h0-1 .. h0+8, cols -1 .. 32, zeros outside the image; loaded into
   // registers one chunk ahead (issued before the current chunk's MFMAs and epilogue)
@@ -335,8 +339,9 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float v = acc[mt][nt][j] + bb[nt];
-          st_s[nt] += v;
-          st_q[nt] += v * v;
+          const float d = v - kk[nt];   // shifted sums (kk = 0 unshifted)
+          st_s[nt] += d;
+          st_q[nt] += d * d;
           const int p = wid * 64 + mt * 16 + 4 * (lane >> 4) + j;
           ct[p * CST + nt * 16 + (lane & 15)] = f2bf(v);
         }
@@ -370,6 +375,7 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
       const float v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
       stat_out(stats, blockIdx.x, shards, 2 * CO, k * CO + c, v);
     }
+    stat_krow(stats, shards, 2 * CO, kshift, CO);
   }
 }
 
@@ -390,10 +396,11 @@ int conv_stem_stat_rows(int N, int H) { return std::min(kFGrid, N * (H / kSR)); 
 void conv_stem_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, float* stats,
                           int N, int H, int Cout, hipStream_t st) {
   const int grid = conv_stem_stat_rows(N, H), sh = stat_shards();
+  const float* k = stats ? stat_shift() : nullptr;
   switch (Cout) {
-    case 16: hipLaunchKernelGGL(stem_fwd_kernel<16>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh); break;
-    case 32: hipLaunchKernelGGL(stem_fwd_kernel<32>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh); break;
-    default: hipLaunchKernelGGL(stem_fwd_kernel<64>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh); break;
+    case 16: hipLaunchKernelGGL(stem_fwd_kernel<16>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh, k); break;
+    case 32: hipLaunchKernelGGL(stem_fwd_kernel<32>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh, k); break;
+    default: hipLaunchKernelGGL(stem_fwd_kernel<64>, dim3(grid), dim3(256), 0, st, x, w, bias, y, N, H, stats, sh, k); break;
   }
 }
 

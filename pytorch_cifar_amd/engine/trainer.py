@@ -117,10 +117,12 @@ class TrainStep:
                 add(st.get("momentum_buffer"))
         for b in inner.buffers():
             add(b)
-        from ..ops.functional import rng_states
+        from ..ops.functional import bn_pilots, rng_states
 
         for r in rng_states(inner):      # dropout Philox step counters
             add(r)
+        for k in bn_pilots(inner):       # BN-statistics shifts (previous batch means)
+            add(k)
         add(self.metrics)
         return out
 
@@ -149,14 +151,19 @@ class TrainStep:
                 self.opt._arena_first = first
 
         def born_in_warmup():
-            # state created by the warm-ups themselves (the dropout Philox states appear on the
-            # first training forward): roll it back to its creation value {seed, step 0, tickets 0}
-            from ..ops.functional import rng_states
+            # state created by the warm-ups themselves (the dropout Philox states and the BN
+            # pilots appear on the first training forward): roll it back to its creation value
+            # ({seed, step 0, tickets 0}; a zero shift)
+            from ..ops.functional import bn_pilots, rng_states
 
+            inner = getattr(self.net, "module", self.net)
             with torch.no_grad():
-                for r in rng_states(getattr(self.net, "module", self.net)):
+                for r in rng_states(inner):
                     if id(r) not in known:
                         r[1:].zero_()
+                for k in bn_pilots(inner):
+                    if id(k) not in known:
+                        k.zero_()
 
         try:
             s = torch.cuda.Stream()

@@ -41,8 +41,9 @@ class Conv2d(nn.Conv2d):
         # travel through the conv's sharded accumulator instead of a slab (ops.functional.StatAcc)
         if want_stats and self.__dict__.get("_pca_acc_ok") and OF.acc_enabled(self.out_channels, x.device):
             acc = OF.stat_acc(self, "fwd", self.out_channels, 2, x.device)
+        pilot = OF.conv_pilot(self, x.device) if want_stats else None
         y, stats = OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.groups,
-                             want_stats, acc)
+                             want_stats, acc, pilot)
         if stats is not None:
             setattr(y, _STATS_ATTR, stats)
             y._pca_stats_src = self

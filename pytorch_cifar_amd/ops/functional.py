@@ -447,16 +447,25 @@ class StatAcc:
     ``state``: "clean" (all zero), "filled" (a producer added into it), "used" (a consumer folded
     it; it is cleared by the other pass of its BN, or by a memset before the next production)."""
 
-    __slots__ = ("buf", "R", "NS", "C", "state")
+    __slots__ = ("buf", "R", "NS", "C", "state", "shifted")
 
     def __init__(self, C, NS, device):
         self.C, self.NS, self.R = C, NS, acc_shards(C)
-        self.buf = torch.zeros(self.R * NS * C, dtype=torch.float32, device=device)
+        # [R][NS][C] sums + one K row (the shift a forward-statistics producer subtracted)
+        self.buf = torch.zeros(self.R * NS * C + C, dtype=torch.float32, device=device)
         self.state = "clean"
+        self.shifted = False   # the last producer subtracted K (and wrote the K row)
 
     def slab(self, ns=2):
         """[R][ns][C] view (finalize fallback path)."""
         return self.buf[: self.R * ns * self.C].view(self.R, ns, self.C)
+
+    def krow(self):
+        """The K row of a shifted forward accumulator, or None."""
+        if not self.shifted:
+            return None
+        o = self.R * 2 * self.C
+        return self.buf[o: o + self.C]
 
     def ensure_clean(self):
         if self.state != "clean":
@@ -467,6 +476,40 @@ class StatAcc:
         """Called before a producer adds in."""
         self.ensure_clean()
         self.state = "filled"
+        self.shifted = False
+
+
+# ------------------------------------------------- shifted (robust) BatchNorm forward sums
+# A conv that delivers its output's BN statistics subtracts a per-channel pilot mean K from every
+# value before summing (csrc/common.h stat_shift): var = E[(x-K)^2] - E[x-K]^2 has no catastrophic
+# cancellation once K is near the batch mean, which the previous batch's mean is. The pilot
+# lives on the producing conv (persistent, so hipGraph replays see a stable address); the
+# consuming BN links it on first sight and its finalize / fold writes each batch mean into it.
+def conv_pilot(conv, device):
+    """The pilot tensor of ``conv`` on ``device`` (None until a BN linked it)."""
+    d = conv.__dict__.get("_pca_pilot")
+    if d is None:
+        return None
+    return d.get(device.index if device.index is not None else torch.cuda.current_device())
+
+
+def link_pilot(conv, C, device):
+    """The consuming BN makes sure its producer has a pilot ([C] fp32, zero until the first batch
+    mean lands in it) and returns it."""
+    d = conv.__dict__.setdefault("_pca_pilot", {})
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    t = d.get(key)
+    if t is None or t.numel() != C:
+        t = d[key] = torch.zeros(C, dtype=torch.float32, device=device)
+    return t
+
+
+def bn_pilots(model):
+    """Every pilot tensor of ``model``'s convs (training-step state, like the BN buffers)."""
+    out = []
+    for m in model.modules():
+        out += list(m.__dict__.get("_pca_pilot", {}).values())
+    return out
 
 
 def acc_enabled(C: int, device) -> bool:
@@ -538,7 +581,7 @@ class _ConvMFMA(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, groups, want_stats, cin_pad, slot=None,
-                owner=False, bnsrc=None, acc=None):
+                owner=False, bnsrc=None, acc=None, pilot=None):
         C = _C()
         ctx.slot, ctx.owner = slot, owner
         ctx.bnsrc = bnsrc
@@ -562,12 +605,17 @@ class _ConvMFMA(torch.autograd.Function):
                 wb, wt = C.weight_prep(w_phys, groups, need_dx)
         else:
             wb, wt = _prepped_weight(weight, groups, w_phys, need_dx)
+        if not want_stats:
+            pilot = None
         if acc is not None and want_stats:
             acc.begin()
-            y, _ = C.conv_fwd(x, wb, bias, stride, padding, groups, True, acc.buf, acc.R)
+            y, _ = C.conv_fwd(x, wb, bias, stride, padding, groups, True, acc.buf, acc.R, pilot)
+            acc.shifted = pilot is not None
             stats = None                  # delivered through the accumulator (conv2d returns it)
         else:
-            y, stats = C.conv_fwd(x, wb, bias, stride, padding, groups, want_stats)
+            y, stats = C.conv_fwd(x, wb, bias, stride, padding, groups, want_stats, None, 0, pilot)
+            if pilot is not None and stats is not None and stats.numel():
+                stats._pca_kin = pilot    # the slab's sums are of x - pilot (finalize adds it back)
         ctx.geom = (stride, padding, groups, cin_pad, x.shape[1], x.shape[2])
         ctx.save_for_backward(x, wt if need_dx else None)
         ctx.weight = weight
@@ -583,7 +631,7 @@ class _ConvMFMA(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return (None,) * 12
+            return (None,) * 13
         C = _C()
         x, wt = ctx.saved_tensors
         stride, padding, groups, cin_pad, H, W = ctx.geom
@@ -644,7 +692,7 @@ class _ConvMFMA(torch.autograd.Function):
                     G.accumulate(bias, db)
                 else:
                     db_ret = db
-        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None, None
+        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None, None, None
 
 
 class _ConvDirect(torch.autograd.Function):
@@ -765,9 +813,11 @@ class _ConvDepthwise(torch.autograd.Function):
 _DW_BN_FUSE = os.environ.get("PCA_DW_BN_FUSE", "0") == "1"
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False, acc=None):
+def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False, acc=None,
+           pilot=None):
     """NCHW-shaped conv. On GPU returns (y, stats) where stats are BN partials (a slab tensor, or
-    ``acc`` — a :class:`StatAcc` the epilogue added into — when one is given), or None."""
+    ``acc`` — a :class:`StatAcc` the epilogue added into — when one is given), or None. With
+    ``pilot`` (the consuming BN's shift, :func:`link_pilot`) the MFMA paths sum x - pilot."""
     if isinstance(stride, (tuple, list)):
         assert stride[0] == stride[1]
         stride = stride[0]
@@ -797,7 +847,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
         slot, owner = _slot_for_conv(x)
         bnsrc = getattr(x, "_pca_bnsrc", None) if x.requires_grad else None
         y, stats = _ConvMFMA.apply(to_nhwc(x), weight, bias, stride, padding, groups, want_stats, 0,
-                                   slot, owner, bnsrc, acc if want_stats else None)
+                                   slot, owner, bnsrc, acc if want_stats else None, pilot)
         if want_stats and acc is not None:
             return to_nchw(y), acc
         return to_nchw(y), (stats if want_stats else None)
@@ -806,7 +856,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
         cp = _round8(Cin)
         # (BN partial sums into the accumulator as for every other MFMA conv: no finalize launch)
         y, stats = _ConvMFMA.apply(to_nhwc(x, pad_to=cp), weight, bias, stride, padding, groups, want_stats, cp,
-                                   None, False, None, acc if want_stats else None)
+                                   None, False, None, acc if want_stats else None, pilot)
         if want_stats and acc is not None:
             return to_nchw(y), acc
         return to_nchw(y), (stats if want_stats else None)
@@ -913,19 +963,22 @@ def add_bias(y_nhwc, bias):
 
 # -------------------------------------------------------------------------- batch norm
 class _BNCfg:
-    __slots__ = ("bn", "bn2", "act", "training", "count", "src", "bacc", "faccs")
+    __slots__ = ("bn", "bn2", "act", "training", "count", "src", "bacc", "faccs", "pilot", "pilot2")
 
     def __init__(self, bn, bn2, act, training, count):
         self.bn, self.bn2, self.act, self.training, self.count = bn, bn2, act, training, count
+        self.pilot = self.pilot2 = None   # the producers' pilots (receive this batch's means)
         self.src = None
         self.bacc = None      # the BN's backward StatAcc (sharded sums of dz, dz*xhat[, dz*xhat2])
         self.faccs = ()       # forward StatAccs this BN consumed (cleared by its backward kernel)
 
 
-def _bn_aux(C, bn, y, stats, training, count):
+def _bn_aux(C, bn, y, stats, training, count, pilot=None, kin=None):
+    """Finalize: aux [mean | invstd | scale | shift]. ``kin``: the shift the sums are of (pilot /
+    K row / centred pass); ``pilot``: receives the batch mean (the producer's next shift)."""
     if isinstance(stats, StatAcc):
         # an accumulator the fused kernel cannot consume here: finalize from its shard rows
-        aux = _bn_aux(C, bn, y, stats.slab(), training, count)
+        aux = _bn_aux(C, bn, y, stats.slab(), training, count, pilot, stats.krow())
         stats.state = "used"
         return aux
     use_batch = training or bn.running_mean is None
@@ -936,12 +989,16 @@ def _bn_aux(C, bn, y, stats, training, count):
         rv = torch.ones(y.shape[-1], device=y.device)
     update = training and bn.running_mean is not None
     if use_batch and stats is None:
-        stats = C.bn_stats(y)
+        # no producer delivered sums: one centred pass (sums of y - y[0]; robust variance)
+        stats, kin = C.bn_stats_centered(y)
+    elif use_batch and kin is None:
+        kin = getattr(stats, "_pca_kin", None)
     momentum = bn.momentum if bn.momentum is not None else 0.1
     w = bn.weight.detach() if bn.weight is not None else None
     b = bn.bias.detach() if bn.bias is not None else None
     return C.bn_finalize(stats if use_batch else None, float(count), w, b, rm, rv,
-                         bn.num_batches_tracked if update else None, momentum, bn.eps, use_batch, update)
+                         bn.num_batches_tracked if update else None, momentum, bn.eps, use_batch, update,
+                         kin if use_batch else None, pilot if use_batch else None)
 
 
 class _BatchNormAct(torch.autograd.Function):
@@ -973,7 +1030,9 @@ class _BatchNormAct(torch.autograd.Function):
                 bn2.running_var if a2 is not None else None,
                 bn2.num_batches_tracked if a2 is not None else None,
                 mom(bn2) if a2 is not None else 0.1, bn2.eps if a2 is not None else 1e-5,
-                ACT[cfg.act], relu, cfg.bacc.buf if cfg.bacc is not None else None)
+                ACT[cfg.act], relu, cfg.bacc.buf if cfg.bacc is not None else None,
+                stats.shifted, cfg.pilot, a2.shifted if a2 is not None else False,
+                cfg.pilot2 if a2 is not None else None)
             if cfg.bacc is not None:
                 cfg.bacc.state = "clean"      # block 0 cleared this BN's backward accumulator
             stats.state = "used"
@@ -986,11 +1045,11 @@ class _BatchNormAct(torch.autograd.Function):
                 mask = None
         else:
             aux = _bn_aux(C, bn, y, stats if isinstance(stats, StatAcc) or (stats is not None and stats.numel()) else None,
-                          cfg.training, cfg.count)
+                          cfg.training, cfg.count, cfg.pilot)
             aux2 = None
             if y2 is not None:
                 aux2 = _bn_aux(C, bn2, y2, stats2 if isinstance(stats2, StatAcc) or (stats2 is not None and stats2.numel()) else None,
-                               cfg.training, cfg.count)
+                               cfg.training, cfg.count, cfg.pilot2)
             out, mask = C.bn_apply(y, aux, res, y2, aux2, ACT[cfg.act], relu)
             if cfg.bacc is not None:
                 cfg.bacc.ensure_clean()
@@ -1146,6 +1205,15 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
         st2 = residual_bn[2] if len(residual_bn) > 2 else None
         y2 = to_nhwc(xb)
     cfg = _BNCfg(bn, bn2, act, training, N * H * W)
+    if training and bn.running_mean is not None:
+        # the producing MFMA conv(s) subtract this BN's pilot mean from their sums from now on
+        p1 = getattr(x, "_pca_stats_src", None)
+        if p1 is not None:
+            cfg.pilot = link_pilot(p1, Cc, y.device)
+        if bn2 is not None and bn2.running_mean is not None:
+            p2 = getattr(residual_bn[1], "_pca_stats_src", None)
+            if p2 is not None:
+                cfg.pilot2 = link_pilot(p2, Cc, y.device)
     if _FUSE_BN_BWD and torch.is_grad_enabled() and training:
         cfg.src = True                # request: forward replaces it with the _BNSrc record
     if training and acc_enabled(Cc, y.device) and \

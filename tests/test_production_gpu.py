@@ -64,7 +64,8 @@ def _zero(model, arena=None):
 
 
 @pytest.mark.parametrize("name,batch,factor", [("ResNet18", 1024, 3.0), ("ResNet18", 128, 3.0),
-                                               ("MobileNetV2", 128, 3.0),
+                                               ("MobileNetV2", 1024, 3.0), ("MobileNetV2", 128, 3.0),
+                                               ("EfficientNetB0", 1024, 3.0),
                                                ("EfficientNetB0", 128, 3.0)])
 def test_production_step_matches_fp32(name, batch, factor):
     from pytorch_cifar_amd import models
@@ -95,27 +96,15 @@ def test_production_step_matches_fp32(name, batch, factor):
     assert e_n <= factor * e_s + 0.02, f"logits: native {e_n:.4f} vs stock-bf16 {e_s:.4f}"
     gr = dict(ref.named_parameters())
     gs = dict(stock.named_parameters())
-    norms = sorted(p.grad.norm().item() for p in gr.values() if p.grad is not None)
-    scale = norms[len(norms) // 2]
-
-    def se(n):
-        return ".se." in n or ".fc1." in n or ".fc2." in n
-
+    # Every parameter gradient on its own scale: the relative error against the fp32 gradient of
+    # that same tensor (its own norm), within `factor` of what stock bf16 gets on that tensor.
+    # (No escape for tensors with small gradients: late BN beta/gamma and SE biases are checked
+    # like everything else.)
     errs = {n: (rel(p.grad, gr[n].grad), rel(gs[n].grad, gr[n].grad))
             for n, p in native.named_parameters() if gr[n].grad is not None}
-    floor = {k: sorted(e[1] for n, e in errs.items() if se(n) == k) for k in (True, False)}
-    floor = {k: (v[len(v) // 2] if v else 0.0) for k, v in floor.items()}
-    bad = []
-    for n, p in native.named_parameters():
-        if gr[n].grad is None:
-            continue
-        en, es = errs[n]
-        if se(n):
-            es = max(es, floor[True])
-        small = (p.grad.float() - gr[n].grad.float()).norm().item() <= 0.02 * scale
-        if en > factor * es + 0.03 and not small:
-            bad.append((n, round(en, 4), round(es, 4)))
-    assert not bad, f"{name} bs{batch}: grads worse than stock bf16 (name, native, stock): {bad[:8]}"
+    bad = [(n, round(en, 4), round(es, 4)) for n, (en, es) in errs.items()
+           if en > factor * es + 0.03]
+    assert not bad, f"{name} bs{batch}: grads worse than stock bf16 (name, native, stock): {bad[:12]}"
     bs = dict(stock.named_buffers())
     for (n, br), (_, bn) in zip(ref.named_buffers(), native.named_buffers()):
         if br.dtype.is_floating_point:
