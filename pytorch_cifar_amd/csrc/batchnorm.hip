@@ -310,7 +310,9 @@ __device__ __forceinline__ void compute_dz(const bf16* dout, const bf16* out, co
 // sees only a few rows: a guarded / loop-carried chain of them (and branchy per-element loads
 // of the constants) left the kernel latency-bound at ~10 us whatever the size.
 constexpr int kBwdRows = 4;
-template <bool MASK, bool SWISH>
+// RA: activation derivative recomputed from y and aux scale | shift (0 none, ACT_SWISH,
+// ACT_RELU_Y)
+template <bool MASK, int RA>
 __device__ __forceinline__ void bwd_reduce_rows(const bf16* __restrict__ dout,
                                                 const bf16* __restrict__ y,
                                                 const uint8_t* __restrict__ mask,
@@ -337,7 +339,7 @@ __device__ __forceinline__ void bwd_reduce_rows(const bf16* __restrict__ dout,
   mean[4] = m1.x; mean[5] = m1.y; mean[6] = m1.z; mean[7] = m1.w;
   istd[0] = i0.x; istd[1] = i0.y; istd[2] = i0.z; istd[3] = i0.w;
   istd[4] = i1.x; istd[5] = i1.y; istd[6] = i1.z; istd[7] = i1.w;
-  if constexpr (SWISH) {
+  if constexpr (RA != 0) {
     const float4 s0 = a4[2 * q], s1 = a4[2 * q + 1], h0 = a4[3 * q], h1 = a4[3 * q + 1];
     sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
     sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
@@ -352,7 +354,7 @@ __device__ __forceinline__ void bwd_reduce_rows(const bf16* __restrict__ dout,
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
       float a = ((mr[k] >> v) & 1u) ? dz[v] * wgt[k] : 0.f;
-      if constexpr (SWISH) a *= act_grad(yy[v] * sc[v] + sh[v], ACT_SWISH);
+      if constexpr (RA != 0) a *= act_grad(yy[v] * sc[v] + sh[v], RA);
       acc[0][v] += a;
       acc[1][v] += a * (yy[v] - mean[v]) * istd[v];
     }
@@ -395,13 +397,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         // masked-ReLU / no-act / swish fast path (bwd_reduce_rows)
         if (mask)
           for (; r < r1; r += kBwdRows * rp.RPP)
-            bwd_reduce_rows<true, false>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+            bwd_reduce_rows<true, 0>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
         else if (act == ACT_SWISH)
           for (; r < r1; r += kBwdRows * rp.RPP)
-            bwd_reduce_rows<false, true>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+            bwd_reduce_rows<false, ACT_SWISH>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+        else if (act == ACT_RELU_Y)
+          for (; r < r1; r += kBwdRows * rp.RPP)
+            bwd_reduce_rows<false, ACT_RELU_Y>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
         else if (act == ACT_NONE)
           for (; r < r1; r += kBwdRows * rp.RPP)
-            bwd_reduce_rows<false, false>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+            bwd_reduce_rows<false, 0>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
       }
       for (; r < r1; r += rp.RPP) {
         const size_t e = (size_t)r * C + c0;
@@ -613,7 +618,8 @@ __global__ __launch_bounds__(256) void bn_apply_rows_kernel(
                                      out, mask);
 }
 
-// KIND: 0 = no activation, 1 = ReLU through the 1-bit mask, 2 = swish (z recomputed from y)
+// KIND: 0 = no activation, 1 = ReLU through the 1-bit mask, 2 = swish (z recomputed from y),
+// 3 = ReLU with the sign recomputed from y (ACT_RELU_Y)
 // `coef` = [3|6][C] affine coefficients in global memory or LDS (fused-finalize kernel below)
 template <bool RES, bool DUAL, int KIND>
 __device__ __forceinline__ void bn_bwd_apply_rows_body(
@@ -629,7 +635,7 @@ __device__ __forceinline__ void bn_bwd_apply_rows_body(
   float ca[8], cb[8], cd[8], ca2[8], cb2[8], cd2[8], zs[8], zb[8];
 #pragma unroll
   for (int v = 0; v < 8; ++v) {
-    if constexpr (KIND == 2) {
+    if constexpr (KIND == 2 || KIND == 3) {
       zs[v] = aux[2 * C + c0 + v];
       zb[v] = aux[3 * C + c0 + v];
     }
@@ -665,9 +671,10 @@ __device__ __forceinline__ void bn_bwd_apply_rows_body(
 #pragma unroll
         for (int v = 0; v < 8; ++v) dz[v] = ((vm[u] >> v) & 1u) ? dz[v] : 0.f;
       }
-      if constexpr (KIND == 2) {
+      if constexpr (KIND == 2 || KIND == 3) {
 #pragma unroll
-        for (int v = 0; v < 8; ++v) dz[v] *= act_grad(yy[v] * zs[v] + zb[v], ACT_SWISH);
+        for (int v = 0; v < 8; ++v)
+          dz[v] *= act_grad(yy[v] * zs[v] + zb[v], KIND == 2 ? ACT_SWISH : ACT_RELU_Y);
       }
 #pragma unroll
       for (int v = 0; v < 8; ++v) o[v] = ca[v] * dz[v] + cb[v] * yy[v] + cd[v];
@@ -998,7 +1005,8 @@ void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask,
                          bf16* dy, bf16* dres, const bf16* y2, bf16* dy2, hipStream_t st) {
   const bool masked = act == ACT_RELU && mask != nullptr;
   const bool swish = act == ACT_SWISH && !dres && !y2;
-  if (rows_enabled() && C % 8 == 0 && C <= 2048 && (masked || act == ACT_NONE || swish)) {
+  const bool relu_y = act == ACT_RELU_Y && !dres && !y2;
+  if (rows_enabled() && C % 8 == 0 && C <= 2048 && (masked || act == ACT_NONE || swish || relu_y)) {
     const int M = (int)(total / C);
     const dim3 gr(rows_grid(M, C)), bl(256);
 #define PCA_BWD(R, D, K) \
@@ -1010,6 +1018,8 @@ void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask,
       else PCA_BWD(false, false, 1);
     } else if (swish) {
       PCA_BWD(false, false, 2);
+    } else if (relu_y) {
+      PCA_BWD(false, false, 3);
     } else {
       if (dres && y2) PCA_BWD(true, true, 0);
       else if (dres) PCA_BWD(true, false, 0);

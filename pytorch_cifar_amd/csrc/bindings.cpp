@@ -179,6 +179,15 @@ void dw_fwd_launch(const bf16*, const float*, int, int, int, int, int, int, int,
 void dw_dgrad_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int, int,
                      int, bf16*, hipStream_t);
 int dw_wgrad_partials(int, int, int);
+bool dw_in_supported(int N, int H, int W, int C, int Ho, int Wo, int Co, int KH, int KW, int s,
+                     int p, int act);
+void dw_fwd_in_launch(const bf16* x, const float* wT, int N, int H, int W, int C, int Ho, int Wo,
+                      int Co, int KH, int KW, int s, int p, const float* isc, const float* ish,
+                      int act, bf16* y, hipStream_t st);
+void dw_wgrad_in_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, int Ho, int Wo,
+                        int Co, int KH, int KW, int s, int p, const float* isc, const float* ish,
+                        int act, float* partial, int chunks, int accum, float* dw,
+                        hipStream_t st);
 bool dw_fwd_stats_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int,
                          int, int, bf16*, float*, int, hipStream_t);
 bool dw_dgrad_bn_launch(const bf16*, const float*, int, int, int, int, int, int, int, int, int,
@@ -978,11 +987,18 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
     dbeta2 = pick(dbeta2_acc);
   }
   auto coef = at::empty({dual ? 6 : 3, C}, fopt);
+  // (the finalize's block 0 also clears the forward accumulators this BN consumed, if any)
+  const bool nz1 = zero1.has_value() && zero1->defined();
+  const bool nz2 = zero2.has_value() && zero2->defined();
+  if (nz1) check_f32(*zero1, "zero1");
+  if (nz2) check_f32(*zero2, "zero2");
   pca::bn_bwd_finalize_launch(stat, R, NS, C, (float)M, ptr<float>(aux), optr<float>(gamma),
                               optr<float>(aux2), optr<float>(gamma2), training ? 1 : 0,
                               ptr<float>(dgamma), ptr<float>(dbeta),
                               dual ? ptr<float>(dgamma2) : nullptr,
-                              dual ? ptr<float>(dbeta2) : nullptr, ptr<float>(coef), 1, st);
+                              dual ? ptr<float>(dbeta2) : nullptr, ptr<float>(coef), 1, st,
+                              nz1 ? ptr<float>(*zero1) : nullptr, nz1 ? (int)zero1->numel() : 0,
+                              nz2 ? ptr<float>(*zero2) : nullptr, nz2 ? (int)zero2->numel() : 0);
   auto dy = at::empty_like(y);
   Tensor dres, dy2;
   if (need_dres) dres = at::empty_like(y);
@@ -1647,6 +1663,59 @@ std::vector<Tensor> dw_dgrad_bn(const Tensor& dy, const Tensor& wT, int H, int W
   return {dx, at::full({1}, ok ? 1 : 0, dy.options().dtype(at::kInt).device(at::kCPU))};
 }
 
+// ---- depthwise with the producer BN(+act) applied on the input loads (the BN output is never
+// written): y = the BN input, aux = its [mean | istd | scale | shift] rows, act 1 relu / 2 swish
+bool dw_in_supported_t(const Tensor& y, int Co, int KH, int KW, int stride, int pad, int act) {
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  return pca::dw_in_supported(N, H, W, C, out_dim(H, KH, stride, pad), out_dim(W, KW, stride, pad),
+                              Co, KH, KW, stride, pad, act);
+}
+
+Tensor dw_fwd_in(const Tensor& y, const Tensor& wT, int KH, int KW, int stride, int pad,
+                 const Tensor& aux, int act) {
+  check_bf16(y, "y");
+  check_f32(wT, "wT");
+  check_f32(aux, "aux");
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  const int Co = wT.size(1);
+  TORCH_CHECK(wT.size(0) == KH * KW && Co == C, "depthwise (multiplier 1) weight shape");
+  TORCH_CHECK(aux.numel() >= 4 * C, "aux [mean|istd|scale|shift][C]");
+  const int Ho = out_dim(H, KH, stride, pad), Wo = out_dim(W, KW, stride, pad);
+  TORCH_CHECK(pca::dw_in_supported(N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad, act),
+              "dw_fwd_in: unsupported geometry / activation");
+  auto out = at::empty({N, Ho, Wo, Co}, y.options());
+  const float* a = ptr<float>(aux);
+  pca::dw_fwd_in_launch(ptr<bf16>(y), ptr<float>(wT), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad,
+                        a + 2 * C, a + 3 * C, act, ptr<bf16>(out), cur_stream());
+  return out;
+}
+
+Tensor dw_wgrad_in(const Tensor& y, const Tensor& dy, int KH, int KW, int stride, int pad,
+                   const Tensor& aux, int act, const optional<Tensor>& accum) {
+  check_bf16(y, "y");
+  check_bf16(dy, "dy");
+  check_f32(aux, "aux");
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo, "geometry");
+  TORCH_CHECK(pca::dw_in_supported(N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad, act),
+              "dw_wgrad_in: unsupported geometry / activation");
+  TORCH_CHECK(aux.numel() >= 4 * C, "aux [mean|istd|scale|shift][C]");
+  const int chunks = pca::dw_wgrad_partials(N, Ho, Wo);
+  auto fopt = y.options().dtype(at::kFloat);
+  auto partial = at::empty({chunks, KH * KW, Co}, fopt);
+  const bool acc = accum.has_value() && accum->defined();
+  Tensor dw = acc ? *accum : at::empty({Co, KH * KW}, fopt);
+  if (acc)
+    TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.is_contiguous() && dw.numel() == (int64_t)Co * KH * KW,
+                "dw_wgrad_in: accum must be a contiguous fp32 [Co*KH*KW] tensor");
+  const float* a = ptr<float>(aux);
+  pca::dw_wgrad_in_launch(ptr<bf16>(y), ptr<bf16>(dy), N, H, W, C, Ho, Wo, Co, KH, KW, stride, pad,
+                          a + 2 * C, a + 3 * C, act, ptr<float>(partial), chunks, acc ? 1 : 0,
+                          ptr<float>(dw), cur_stream());
+  return dw;
+}
+
 // returns dw fp32 [Cout, KH*KW]
 // dW [Co, KH*KW] fp32; with `accum` given (fp32, Co*KH*KW contiguous, e.g. the parameter's view
 // of the gradient arena) the result is added into it by the final reduce and `accum` returned
@@ -1856,6 +1925,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("act_bwd", &act_bwd);
   m.def("add_act", &add_act);
   m.def("dw_fwd", &dw_fwd);
+  m.def("dw_in_supported", &dw_in_supported_t);
+  m.def("dw_fwd_in", &dw_fwd_in, "depthwise conv of act(BN(y)) with the BN applied on the loads");
+  m.def("dw_wgrad_in", &dw_wgrad_in, py::arg("y"), py::arg("dy"), py::arg("KH"), py::arg("KW"),
+        py::arg("stride"), py::arg("pad"), py::arg("aux"), py::arg("act"),
+        py::arg("accum") = py::none());
   m.def("dw_dgrad", &dw_dgrad);
   m.def("dw_wgrad", &dw_wgrad, py::arg("x"), py::arg("dy"), py::arg("KH"), py::arg("KW"),
         py::arg("stride"), py::arg("pad"), py::arg("accum") = py::none());

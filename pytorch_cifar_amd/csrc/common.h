@@ -118,12 +118,15 @@ __device__ __forceinline__ void stat_krow(float* base, int shards, size_t rowlen
     for (int c = threadIdx.x; c < C; c += blockDim.x) base[(size_t)shards * rowlen + c] = k[c];
 }
 
-enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_SIGMOID = 3 };
+// ACT_RELU_Y: ReLU whose backward recomputes the sign from the BN input (z = y*scale + shift)
+// instead of a stored mask / output — the BN output of a depthwise consumer that applies the BN
+// on its loads (dwconv.hip "input transform") is never written
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_SIGMOID = 3, ACT_RELU_Y = 4 };
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
 __device__ __forceinline__ float apply_act(float v, int act) {
-  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  if (act == ACT_RELU || act == ACT_RELU_Y) return fmaxf(v, 0.f);
   if (act == ACT_SWISH) return v * sigmoidf_(v);
   if (act == ACT_SIGMOID) return sigmoidf_(v);
   return v;
@@ -131,7 +134,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 
 // d act(z)/dz evaluated from the pre-activation z.
 __device__ __forceinline__ float act_grad(float z, int act) {
-  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_RELU || act == ACT_RELU_Y) return z > 0.f ? 1.f : 0.f;
   if (act == ACT_SWISH) {
     const float s = sigmoidf_(z);
     return s * (1.f + z * (1.f - s));

@@ -44,6 +44,7 @@ struct HxGeom {
   const bf16* bn_y2;
   const float* bn_aux2;
   const float* kshift;   // forward stats: per-channel shift K (common.h stat_shift), or nullptr
+  int ilv;               // forward: interleaved fragment reads (hx_ilv_enabled)
 };
 
 // dgrad: prefetch the fused BN reduce's y during the last tap (true) or load it at the epilogue
@@ -52,6 +53,15 @@ struct HxGeom {
 #define PCA_HX_PREFETCH_Y 0
 #endif
 constexpr bool kHxPrefetchY = PCA_HX_PREFETCH_Y != 0;
+// forward: second half's fragment reads interleaved with the first half's MFMAs (HxGeom::ilv,
+// PCA_HX_ILV=0 turns it off for A/B)
+static bool hx_ilv_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PCA_HX_ILV");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 // MODE 3 (dual-BN third sum) is compiled out: its 48 per-lane sums spill the 8-wave variants
 // (180+ registers); the dual-BN block-tail dgrads stay on the generic igemm
 constexpr bool kHxDual = false;
@@ -288,9 +298,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
         // tap (kh, kw) reads halo row offset kh*(W+2) + kw; the 2x2 stride-2 dgrad taps are the
         // dY pixels (y, x) .. (y+1, x+1): halo offsets 1..2
         const int toff = KS == 3 ? (tap / 3) * W2 + (tap % 3) : (1 + tap / 2) * W2 + 1 + (tap % 2);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          bf16x8 fa[4], fb[4];
+        auto load_half = [&](int h, bf16x8* fa, bf16x8* fb) {
 #pragma unroll
           for (int mi = 0; mi < 4; ++mi) {
             const int R = rb[mi] + toff;
@@ -300,11 +308,38 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni)
             fb[ni] = *reinterpret_cast<const lds_bf16x8*>(lds_base + Boff + (boff[ni] ^ (h << 6)));
+        };
+        auto mfma_half = [&](const bf16x8* fa, const bf16x8* fb) {
 #pragma unroll
           for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
               acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ni], fa[mi], acc[mi][ni], 0, 0, 0);
+        };
+        if (MODE == 0 && g.ilv) {   // (wave-uniform; PCA_HX_ILV=0 selects the plain order)
+          // the second half's 8 fragment reads issued between the first half's MFMAs (one per
+          // MFMA, sched_group_barrier; conv3x3_c64.hip's per-step interleave): only the first
+          // half's reads are exposed after the tap barrier
+          bf16x8 fa[2][4], fb[2][4];
+          load_half(0, fa[0], fb[0]);
+          __builtin_amdgcn_sched_barrier(0);
+          load_half(1, fa[1], fb[1]);
+          mfma_half(fa[0], fb[0]);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_half(fa[1], fb[1]);
+        } else {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            bf16x8 fa[4], fb[4];
+            load_half(h, fa, fb);
+            mfma_half(fa, fb);
+          }
         }
       }
     }
@@ -542,6 +577,7 @@ int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf
   g.bn_y2 = mode == 1 && bn_part ? bn_y2 : nullptr;   // (accumulator mode: rows of 3 sums)
   g.bn_aux2 = g.bn_y2 ? bn_aux2 : nullptr;
   g.kshift = mode == 0 && stats ? stat_shift() : nullptr;
+  g.ilv = hx_ilv_enabled() ? 1 : 0;
   if (mode == 0) return hx_dispatch<0>(a, b, y, stats, addend, bias, g, H, st, launch);
   if (mode == 1) return hx_dispatch<1>(a, b, y, stats, addend, bias, g, H, st, launch);
   return hx_dispatch<2>(a, b, y, stats, addend, bias, g, H, st, launch);

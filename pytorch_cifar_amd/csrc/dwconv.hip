@@ -239,17 +239,48 @@ __device__ __forceinline__ typename DwVec<V>::T dw_pack(const float* f) {
   else return pack2(f[0], f[1]);
 }
 
+// Input transform (IN != 0): the kernel's input is the PRE-BatchNorm tensor y of the BN(+act)
+// that feeds this depthwise conv, and every loaded vector becomes act(y * scale + shift) — the
+// BN's output, rounded to bf16 exactly as its apply pass would store it — before it enters the
+// window; zero padding stays zero. The BN's output tensor is never written or read again
+// (mobilenetv2.py:31-35 conv1 -> bn1 -> relu -> conv2, efficientnet.py:96-98 with swish).
+template <int V, int IN>
+__device__ __forceinline__ typename DwVec<V>::T dw_in(const typename DwVec<V>::T& u,
+                                                      const float* sc, const float* sh) {
+  if constexpr (IN == 0) {
+    return u;
+  } else {
+    float f[V];
+    dw_unpack<V>(u, f);
+#pragma unroll
+    for (int v = 0; v < V; ++v) f[v] = apply_act(f[v] * sc[v] + sh[v], IN);
+    return dw_pack<V>(f);
+  }
+}
+
+// per-thread scale / shift of its V channels (IN != 0)
+template <int V, int IN>
+__device__ __forceinline__ void dw_in_coef(const float* isc, const float* ish, int c, float* sc,
+                                           float* sh) {
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    sc[v] = IN ? isc[c + v] : 1.f;
+    sh[v] = IN ? ish[c + v] : 0.f;
+  }
+}
+
 // the K vectors (kw = 0..K-1) of input row ih starting at column iw0 (zeros outside the image)
-template <int K, int V>
+template <int K, int V, int IN = 0>
 __device__ __forceinline__ void dwk_load_row(const bf16* xn, const DwGeom& g, int ih, int iw0,
-                                             typename DwVec<V>::T* r) {
+                                             typename DwVec<V>::T* r, const float* sc = nullptr,
+                                             const float* sh = nullptr) {
   using T = typename DwVec<V>::T;
   const bool rok = (unsigned)ih < (unsigned)g.H;
 #pragma unroll
   for (int kw = 0; kw < K; ++kw) {
     const int iw = iw0 + kw;
     r[kw] = (rok && (unsigned)iw < (unsigned)g.W)
-                ? *reinterpret_cast<const T*>(xn + ((size_t)ih * g.W + iw) * g.C)
+                ? dw_in<V, IN>(*reinterpret_cast<const T*>(xn + ((size_t)ih * g.W + iw) * g.C), sc, sh)
                 : dw_zero<V>();
   }
 }
@@ -263,10 +294,12 @@ __device__ __forceinline__ void dwk_roll(T (&win)[K][K]) {
     for (int kw = 0; kw < K; ++kw) win[k][kw] = win[k + S][kw];
 }
 
-template <int K, int S, int V, bool FLIP>
+template <int K, int S, int V, bool FLIP, int IN = 0>
 __global__ __launch_bounds__(256) void dwk_fwd_kernel(const bf16* __restrict__ x,
                                                       const float* __restrict__ wT, DwGeom g,
-                                                      int rpt, bf16* __restrict__ y) {
+                                                      int rpt, bf16* __restrict__ y,
+                                                      const float* __restrict__ isc = nullptr,
+                                                      const float* __restrict__ ish = nullptr) {
   using T = typename DwVec<V>::T;
   constexpr int KK = K * K;
   const int G = g.C / V;
@@ -298,14 +331,17 @@ __global__ __launch_bounds__(256) void dwk_fwd_kernel(const bf16* __restrict__ x
     const bf16* xn = x + (size_t)n * g.H * g.W * g.C + c;
     const int oh0 = strip * rpt, oh1 = min(g.Ho, oh0 + rpt);
     const int iw0 = ow * S - g.p;
+    float isv[V], ihv[V];
+    dw_in_coef<V, IN>(isc, ish, c, isv, ihv);
     T win[K][K];
 #pragma unroll
-    for (int k = 0; k < K - S; ++k) dwk_load_row<K, V>(xn, g, oh0 * S - g.p + k, iw0, win[k]);
+    for (int k = 0; k < K - S; ++k)
+      dwk_load_row<K, V, IN>(xn, g, oh0 * S - g.p + k, iw0, win[k], isv, ihv);
     bf16* yr = y + (((size_t)n * g.Ho + oh0) * g.Wo + ow) * g.Co + c;
     for (int oh = oh0; oh < oh1; ++oh) {
       const int ih0 = oh * S - g.p;
 #pragma unroll
-      for (int k = K - S; k < K; ++k) dwk_load_row<K, V>(xn, g, ih0 + k, iw0, win[k]);
+      for (int k = K - S; k < K; ++k) dwk_load_row<K, V, IN>(xn, g, ih0 + k, iw0, win[k], isv, ihv);
       float acc[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[v] = 0.f;
@@ -328,11 +364,13 @@ __global__ __launch_bounds__(256) void dwk_fwd_kernel(const bf16* __restrict__ x
 // partial[block.x][tap][Co]: block (x, y) owns channel groups [y*GB, y*GB + GB) (GB <= 256);
 // thread t owns group y*GB + t % GB and walks the column strips item = x*W + t/GB (+ gridDim.x*W
 // ...), W = 256 / GB workers per group
-template <int K, int S, int V>
+template <int K, int S, int V, int IN = 0>
 __global__ __launch_bounds__(256) void dwk_wgrad_kernel(const bf16* __restrict__ x,
                                                         const bf16* __restrict__ dy, DwGeom g,
                                                         int rpt, int GB,
-                                                        float* __restrict__ partial) {
+                                                        float* __restrict__ partial,
+                                                        const float* __restrict__ isc = nullptr,
+                                                        const float* __restrict__ ish = nullptr) {
   using T = typename DwVec<V>::T;
   constexpr int KK = K * K;
   __shared__ float red[256 * V];
@@ -358,14 +396,17 @@ __global__ __launch_bounds__(256) void dwk_wgrad_kernel(const bf16* __restrict__
       const bf16* xn = x + (size_t)n * g.H * g.W * g.C + c;
       const int oh0 = strip * rpt, oh1 = min(g.Ho, oh0 + rpt);
       const int iw0 = ow * S - g.p;
+      float isv[V], ihv[V];
+      dw_in_coef<V, IN>(isc, ish, c, isv, ihv);
       T win[K][K];
 #pragma unroll
-      for (int k = 0; k < K - S; ++k) dwk_load_row<K, V>(xn, g, oh0 * S - g.p + k, iw0, win[k]);
+      for (int k = 0; k < K - S; ++k)
+        dwk_load_row<K, V, IN>(xn, g, oh0 * S - g.p + k, iw0, win[k], isv, ihv);
       const bf16* dr = dy + (((size_t)n * g.Ho + oh0) * g.Wo + ow) * g.Co + c;
       for (int oh = oh0; oh < oh1; ++oh) {
         const int ih0 = oh * S - g.p;
 #pragma unroll
-        for (int k = K - S; k < K; ++k) dwk_load_row<K, V>(xn, g, ih0 + k, iw0, win[k]);
+        for (int k = K - S; k < K; ++k) dwk_load_row<K, V, IN>(xn, g, ih0 + k, iw0, win[k], isv, ihv);
         float d[V];
         dw_unpack<V>(*reinterpret_cast<const T*>(dr), d);
         dr += (size_t)g.Wo * g.Co;
@@ -749,47 +790,49 @@ static int dwk_vec(int kind, int C) {
 
 static int dwk_rpt(int Ho) { return Ho < 8 ? Ho : 8; }
 
-template <int K, int V>
+template <int K, int V, int IN = 0>
 static void dwk_fwd_t(const bf16* x, const float* wT, const DwGeom& g, bool flip, bf16* y,
-                      hipStream_t st) {
+                      hipStream_t st, const float* isc = nullptr, const float* ish = nullptr) {
   const int rpt = dwk_rpt(g.Ho);
   const size_t work = (size_t)g.N * cdiv(g.Ho, rpt) * g.Wo * (g.C / V);
   const dim3 grid(gcap(work)), block(256);
   if (g.s == 1) {
-    if (flip) hipLaunchKernelGGL((dwk_fwd_kernel<K, 1, V, true>), grid, block, 0, st, x, wT, g, rpt, y);
-    else hipLaunchKernelGGL((dwk_fwd_kernel<K, 1, V, false>), grid, block, 0, st, x, wT, g, rpt, y);
+    if (flip) hipLaunchKernelGGL((dwk_fwd_kernel<K, 1, V, true>), grid, block, 0, st, x, wT, g, rpt, y, nullptr, nullptr);
+    else hipLaunchKernelGGL((dwk_fwd_kernel<K, 1, V, false, IN>), grid, block, 0, st, x, wT, g, rpt, y, isc, ish);
   } else {
-    hipLaunchKernelGGL((dwk_fwd_kernel<K, 2, V, false>), grid, block, 0, st, x, wT, g, rpt, y);
+    hipLaunchKernelGGL((dwk_fwd_kernel<K, 2, V, false, IN>), grid, block, 0, st, x, wT, g, rpt, y, isc, ish);
   }
 }
 
+template <int IN = 0>
 static void dwk_fwd(int kind, const bf16* x, const float* wT, const DwGeom& g, bool flip, bf16* y,
-                    hipStream_t st) {
+                    hipStream_t st, const float* isc = nullptr, const float* ish = nullptr) {
   const int v = dwk_vec(kind, g.C);
   if (kind == 3) {
-    if (v == 8) dwk_fwd_t<3, 8>(x, wT, g, flip, y, st);
-    else if (v == 4) dwk_fwd_t<3, 4>(x, wT, g, flip, y, st);
-    else dwk_fwd_t<3, 2>(x, wT, g, flip, y, st);
+    if (v == 8) dwk_fwd_t<3, 8, IN>(x, wT, g, flip, y, st, isc, ish);
+    else if (v == 4) dwk_fwd_t<3, 4, IN>(x, wT, g, flip, y, st, isc, ish);
+    else dwk_fwd_t<3, 2, IN>(x, wT, g, flip, y, st, isc, ish);
   } else if (kind == 5) {
-    if (v == 4) dwk_fwd_t<5, 4>(x, wT, g, flip, y, st);
-    else dwk_fwd_t<5, 2>(x, wT, g, flip, y, st);
+    if (v == 4) dwk_fwd_t<5, 4, IN>(x, wT, g, flip, y, st, isc, ish);
+    else dwk_fwd_t<5, 2, IN>(x, wT, g, flip, y, st, isc, ish);
   } else {
-    dwk_fwd_t<7, 2>(x, wT, g, flip, y, st);
+    dwk_fwd_t<7, 2, IN>(x, wT, g, flip, y, st, isc, ish);
   }
 }
 
-template <int K, int V>
+template <int K, int V, int IN = 0>
 static void dwk_wgrad_t(const bf16* x, const bf16* dy, const DwGeom& g, int chunks,
-                        float* partial, hipStream_t st) {
+                        float* partial, hipStream_t st, const float* isc = nullptr,
+                        const float* ish = nullptr) {
   const int G = g.Co / V;
   const int ny = cdiv(G, 256);
   const int GB = cdiv(G, ny);
   const int rpt = dwk_rpt(g.Ho);
   const dim3 grid(chunks, ny), block(256);
   if (g.s == 1)
-    hipLaunchKernelGGL((dwk_wgrad_kernel<K, 1, V>), grid, block, 0, st, x, dy, g, rpt, GB, partial);
+    hipLaunchKernelGGL((dwk_wgrad_kernel<K, 1, V, IN>), grid, block, 0, st, x, dy, g, rpt, GB, partial, isc, ish);
   else
-    hipLaunchKernelGGL((dwk_wgrad_kernel<K, 2, V>), grid, block, 0, st, x, dy, g, rpt, GB, partial);
+    hipLaunchKernelGGL((dwk_wgrad_kernel<K, 2, V, IN>), grid, block, 0, st, x, dy, g, rpt, GB, partial, isc, ish);
 }
 
 // k3 with 8-channel groups
@@ -855,6 +898,48 @@ bool dw_dgrad_bn_launch(const bf16* dy, const float* wT, int N, int H, int W, in
   if (act == 1) hipLaunchKernelGGL((dwk_epi_s2_kernel<3, 2>), grid, block, 0, st, dy, wT, g, dx, e);
   else hipLaunchKernelGGL((dwk_epi_s2_kernel<3, 3>), grid, block, 0, st, dy, wT, g, dx, e);
   return true;
+}
+
+// ---- depthwise conv with the producer BN(+act) applied on its input loads (IN transform) ----
+// supported: the k3 / k5 / k7 fast paths, multiplier 1 (the mobile zoo's depthwise convs)
+bool dw_in_supported(int N, int H, int W, int C, int Ho, int Wo, int Co, int KH, int KW, int s,
+                     int p, int act) {
+  DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
+  return dwk_kind(g) != 0 && g.mult == 1 && (act == ACT_RELU || act == ACT_SWISH);
+}
+
+// x is the BN input y; isc / ish = that BN's scale / shift rows (aux rows 2 and 3)
+void dw_fwd_in_launch(const bf16* x, const float* wT, int N, int H, int W, int C, int Ho, int Wo,
+                      int Co, int KH, int KW, int s, int p, const float* isc, const float* ish,
+                      int act, bf16* y, hipStream_t st) {
+  DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
+  const int kind = dwk_kind(g);
+  if (act == ACT_SWISH) dwk_fwd<ACT_SWISH>(kind, x, wT, g, false, y, st, isc, ish);
+  else dwk_fwd<ACT_RELU>(kind, x, wT, g, false, y, st, isc, ish);
+}
+
+void dw_wgrad_in_launch(const bf16* x, const bf16* dy, int N, int H, int W, int C, int Ho, int Wo,
+                        int Co, int KH, int KW, int s, int p, const float* isc, const float* ish,
+                        int act, float* partial, int chunks, int accum, float* dw,
+                        hipStream_t st) {
+  DwGeom g = dwg(N, H, W, C, Ho, Wo, Co, KH, KW, s, p);
+  const int kind = dwk_kind(g);
+  const int T = KH * KW;
+  const int v = dwk_vec(kind, Co);
+#define PCA_DWIN(K_, V_)                                                                  \
+  do {                                                                                    \
+    if (act == ACT_SWISH) dwk_wgrad_t<K_, V_, ACT_SWISH>(x, dy, g, chunks, partial, st, isc, ish); \
+    else dwk_wgrad_t<K_, V_, ACT_RELU>(x, dy, g, chunks, partial, st, isc, ish);          \
+  } while (0)
+  if (kind == 3 && v == 8) PCA_DWIN(3, 8);
+  else if (kind == 3 && v == 4) PCA_DWIN(3, 4);
+  else if (kind == 3) PCA_DWIN(3, 2);
+  else if (kind == 5 && v == 4) PCA_DWIN(5, 4);
+  else if (kind == 5) PCA_DWIN(5, 2);
+  else PCA_DWIN(7, 2);
+#undef PCA_DWIN
+  hipLaunchKernelGGL(dw_wgrad_final4_kernel, dim3(cdiv(T * Co, 32)), dim3(256), 0, st, partial,
+                     chunks, T, Co, dw, accum);
 }
 
 void dw_fwd_launch(const bf16* x, const float* wT, int N, int H, int W, int C, int Ho, int Wo,

@@ -56,8 +56,10 @@ class Block(tnn.Module):
         self.has_skip = (stride == 1) and (in_channels == out_channels)
 
     def forward(self, x):
-        out = x if self.expand_ratio == 1 else self.bn1(self.conv1(x), act="swish")
-        out = self.bn2(self.conv2(out), act="swish")
+        if self.expand_ratio == 1:
+            out = self.bn2(self.conv2(x), act="swish")
+        else:   # bn1 + swish applied inside the depthwise conv2's loads
+            out = self.bn2(F.bn_act_dwconv(self.bn1, self.conv1(x), "swish", self.conv2), act="swish")
         out = self.se(out)
         y = self.conv3(out)
         if self.has_skip:

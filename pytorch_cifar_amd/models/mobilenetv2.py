@@ -1,7 +1,9 @@
 """MobileNetV2, CIFAR strides (parity: reference models/mobilenetv2.py:11-77).
 
 Inverted residual: expand 1x1 (+BN+ReLU) -> depthwise 3x3 (+BN+ReLU) -> project 1x1 + BN, and
-for stride 1 the residual (identity or 1x1 conv+BN) is folded into the projection BN pass."""
+for stride 1 the residual (identity or 1x1 conv+BN) is folded into the projection BN pass. The
+expand BN + ReLU is applied on the depthwise kernel's input loads (ops.functional.bn_act_dwconv):
+the expanded activation is written once (pre-BN) instead of twice."""
 import torch.nn as tnn
 
 from ..nn import BatchNorm2d, Conv2d, Linear, Sequential
@@ -29,8 +31,9 @@ class Block(tnn.Module):
                 BatchNorm2d(out_planes))
 
     def forward(self, x):
-        out = self.bn1(self.conv1(x), act="relu")
-        out = self.bn2(self.conv2(out), act="relu")
+        # bn1 + ReLU applied inside the depthwise conv2's loads (its output is never written)
+        out = F.bn_act_dwconv(self.bn1, self.conv1(x), "relu", self.conv2)
+        out = self.bn2(out, act="relu")
         if self.stride == 1:
             return self.bn3(self.conv3(out), **shortcut_kwargs(self.shortcut, x))
         return self.bn3(self.conv3(out))

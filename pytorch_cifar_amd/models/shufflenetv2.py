@@ -43,8 +43,7 @@ class BasicBlock(tnn.Module):
 
     def forward(self, x):
         x1, x2 = self.split(x)
-        out = self.bn1(self.conv1(x2), act="relu")
-        out = self.bn2(self.conv2(out))
+        out = self.bn2(F.bn_act_dwconv(self.bn1, self.conv1(x2), "relu", self.conv2))
         out = self.bn3(self.conv3(out), act="relu")
         return self._join(x1, out)
 
@@ -73,8 +72,8 @@ class DownBlock(tnn.Module):
 
     def forward(self, x):
         left = self.bn2(self.conv2(self.bn1(self.conv1(x))), act="relu")
-        right = self.bn3(self.conv3(x), act="relu")
-        right = self.bn5(self.conv5(self.bn4(self.conv4(right))), act="relu")
+        right = self.bn4(F.bn_act_dwconv(self.bn3, self.conv3(x), "relu", self.conv4))
+        right = self.bn5(self.conv5(right), act="relu")
         if self.shuffle.groups == 2 and left.shape == right.shape:
             return F.cat_shuffle2(left, right)
         return self.shuffle(F.cat([left, right], 1))

@@ -9,6 +9,7 @@ from ..ops.functional import (  # noqa: F401
     adaptive_avg_pool2d,
     add_act,
     avg_pool2d,
+    bn_act_dwconv,
     cat,
     cat_shuffle2,
     channel_shuffle,

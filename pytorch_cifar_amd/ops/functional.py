@@ -1244,6 +1244,121 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
     return v
 
 
+# ------------------------------------------- BN(+act) applied inside the depthwise consumer
+# act(BN(y)) -> depthwise conv as ONE node (mobilenetv2.py:31-35 conv1 -> bn1 -> relu -> conv2,
+# efficientnet.py:96-98 with swish, mobilenet.py's pointwise BN -> next block's depthwise): the
+# BN's batch statistics are folded by one small finalize launch, and its affine + activation are
+# applied on the depthwise kernels' input loads (csrc/dwconv.hip "input transform") — in the
+# forward and again in the weight gradient — so the BN output is never written, and read back by
+# neither. The backward recomputes the activation derivative from y (ACT_RELU_Y / swish from the
+# aux scale | shift) instead of a stored mask, reduces the BN-backward sums of the depthwise
+# dgrad's output and applies them in one pass (whose finalize also clears the forward
+# accumulator the BN consumed). PCA_DW_IN_FUSE=0: the separate BN apply pass + plain depthwise.
+_DW_IN_FUSE = os.environ.get("PCA_DW_IN_FUSE", "1") != "0"
+_ACT_RELU_Y = 4
+
+
+class _BNActDW(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, gamma, beta, weight, stats, cfg, stride, padding):
+        C = _C()
+        bn = cfg.bn
+        aux = _bn_aux(C, bn, y, stats, cfg.training, cfg.count, cfg.pilot)
+        cfg.faccs = (stats,) if isinstance(stats, StatAcc) else ()
+        KH, KW = weight.shape[2], weight.shape[3]
+        wT = _dw_weight(weight)
+        out = C.dw_fwd_in(y, wT, KH, KW, stride, padding, aux, ACT[cfg.act])
+        ctx.save_for_backward(y, wT, aux)
+        ctx.cfg = cfg
+        ctx.geom = (stride, padding, KH, KW)
+        ctx.weight = weight
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = _C()
+        y, wT, aux = ctx.saved_tensors
+        cfg, bn = ctx.cfg, ctx.cfg.bn
+        stride, padding, KH, KW = ctx.geom
+        dout = dout.contiguous()
+        H, W, Cx = y.shape[1], y.shape[2], y.shape[3]
+        act = ACT[cfg.act]
+        w = ctx.weight
+        dw_ret = None
+        if w.requires_grad:
+            buf = G.grad_buffer(w) if w.is_leaf else None
+            if buf is not None and buf.is_contiguous():
+                C.dw_wgrad_in(y, dout, KH, KW, stride, padding, aux, act, buf.view(-1))
+                G.fire(w)
+            else:
+                dwt = C.dw_wgrad_in(y, dout, KH, KW, stride, padding, aux, act)
+                if w.is_leaf:
+                    G.accumulate(w, dwt.view(w.shape[0], KH, KW, 1))
+                else:
+                    dw_ret = dwt.view(w.shape)
+        # gradient w.r.t. act(BN(y)), then the BN(+act) backward with the derivative from y
+        dz = C.dw_dgrad(dout, wT, H, W, Cx, KH, KW, stride, padding)
+
+        def acc(p):
+            if p is None or not p.requires_grad or not p.is_leaf:
+                return None
+            return G.grad_buffer(p)
+
+        g1, b1 = acc(bn.weight), acc(bn.bias)
+        zero1 = None
+        for fa in cfg.faccs:
+            if fa.state == "used":
+                zero1 = fa.buf            # cleared by the backward finalize's block 0
+                fa.state = "clean"
+        cfg.faccs = ()
+        dy, _, _, dg, db, _, _ = C.bn_backward(
+            dz, None, None, y, aux, bn.weight.detach() if bn.weight is not None else None,
+            None, None, None, _ACT_RELU_Y if act == 1 else act,
+            cfg.training or bn.running_mean is None, False, g1, b1, None, None, None, None, 0,
+            False, zero1, None)
+        ret = {}
+        for p, buf, val, slot in ((bn.weight, g1, dg, 1), (bn.bias, b1, db, 2)):
+            if p is None or not p.requires_grad:
+                continue
+            if not p.is_leaf:
+                ret[slot] = val
+            elif buf is not None:
+                G.fire(p)
+            else:
+                G.accumulate(p, val)
+        return dy, ret.get(1), ret.get(2), dw_ret, None, None, None, None
+
+
+def bn_act_dwconv(bn, x, act, conv):
+    """``conv(act(bn(x)))`` for a depthwise ``conv`` (groups == channels, multiplier 1, no bias):
+    one fused node on the GPU (BN applied on the depthwise kernels' loads), the plain composition
+    elsewhere (CPU reference path, unsupported geometry / activation, PCA_DW_IN_FUSE=0)."""
+    Cc = x.shape[1]
+    ks, st, pd = conv.kernel_size, conv.stride, conv.padding
+    simple = (conv.groups == Cc and conv.out_channels == Cc and conv.bias is None
+              and ks[0] == ks[1] and st[0] == st[1] and pd[0] == pd[1])
+    if (not _DW_IN_FUSE or _ref(x) or not simple or act not in ("relu", "swish", "silu")
+            or bn.running_mean is None or torch.is_autocast_enabled() or Cc % 8
+            or not _C().dw_in_supported(to_nhwc(x), Cc, ks[0], ks[1], st[0], pd[0], ACT[act])):
+        return conv(bn(x, act=act))
+    training = bn.training
+    stats = getattr(x, "_pca_stats", None) if training else None
+    y = to_nhwc(x)
+    N, _, H, W = x.shape
+    cfg = _BNCfg(bn, None, act, training, N * H * W)
+    if training:
+        p1 = getattr(x, "_pca_stats_src", None)
+        if p1 is not None:
+            cfg.pilot = link_pilot(p1, Cc, y.device)
+            if acc_enabled(Cc, y.device):
+                p1._pca_acc_ok = True     # the producer delivers into its accumulator from now on
+    out = _BNActDW.apply(y, bn.weight, bn.bias, conv.weight, stats, cfg, st[0], pd[0])
+    v = to_nchw(out)
+    if training:
+        v._pca_stats_src = conv
+    return v
+
+
 # ------------------------------------------------------------------------ activations
 class _Act(torch.autograd.Function):
     @staticmethod
