@@ -17,6 +17,7 @@ import os
 _lib = None
 _err: Exception | None = None
 _debug = os.environ.get("PCA_DEBUG_SYNC", "0") == "1"
+_trace = os.environ.get("PCA_DEBUG_TRACE", "0") == "1"
 
 
 class _DebugProxy:
@@ -34,6 +35,12 @@ class _DebugProxy:
         def wrapped(*a, **k):
             import torch
 
+            if _trace:   # PCA_DEBUG_TRACE=1: name every op before it runs (a device fault that
+                         # aborts the process then has its op on the last stderr line)
+                import sys
+
+                shapes = [tuple(x.shape) for x in a if hasattr(x, "shape")][:4]
+                print(f"[native] {name} {shapes}", file=sys.stderr, flush=True)
             out = fn(*a, **k)
             err = self._mod.last_error()
             if err:

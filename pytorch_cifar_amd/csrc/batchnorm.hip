@@ -184,10 +184,14 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     const float* __restrict__ stat, int R, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     int64_t* __restrict__ nbt, float momentum, float eps, int training, int update_running,
-    float* __restrict__ aux, const float* kin, float* pilot_out) {
+    float* __restrict__ aux, const float* kin, float* pilot_out, float* zero, int zero_n) {
   __shared__ float red[16][64][2];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
+  // block 0 clears this BN's backward accumulator (its consumer dgrad refills it later in the
+  // step; no memset launch on the separate-statistics path)
+  if (zero && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < zero_n; i += blockDim.x) zero[i] = 0.f;
   if (blockIdx.x == 0 && threadIdx.x == 0 && update_running && nbt) nbt[0] += 1;
   float s = 0.f, q = 0.f;
   if (training && c < C) {
@@ -918,10 +922,11 @@ int colsum_launch(const float* in, int R, int L, float* out, hipStream_t st) {
 void bn_finalize_launch(const float* stat, int R, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, int64_t* nbt,
                         float momentum, float eps, int training, int update_running, float* aux,
-                        hipStream_t st, const float* kin, float* pilot_out) {
+                        hipStream_t st, const float* kin, float* pilot_out, float* zero,
+                        int zero_n) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C, count,
                      gamma, beta, rmean, rvar, nbt, momentum, eps, training, update_running, aux,
-                     kin, pilot_out);
+                     kin, pilot_out, zero, zero_n);
 }
 
 void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const bf16* res,

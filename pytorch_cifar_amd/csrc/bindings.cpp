@@ -70,7 +70,8 @@ int colsum_launch(const float*, int, int, float*, hipStream_t);
 void bias_grad_fold_launch(const float*, int, int, int, float*, hipStream_t);
 void bn_finalize_launch(const float*, int, int, double, const float*, const float*, float*, float*,
                         int64_t*, float, float, int, int, float*, hipStream_t,
-                        const float* kin = nullptr, float* pilot_out = nullptr);
+                        const float* kin = nullptr, float* pilot_out = nullptr,
+                        float* zero = nullptr, int zero_n = 0);
 void bn_apply_launch(const bf16*, const float*, int, size_t, const bf16*, const bf16*,
                      const float*, int, bf16*, uint8_t*, hipStream_t);
 void bn_bwd_reduce_launch(const bf16*, const bf16*, const uint8_t*, const bf16*, const float*,
@@ -686,7 +687,7 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
                    const optional<Tensor>& beta, const Tensor& rmean, const Tensor& rvar,
                    const optional<Tensor>& nbt, double momentum, double eps, bool training,
                    bool update_running, const optional<Tensor>& kin,
-                   const optional<Tensor>& pilot_out) {
+                   const optional<Tensor>& pilot_out, const optional<Tensor>& zero) {
   const int C = rmean.numel();
   auto aux = at::empty({4, C}, rmean.options());
   const float* stat = nullptr;
@@ -717,7 +718,8 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
                           ptr<float>(rmean), ptr<float>(rvar), optr<int64_t>(nbt), (float)momentum,
                           (float)eps, training ? 1 : 0, update_running ? 1 : 0, ptr<float>(aux),
                           cur_stream(), training ? optr<float>(kin) : nullptr,
-                          training ? optr<float>(pilot_out) : nullptr);
+                          training ? optr<float>(pilot_out) : nullptr, optr<float>(zero),
+                          (zero.has_value() && zero->defined()) ? (int)zero->numel() : 0);
   return aux;
 }
 
@@ -1856,7 +1858,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize", &bn_finalize, py::arg("partial"), py::arg("count"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("momentum"),
         py::arg("eps"), py::arg("training"), py::arg("update_running"), py::arg("kin") = py::none(),
-        py::arg("pilot_out") = py::none());
+        py::arg("pilot_out") = py::none(), py::arg("zero") = py::none());
   m.def("bn_apply", &bn_apply);
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("mask"), py::arg("y"),
         py::arg("aux"), py::arg("gamma"), py::arg("y2"), py::arg("aux2"), py::arg("gamma2"),

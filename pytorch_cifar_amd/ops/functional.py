@@ -485,8 +485,13 @@ class StatAcc:
 # cancellation once K is near the batch mean, which the previous batch's mean is. The pilot
 # lives on the producing conv (persistent, so hipGraph replays see a stable address); the
 # consuming BN links it on first sight and its finalize / fold writes each batch mean into it.
+_BN_SHIFT = os.environ.get("PCA_BN_SHIFT", "1") != "0"   # 0: unshifted sums (A/B)
+
+
 def conv_pilot(conv, device):
     """The pilot tensor of ``conv`` on ``device`` (None until a BN linked it)."""
+    if not _BN_SHIFT:
+        return None
     d = conv.__dict__.get("_pca_pilot")
     if d is None:
         return None
@@ -973,12 +978,13 @@ class _BNCfg:
         self.faccs = ()       # forward StatAccs this BN consumed (cleared by its backward kernel)
 
 
-def _bn_aux(C, bn, y, stats, training, count, pilot=None, kin=None):
+def _bn_aux(C, bn, y, stats, training, count, pilot=None, kin=None, zero=None):
     """Finalize: aux [mean | invstd | scale | shift]. ``kin``: the shift the sums are of (pilot /
-    K row / centred pass); ``pilot``: receives the batch mean (the producer's next shift)."""
+    K row / centred pass); ``pilot``: receives the batch mean (the producer's next shift);
+    ``zero``: a StatAcc (this BN's backward accumulator) the finalize kernel clears."""
     if isinstance(stats, StatAcc):
         # an accumulator the fused kernel cannot consume here: finalize from its shard rows
-        aux = _bn_aux(C, bn, y, stats.slab(), training, count, pilot, stats.krow())
+        aux = _bn_aux(C, bn, y, stats.slab(), training, count, pilot, stats.krow(), zero)
         stats.state = "used"
         return aux
     use_batch = training or bn.running_mean is None
@@ -996,9 +1002,13 @@ def _bn_aux(C, bn, y, stats, training, count, pilot=None, kin=None):
     momentum = bn.momentum if bn.momentum is not None else 0.1
     w = bn.weight.detach() if bn.weight is not None else None
     b = bn.bias.detach() if bn.bias is not None else None
-    return C.bn_finalize(stats if use_batch else None, float(count), w, b, rm, rv,
-                         bn.num_batches_tracked if update else None, momentum, bn.eps, use_batch, update,
-                         kin if use_batch else None, pilot if use_batch else None)
+    aux = C.bn_finalize(stats if use_batch else None, float(count), w, b, rm, rv,
+                        bn.num_batches_tracked if update else None, momentum, bn.eps, use_batch, update,
+                        kin if use_batch else None, pilot if use_batch else None,
+                        zero.buf if zero is not None else None)
+    if zero is not None:
+        zero.state = "clean"
+    return aux
 
 
 class _BatchNormAct(torch.autograd.Function):
@@ -1044,8 +1054,9 @@ class _BatchNormAct(torch.autograd.Function):
             if mask is not None and not mask.numel():
                 mask = None
         else:
+            # (the finalize kernel's block 0 clears this BN's backward accumulator: no memset)
             aux = _bn_aux(C, bn, y, stats if isinstance(stats, StatAcc) or (stats is not None and stats.numel()) else None,
-                          cfg.training, cfg.count, cfg.pilot)
+                          cfg.training, cfg.count, cfg.pilot, zero=cfg.bacc)
             aux2 = None
             if y2 is not None:
                 aux2 = _bn_aux(C, bn2, y2, stats2 if isinstance(stats2, StatAcc) or (stats2 is not None and stats2.numel()) else None,

@@ -22,11 +22,11 @@ pytestmark = pytest.mark.gpu
 
 
 def rel(a, b):
-    a, b = a.detach().float(), b.detach().float()
+    a, b = a.detach().float(), b.detach().float().to(a.device)
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-def _step(model, x, y, mode):
+def _step(model, x, y, mode, fmt=torch.channels_last):
     from pytorch_cifar_amd.ops.functional import cross_entropy, reference_kernels
 
     if mode == "native":
@@ -35,7 +35,7 @@ def _step(model, x, y, mode):
         loss.backward()
     else:
         with reference_kernels():
-            xx = x.contiguous(memory_format=torch.channels_last)
+            xx = x.contiguous(memory_format=fmt)
             if mode == "bf16":
                 with torch.autocast("cuda", dtype=torch.bfloat16):
                     out = model(xx)
@@ -74,8 +74,14 @@ def test_production_step_matches_fp32(name, batch, factor):
     base = models.MODEL_REGISTRY[name]()
     if hasattr(base, "cfg") and isinstance(base.cfg, dict) and "dropout_rate" in base.cfg:
         base.cfg = dict(base.cfg, dropout_rate=0.0)   # identical masks are not the point here
-    ref = copy.deepcopy(base).cuda().to(memory_format=torch.channels_last)
-    stock = copy.deepcopy(base).cuda().to(memory_format=torch.channels_last)
+    # The depthwise nets at bs1024: the fp32 oracle runs on the CPU and the stock bf16 step NCHW
+    # (MIOpen's channels_last depthwise backward at that size faulted the device in round 4; the
+    # NCHW bf16 step is the one the stock comparator bench runs).
+    big_dw = batch > 128 and name != "ResNet18"
+    fmt = torch.contiguous_format if big_dw else torch.channels_last
+    ref = copy.deepcopy(base).to(memory_format=fmt)
+    ref = ref if big_dw else ref.cuda()
+    stock = copy.deepcopy(base).cuda().to(memory_format=fmt)
     native = copy.deepcopy(base).cuda()
     arena = _prep_native(native)
     for m in (ref, stock, native):
@@ -88,8 +94,12 @@ def test_production_step_matches_fp32(name, batch, factor):
         _zero(ref)
         _zero(stock)
         _zero(native, arena)
-        out_r, _ = _step(ref, x, y, "fp32")
-        out_s, _ = _step(stock, x, y, "bf16")
+        if big_dw:
+            out_r, _ = _step(ref, x.cpu(), y.cpu(), "fp32", fmt)
+            out_r = out_r.cuda()
+        else:
+            out_r, _ = _step(ref, x, y, "fp32", fmt)
+        out_s, _ = _step(stock, x, y, "bf16", fmt)
         out_n, _ = _step(native, x, y, "native")
         torch.cuda.synchronize()
     e_n, e_s = rel(out_n, out_r), rel(out_s, out_r)
@@ -109,7 +119,7 @@ def test_production_step_matches_fp32(name, batch, factor):
     for (n, br), (_, bn) in zip(ref.named_buffers(), native.named_buffers()):
         if br.dtype.is_floating_point:
             en, es = rel(bn, br), rel(bs[n], br)
-            assert en <= factor * es + 0.03 or (bn - br).abs().max().item() < 1e-4, (n, en, es)
+            assert en <= factor * es + 0.03 or (bn - br.to(bn.device)).abs().max().item() < 1e-4, (n, en, es)
 
 
 def test_resnet18_loss_trajectory_matches_stock_bf16():
