@@ -54,11 +54,11 @@ struct HxGeom {
 #endif
 constexpr bool kHxPrefetchY = PCA_HX_PREFETCH_Y != 0;
 // forward: second half's fragment reads interleaved with the first half's MFMAs (HxGeom::ilv,
-// PCA_HX_ILV=0 turns it off for A/B)
+// opt-in PCA_HX_ILV=1: measured 0.2-0.5 % slower on ResNet-18 bs1024, README "round 4")
 static bool hx_ilv_enabled() {
   static const bool on = [] {
     const char* e = getenv("PCA_HX_ILV");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -316,7 +316,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
             for (int ni = 0; ni < 4; ++ni)
               acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ni], fa[mi], acc[mi][ni], 0, 0, 0);
         };
-        if (MODE == 0 && g.ilv) {   // (wave-uniform; PCA_HX_ILV=0 selects the plain order)
+        if (MODE == 0 && g.ilv) {   // (wave-uniform; PCA_HX_ILV=1 selects the interleave)
           // the second half's 8 fragment reads issued between the first half's MFMAs (one per
           // MFMA, sched_group_barrier; conv3x3_c64.hip's per-step interleave): only the first
           // half's reads are exposed after the tap barrier

@@ -1264,8 +1264,11 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
 # neither. The backward recomputes the activation derivative from y (ACT_RELU_Y / swish from the
 # aux scale | shift) instead of a stored mask, reduces the BN-backward sums of the depthwise
 # dgrad's output and applies them in one pass (whose finalize also clears the forward
-# accumulator the BN consumed). PCA_DW_IN_FUSE=0: the separate BN apply pass + plain depthwise.
-_DW_IN_FUSE = os.environ.get("PCA_DW_IN_FUSE", "1") != "0"
+# accumulator the BN consumed). Opt-in (PCA_DW_IN_FUSE=1): measured slower than the separate BN
+# apply pass + plain depthwise (MobileNetV2 bs1024 15.40 vs 14.14 ms, EfficientNet-B0 bs128 4.19
+# vs 3.98 ms; README "round 4") - the transform's per-load scale/shift/act costs the depthwise
+# kernels more VALU time than the apply pass's HBM round trip.
+_DW_IN_FUSE = os.environ.get("PCA_DW_IN_FUSE", "0") == "1"
 _ACT_RELU_Y = 4
 
 
@@ -1343,7 +1346,7 @@ class _BNActDW(torch.autograd.Function):
 def bn_act_dwconv(bn, x, act, conv):
     """``conv(act(bn(x)))`` for a depthwise ``conv`` (groups == channels, multiplier 1, no bias):
     one fused node on the GPU (BN applied on the depthwise kernels' loads), the plain composition
-    elsewhere (CPU reference path, unsupported geometry / activation, PCA_DW_IN_FUSE=0)."""
+    elsewhere (CPU reference path, unsupported geometry / activation, PCA_DW_IN_FUSE unset)."""
     Cc = x.shape[1]
     ks, st, pd = conv.kernel_size, conv.stride, conv.padding
     simple = (conv.groups == Cc and conv.out_channels == Cc and conv.bias is None

@@ -1,0 +1,67 @@
+"""Shifted BatchNorm forward sums at the producer kernels (csrc/common.h stat_shift): for every
+forward kernel family that delivers statistics (stem, layer-1 c64, halo hx, generic igemm, 1x1,
+split-K reduce), in slab and sharded-accumulator form:
+
+* the conv output does not depend on the shift (bitwise);
+* a zero shift gives bitwise the unshifted sums;
+* a shift K gives sums of (x - K) (against fp64 on the bf16 output) and, in accumulator form,
+  publishes K in the accumulator's K row.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# (N, Cin, H, Cout, k, stride, pad, cfg): cfg = forced tile config (-1: default selection)
+CASES = [
+    (64, 8, 32, 64, 3, 1, 1, -1),       # stem kernel (8-channel padded RGB)
+    (64, 64, 32, 64, 3, 1, 1, -1),      # layer-1 c64
+    (64, 128, 16, 128, 3, 1, 1, 30),    # halo hx
+    (64, 512, 4, 512, 3, 1, 1, 3),      # generic igemm
+    (64, 96, 8, 576, 1, 1, 0, 3),       # 1x1 (MobileNetV2 expand)
+    (16, 256, 4, 256, 3, 1, 1, 3),      # small M: split-K candidate
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("acc_form", [False, True])
+def test_shifted_stats(case, acc_form):
+    from pytorch_cifar_amd import _native
+
+    C = _native.lib()
+    N, Cin, H, Cout, k, s, p, cfg = case
+    torch.manual_seed(0)
+    x = (torch.randn(N, H, H, Cin, device="cuda") + 3.0).bfloat16()
+    w = torch.randn(Cout, k, k, Cin, device="cuda") * (2.0 / (Cin * k * k)) ** 0.5
+    wb, _ = C.weight_prep(w, 1, False)
+    R = 8
+
+    def run(shift):
+        if acc_form:
+            acc = torch.zeros(R * 2 * Cout + Cout, device="cuda")
+            y, _ = C.conv_fwd(x, wb, None, s, p, 1, True, acc, R, shift)
+            sums = acc[: R * 2 * Cout].view(R, 2, Cout).sum(0)
+            return y, sums, acc[R * 2 * Cout:]
+        y, st = C.conv_fwd(x, wb, None, s, p, 1, True, None, 0, shift)
+        return y, st.sum(0), None
+
+    C.set_conv_tile(0, cfg)
+    C.set_conv_tile(2, 3 if case[0] == 16 else -1)
+    try:
+        y0, s0, _ = run(None)
+        yz, sz, kz = run(torch.zeros(Cout, device="cuda"))
+        K = torch.randn(Cout, device="cuda") + 3.0
+        yk, sk, kk = run(K)
+    finally:
+        C.set_conv_tile(0, -1)
+        C.set_conv_tile(2, -1)
+    assert torch.equal(y0, yz) and torch.equal(y0, yk), "the shift must not change the output"
+    if not acc_form:   # (atomic accumulation order varies between launches)
+        assert torch.equal(s0, sz), "a zero shift must give the unshifted sums bitwise"
+    else:
+        torch.testing.assert_close(sz, s0, rtol=1e-5, atol=1e-2)
+        assert torch.equal(kk, K), "the accumulator's K row must hold the shift"
+    yd = yk.double().reshape(-1, Cout)
+    d = yd - K.double()
+    torch.testing.assert_close(sk[0].double(), d.sum(0), rtol=1e-4, atol=1e-2 * N)
+    torch.testing.assert_close(sk[1].double(), (d * d).sum(0), rtol=1e-4, atol=1e-2 * N)
