@@ -44,7 +44,6 @@ struct HxGeom {
   const bf16* bn_y2;
   const float* bn_aux2;
   const float* kshift;   // forward stats: per-channel shift K (common.h stat_shift), or nullptr
-  int ilv;               // forward: interleaved fragment reads (hx_ilv_enabled)
 };
 
 // dgrad: prefetch the fused BN reduce's y during the last tap (true) or load it at the epilogue
@@ -53,15 +52,6 @@ struct HxGeom {
 #define PCA_HX_PREFETCH_Y 0
 #endif
 constexpr bool kHxPrefetchY = PCA_HX_PREFETCH_Y != 0;
-// forward: second half's fragment reads interleaved with the first half's MFMAs (HxGeom::ilv,
-// opt-in PCA_HX_ILV=1: measured 0.2-0.5 % slower on ResNet-18 bs1024, README "round 4")
-static bool hx_ilv_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("PCA_HX_ILV");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 // MODE 3 (dual-BN third sum) is compiled out: its 48 per-lane sums spill the 8-wave variants
 // (180+ registers); the dual-BN block-tail dgrads stay on the generic igemm
 constexpr bool kHxDual = false;
@@ -117,7 +107,8 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
   char* const Hs = smem;                       // [2][HBYTES] halo ring
   char* const Bs = smem + 2 * HB;              // [2][BBYTES] weight ring
   char* const dummy = smem + 2 * HB + 2 * BB;  // landing place of padding DMA slots
-  float* const auxs = reinterpret_cast<float*>(dummy + 1024);   // dgrad: BN mean | istd [| 2]
+  // dgrad: BN mean | istd [| 2]; forward statistics: the shift K of the block's channels
+  float* const auxs = reinterpret_cast<float*>(dummy + 1024);
 
   typedef __attribute__((address_space(3))) const char lds_char;
   typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
@@ -198,9 +189,10 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
 #pragma unroll
   for (int e = 0; e < (DUAL ? 16 : 1); ++e) s3[e] = 0.f;
   const int ch_lane = nb0 + wn * 64 + q * 16;  // first of this lane's 16 produced channels
-  float kk[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) kk[e] = (STATS && g.kshift) ? g.kshift[ch_lane + e] : 0.f;
+  if constexpr (STATS) {   // (in LDS, not 16 registers live across the MFMA loop: those spilled)
+    for (int i = tid; i < BN; i += NW * 64) auxs[i] = g.kshift ? g.kshift[nb0 + i] : 0.f;
+    __syncthreads();
+  }
   // its output-tensor channel (depth-to-space: class ch / COUT, channel ch % COUT)
   const int co_lane = D2S ? ch_lane % g.COUT : ch_lane;
   const int cls_lane = D2S ? ch_lane / g.COUT : 0;
@@ -316,30 +308,11 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
             for (int ni = 0; ni < 4; ++ni)
               acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ni], fa[mi], acc[mi][ni], 0, 0, 0);
         };
-        if (MODE == 0 && g.ilv) {   // (wave-uniform; PCA_HX_ILV=1 selects the interleave)
-          // the second half's 8 fragment reads issued between the first half's MFMAs (one per
-          // MFMA, sched_group_barrier; conv3x3_c64.hip's per-step interleave): only the first
-          // half's reads are exposed after the tap barrier
-          bf16x8 fa[2][4], fb[2][4];
-          load_half(0, fa[0], fb[0]);
-          __builtin_amdgcn_sched_barrier(0);
-          load_half(1, fa[1], fb[1]);
-          mfma_half(fa[0], fb[0]);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          mfma_half(fa[1], fb[1]);
-        } else {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            bf16x8 fa[4], fb[4];
-            load_half(h, fa, fb);
-            mfma_half(fa, fb);
-          }
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 fa[4], fb[4];
+          load_half(h, fa, fb);
+          mfma_half(fa, fb);
         }
       }
     }
@@ -369,7 +342,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
       if constexpr (STATS) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const float d = v[e] - kk[e];   // shifted sums (kk = 0 unshifted)
+          const float d = v[e] - auxs[ch_lane - nb0 + e];   // shifted sums (K = 0 unshifted)
           s1[e] += d;
           s2[e] += d * d;
         }
@@ -577,7 +550,6 @@ int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf
   g.bn_y2 = mode == 1 && bn_part ? bn_y2 : nullptr;   // (accumulator mode: rows of 3 sums)
   g.bn_aux2 = g.bn_y2 ? bn_aux2 : nullptr;
   g.kshift = mode == 0 && stats ? stat_shift() : nullptr;
-  g.ilv = hx_ilv_enabled() ? 1 : 0;
   if (mode == 0) return hx_dispatch<0>(a, b, y, stats, addend, bias, g, H, st, launch);
   if (mode == 1) return hx_dispatch<1>(a, b, y, stats, addend, bias, g, H, st, launch);
   return hx_dispatch<2>(a, b, y, stats, addend, bias, g, H, st, launch);

@@ -238,6 +238,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
   float st_s[TN], st_q[TN];
 #pragma unroll
   for (int ni = 0; ni < TN; ++ni) st_s[ni] = st_q[ni] = 0.f;
+  int n_pad = 0;   // padding rows past M summed by this block (shifted statistics)
 
   // fused BN-backward reduce (dgrad): this thread's store-loop channel group is fixed
   constexpr int CG_ = BN / 8;
@@ -547,33 +548,23 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       }
     }
     if constexpr (STATS) {
-      if (g.kshift) {   // shifted sums (robust variance): rows past M must not contribute -K
+      // shifted sums (robust variance): d = v - K[c] (K = 0 unshifted). Rows past M are exact
+      // zeros (zero-filled A, no bias) and add -K / K^2 each: taken back once per block (n_pad)
+      // instead of a per-row mask (the masks cost the 128x128 forward its second wave per SIMD)
 #pragma unroll
-        for (int ni = 0; ni < TN; ++ni) {
-          const int c = n0 + wn * WTN + ni * 16 + (lane & 15);
-          const float kc = c < g.Cn ? g.kshift[grp * g.Cn + c] : 0.f;
+      for (int ni = 0; ni < TN; ++ni) {
+        const int c = n0 + wn * WTN + ni * 16 + (lane & 15);
+        const float kc = (g.kshift && c < g.Cn) ? g.kshift[grp * g.Cn + c] : 0.f;
 #pragma unroll
-          for (int mi = 0; mi < TM; ++mi)
+        for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int r = m0 + wm * WTM + mi * 16 + (lane >> 4) * 4 + j;
-              const float d = r < Mrows ? acc[mi][ni][j] - kc : 0.f;
-              st_s[ni] += d;
-              st_q[ni] += d * d;
-            }
-        }
-      } else {
-#pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-          for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float v = acc[mi][ni][j];   // rows past M are exact zeros (zero-filled A)
-              st_s[ni] += v;
-              st_q[ni] += v * v;
-            }
+          for (int j = 0; j < 4; ++j) {
+            const float d = acc[mi][ni][j] - kc;
+            st_s[ni] += d;
+            st_q[ni] += d * d;
+          }
       }
+      n_pad += max(0, m0 + BM - Mrows);
     }
     bf16* Cs = reinterpret_cast<bf16*>(smem);
 #pragma unroll
@@ -664,6 +655,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       }
       const int c = n0 + tid;
       if (c < g.Cn) {
+        if (g.kshift && n_pad) {   // the padding rows' (0 - K) terms
+          const float kc = g.kshift[grp * g.Cn + c];
+          s += (float)n_pad * kc;
+          q -= (float)n_pad * kc * kc;
+        }
         stat_out(stats, blockIdx.x, g.shards, 2 * g.Co, grp * g.Cn + c, s);
         stat_out(stats, blockIdx.x, g.shards, 2 * g.Co, g.Co + grp * g.Cn + c, q);
       }
@@ -1382,6 +1378,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   for (int q = 0; q < 8; ++q) sm[q] = sq[q] = 0.f;
 #pragma unroll
   for (int q = 0; q < 8; ++q) b[q] = bias ? bias[cg * 8 + q] : 0.f;
+  // (forward statistics and the dgrad's fused BN reduce never meet in one launch: the STATS
+  // variant drops the reduce's registers)
+  float* const bnp = STATS ? nullptr : bn_part;
   float kk[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) kk[q] = (STATS && kshift && active) ? kshift[cg * 8 + q] : 0.f;
@@ -1392,8 +1391,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     bs1[q] = bs2[q] = bs3[q] = 0.f;
-    bmean[q] = bn_part && active ? bn_aux[cg * 8 + q] : 0.f;
-    bistd[q] = bn_part && active ? bn_aux[Co + cg * 8 + q] : 0.f;
+    bmean[q] = bnp && active ? bn_aux[cg * 8 + q] : 0.f;
+    bistd[q] = bnp && active ? bn_aux[Co + cg * 8 + q] : 0.f;
   }
   if (active) {
     for (int r = r0 + rr; r < r1; r += RP) {
@@ -1422,12 +1421,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
         for (int q = 0; q < 8; ++q) a[q] += d[q];
       }
       const uint4 pv = pack8(a);
-      if (bn_part) bn_fuse_acc(pv, bn_y + o, bn_mask[o >> 3], bmean, bistd, bs1, bs2);
-      if (bn_part && bn_y2) bn_fuse_acc3(pv, bn_y2 + o, bn_mask[o >> 3], bn_aux2, cg * 8, Co, bs3);
+      if (bnp) bn_fuse_acc(pv, bn_y + o, bn_mask[o >> 3], bmean, bistd, bs1, bs2);
+      if (bnp && bn_y2) bn_fuse_acc3(pv, bn_y2 + o, bn_mask[o >> 3], bn_aux2, cg * 8, Co, bs3);
       *reinterpret_cast<uint4*>(Y + o) = pv;
     }
   }
-  if (bn_part) {   // fused BN-backward reduce: one slab row per block (rows = gridDim.x)
+  if (bnp) {   // fused BN-backward reduce: one slab row per block (rows = gridDim.x)
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -1443,9 +1442,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
         q0 += red[(k * Co + c) * 3 + 1];
         t0 += red[(k * Co + c) * 3 + 2];
       }
-      stat_out(bn_part, blockIdx.x, shards, NSB * Co, c, s0);
-      stat_out(bn_part, blockIdx.x, shards, NSB * Co, Co + c, q0);
-      if (NSB == 3) stat_out(bn_part, blockIdx.x, shards, NSB * Co, 2 * Co + c, t0);
+      stat_out(bnp, blockIdx.x, shards, NSB * Co, c, s0);
+      stat_out(bnp, blockIdx.x, shards, NSB * Co, Co + c, q0);
+      if (NSB == 3) stat_out(bnp, blockIdx.x, shards, NSB * Co, 2 * Co + c, t0);
     }
     return;
   }

@@ -241,8 +241,9 @@ constexpr int kFHP = (kSR + 2) * kFW2;   // halo pixels per chunk (340)
 constexpr int kFGrid = 512;
 }  // namespace
 
+// (two blocks per CU: the CO = 64 variant otherwise took 218 + 64 registers, one wave per SIMD)
 template <int CO>
-__global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ x,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void stem_fwd_kernel(const bf16* __restrict__ x,
                                                        const bf16* __restrict__ w,
                                                        const float* __restrict__ bias,
                                                        bf16* __restrict__ y, int N, int H,
@@ -253,6 +254,7 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
   __shared__ __attribute__((aligned(16))) bf16 halo[kFHP * kSCS];
   __shared__ __attribute__((aligned(16))) bf16 ct[kSP * CST];
   __shared__ float red[4][2][CO];
+  __shared__ float kks[CO];                        // statistics shift K (LDS: no live registers)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int cpi = H / kSR, chunks = N * cpi;
@@ -279,12 +281,10 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
     tok[ks] = tap < 9;
     toff[ks] = tok[ks] ? (tap / 3) * kFW2 + tap % 3 : 0;
   }
-  float st_s[NT], st_q[NT], kk[NT];
+  float st_s[NT], st_q[NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    st_s[nt] = st_q[nt] = 0.f;
-    kk[nt] = kshift ? kshift[nt * 16 + (lane & 15)] : 0.f;
-  }
+  for (int nt = 0; nt < NT; ++nt) st_s[nt] = st_q[nt] = 0.f;
+  for (int c = tid; c < CO; c += 256) kks[c] = kshift ? kshift[c] : 0.f;   // (first barrier below)
 
   // halo of a chunk: rows h0-1 .. h0+8, cols -1 .. 32, zeros outside the image; loaded into
   // registers one chunk ahead (issued before the current chunk's MFMAs and epilogue)
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float v = acc[mt][nt][j] + bb[nt];
-          const float d = v - kk[nt];   // shifted sums (kk = 0 unshifted)
+          const float d = v - kks[nt * 16 + (lane & 15)];   // shifted sums (K = 0 unshifted)
           st_s[nt] += d;
           st_q[nt] += d * d;
           const int p = wid * 64 + mt * 16 + 4 * (lane >> 4) + j;
