@@ -65,8 +65,9 @@ def test_shifted_stats(case, acc_form, det):
     else:
         torch.testing.assert_close(sz, s0, rtol=1e-5, atol=1e-2)
         assert torch.equal(kk, K), "the accumulator's K row must hold the shift"
-    # fp32 sums of N*H*W terms against fp64: bounded by a few ulps of the sum of magnitudes
+    # fp32 per-lane running sums of N*H*W terms against fp64 (measured up to ~5e-5 of the sum of
+    # magnitudes): a wrong or missing shift is off by ~K per term, i.e. by O(1) of that scale
     d = yk.double().reshape(-1, Cout) - K.double()
     scale = d.abs().sum(0)
-    assert ((sk[0].double() - d.sum(0)).abs() <= 1e-5 * scale + 1e-3).all()
-    assert ((sk[1].double() - (d * d).sum(0)).abs() <= 1e-5 * (d * d).sum(0) + 1e-3).all()
+    assert ((sk[0].double() - d.sum(0)).abs() <= 3e-4 * scale + 1e-2).all()
+    assert ((sk[1].double() - (d * d).sum(0)).abs() <= 3e-4 * (d * d).sum(0) + 1e-2).all()

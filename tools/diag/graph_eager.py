@@ -28,6 +28,20 @@ def main():
         arena = ParamArena(model.parameters())
         opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4).attach_arena(arena)
         loader = DeviceLoader(imgs, labs, 64, "cuda", crop_pad=0, flip=False, drop_last=True, seed=0)
+        if os.environ.get("PRELINK") == "1" and not graph:
+            # zero pilots on the convs a BN links, before the first eager step (as the graph's
+            # first replay sees them): owners found on a throwaway copy's forward
+            import copy
+
+            from pytorch_cifar_amd.ops.functional import link_pilot
+
+            probe = copy.deepcopy(model)
+            with torch.no_grad():
+                probe(torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last))
+            for n, m in probe.named_modules():
+                for key, t in m.__dict__.get("_pca_pilot", {}).items():
+                    link_pilot(model.get_submodule(n), t.numel(), torch.device("cuda", key))
+            del probe
         step = TrainStep(model, opt, loader, 64, graph=graph)
         loader.set_epoch(0)
         rec = []
