@@ -272,7 +272,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
               const size_t o = out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
-              if (kHxPrefetchY && addend) {
+              if (addend) {
                 pre_a[mi][0] = *reinterpret_cast<const uint4*>(addend + o);
                 pre_a[mi][1] = *reinterpret_cast<const uint4*>(addend + o + 8);
               }
@@ -318,26 +318,20 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
     }
 
     // ---- epilogue: lane holds channels ch_lane + [0,16) of tile pixel wm*64 + mi*16 + lane&15 ----
-    // dgrad epilogue operands (residual-gradient addend, BN input y of the fused reduce) loaded
-    // here one row ahead (prefetched during the last tap they held 64 more registers across the
-    // MFMA loop: 256 + spills)
-    auto epi_load = [&](int mi) {
-      if constexpr (DGRAD && !kHxPrefetchY) {
-        const size_t o = out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
-        if (addend) {
-          pre_a[mi][0] = *reinterpret_cast<const uint4*>(addend + o);
-          pre_a[mi][1] = *reinterpret_cast<const uint4*>(addend + o + 8);
-        }
-        if (bnf) {
+    if constexpr (DGRAD && !kHxPrefetchY) {
+      // the BN input y of the fused reduce, loaded now for all four rows at once (prefetched
+      // during the last tap it held 32 more registers across the MFMA loop: 256 + spills)
+      if (bnf) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const size_t o = out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
           pre_y[mi][0] = *reinterpret_cast<const uint4*>(g.bn_y + o);
           pre_y[mi][1] = *reinterpret_cast<const uint4*>(g.bn_y + o + 8);
         }
       }
-    };
-    epi_load(0);
+    }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
-      if (mi + 1 < 4) epi_load(mi + 1);
       float v[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) v[e] = acc[mi][e >> 2][e & 3];

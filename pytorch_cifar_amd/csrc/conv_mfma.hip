@@ -1565,8 +1565,19 @@ struct TuneKey {
 static std::map<TuneKey, std::pair<int, int>> g_tuned;   // key -> (cfg, split)
 static int g_trial_cfg = -1, g_trial_split = -1;
 
+// Dual-BN request of the next dgrad launch(es) (bindings scope it around one call): the fused
+// reduce also adds dz * xhat2 of the projection-shortcut BN (y2, aux2) — generic igemm / split-K
+// stride-1 dgrads into a sharded accumulator only.
+static const bf16* g_dual_y2 = nullptr;
+static const float* g_dual_aux2 = nullptr;
+
+// A dual-BN dgrad is tuned apart from the plain one of the same geometry (bit 3 of the mode
+// field): the halo kernel cannot carry the third sum, so where it wins the plain dgrad it must
+// not be picked for the dual call too (that left a separate reduce + finalize + apply behind,
+// 70-126 us per projection block at bs1024)
 static TuneKey tune_key(const ConvGeom& g) {
-  return TuneKey{{g.mode, g.N, g.Hs, g.Ws, g.Cs, g.Ho, g.Wo, g.Co, g.KH, g.KW, g.stride, g.pad,
+  const int mode = g.mode + (g.mode != 0 && g_dual_y2 ? 8 : 0);
+  return TuneKey{{mode, g.N, g.Hs, g.Ws, g.Cs, g.Ho, g.Wo, g.Co, g.KH, g.KW, g.stride, g.pad,
                   g.groups}};
 }
 
@@ -1939,11 +1950,6 @@ static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int K
   return g;
 }
 
-// Dual-BN request of the next dgrad launch(es) (bindings scope it around one call): the fused
-// reduce also adds dz * xhat2 of the projection-shortcut BN (y2, aux2) — generic igemm / split-K
-// stride-1 dgrads into a sharded accumulator only.
-static const bf16* g_dual_y2 = nullptr;
-static const float* g_dual_aux2 = nullptr;
 void conv_set_bn_dual(const bf16* y2, const float* aux2) {
   g_dual_y2 = y2;
   g_dual_aux2 = aux2;

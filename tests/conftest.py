@@ -26,3 +26,19 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _stock_conv_without_miopen(request):
+    """GPU tests compute their stock-PyTorch references with MIOpen disabled (PyTorch's native
+    im2col / depthwise kernels): a fresh box runs MIOpen's solver search for every new conv
+    config, and two of its solvers faulted the device on this pool (a channels_last depthwise
+    backward at MobileNetV2 bs1024, a 1x1 Cin=144 NCHW backward), taking every later test of the
+    process down with them. PCA_TEST_MIOPEN=1 keeps MIOpen."""
+    if "gpu" not in request.keywords or os.environ.get("PCA_TEST_MIOPEN") == "1":
+        yield
+        return
+    import torch
+
+    with torch.backends.cudnn.flags(enabled=False):
+        yield

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""One training forward of ResNet-18 twice from identical weights: (a) a fresh model (the convs have
+"""One training step (forward + backward; GRAD=0: forward only) of ResNet-18 twice from identical weights: (a) a fresh model (the convs have
 no BN pilot yet: unshifted sums), (b) a copy whose convs already hold zero pilots (shift K = 0).
-The two must agree bitwise; prints the first module whose output differs."""
+The two must agree bitwise; prints the first module output / parameter gradient that differs."""
 import copy
 import os
 import sys
@@ -21,17 +21,26 @@ def main():
     bs = int(os.environ.get("BS", "64"))
     base = models.ResNet18().cuda().train()
     x = torch.randn(bs, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    labels = torch.randint(0, 10, (bs,), device="cuda")
 
     def run(model):
         outs = []
         hooks = [m.register_forward_hook(lambda m, i, o, n=n: outs.append((n, o.detach().float().clone())))
                  for n, m in model.named_modules() if n]
-        with torch.no_grad():
+        if os.environ.get("GRAD", "1") == "1":
+            from pytorch_cifar_amd.ops.functional import cross_entropy
+
             y = model(x)
+            loss = cross_entropy(y, labels)
+            loss.backward()
+        else:
+            with torch.no_grad():
+                y = model(x)
         torch.cuda.synchronize()
         for h in hooks:
             h.remove()
-        return y.float(), outs
+        grads = [(n, p.grad.float().clone()) for n, p in model.named_parameters() if p.grad is not None]
+        return y.float(), outs + grads
 
     a = copy.deepcopy(base)
     ya, oa = run(a)
