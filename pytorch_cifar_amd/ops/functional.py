@@ -643,19 +643,28 @@ class _ConvMFMA(torch.autograd.Function):
         dy = dy.contiguous()
         weight, bias = ctx.weight, ctx.bias
         dx = None
-        if ctx.needs_input_grad[0]:
-            slot = ctx.slot
-            src = ctx.bnsrc
-            ctx.bnsrc = None
-            if slot is not None and ctx.owner:
-                add = slot.take()            # the other branch's dX, summed in the epilogue
-                dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add)
-            elif slot is None:
-                dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, None)
-            else:
-                dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
-                if slot.offer(dx):
-                    dx = None                # delivered through the owner's epilogue
+        # with the side stream the weight gradient is issued first, so it runs beside this
+        # conv's dgrad (both only need dy); otherwise dgrad then wgrad on the one stream
+        side_first = wgrad_stream(x.device) is not None
+
+        def do_dgrad():
+            nonlocal dx
+            if ctx.needs_input_grad[0]:
+                slot = ctx.slot
+                src = ctx.bnsrc
+                ctx.bnsrc = None
+                if slot is not None and ctx.owner:
+                    add = slot.take()            # the other branch's dX, summed in the epilogue
+                    dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add)
+                elif slot is None:
+                    dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, None)
+                else:
+                    dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
+                    if slot.offer(dx):
+                        dx = None                # delivered through the owner's epilogue
+
+        if not side_first:
+            do_dgrad()
         KH, KW = weight.shape[2], weight.shape[3]
         dw_ret = db_ret = None
         if weight.requires_grad and cin_pad and weight.is_leaf and KH == 3 and KW == 3:
@@ -686,6 +695,8 @@ class _ConvMFMA(torch.autograd.Function):
                     G.accumulate(weight, dw)
                 else:
                     dw_ret = dw.permute(0, 3, 1, 2)
+        if side_first:
+            do_dgrad()
         if bias is not None and bias.requires_grad:
             bbuf = G.grad_buffer(bias) if bias.is_leaf else None
             if bbuf is not None:

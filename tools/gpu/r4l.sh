@@ -14,7 +14,8 @@ for rep in 1 2; do
   for b in 1024 128; do
     (cd baseline_r3 && timeout -k 10 300 python bench.py --batch $b --steps 30 --warmup 10) > $O/r3_${b}_$rep.json 2>$O/r3.err || exit $?
     timeout -k 10 300 python bench.py --batch $b --steps 30 --warmup 10 > $O/cur_${b}_$rep.json 2>$O/cur.err || exit $?
-    echo "rep$rep bs$b r3 $(ms $O/r3_${b}_$rep.json) cur $(ms $O/cur_${b}_$rep.json)"
+    PCA_WGRAD_STREAM=1 timeout -k 10 300 python bench.py --batch $b --steps 30 --warmup 10 > $O/ws_${b}_$rep.json 2>$O/ws.err || exit $?
+    echo "rep$rep bs$b r3 $(ms $O/r3_${b}_$rep.json) cur $(ms $O/cur_${b}_$rep.json) wgrad-stream $(ms $O/ws_${b}_$rep.json)"
   done
 done
 bash tools/gpu/prof_bench.sh r4l 1024 128 || exit 1
