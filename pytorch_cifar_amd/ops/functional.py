@@ -162,7 +162,10 @@ def _slot_for_residual(x):
 # launches also wait on it (parallel/ddp.py).
 # Measured on MI355X (ResNet-18, hipGraph step): the per-conv cross-stream dependencies cost more
 # than the overlap recovers (bs128 2.28 -> 2.40 ms, bs1024 7.30 -> 7.50 ms), so the side stream
-# is opt-in: PCA_WGRAD_STREAM=1.
+# is opt-in: PCA_WGRAD_STREAM=1. Round 4 re-measured it with the wgrad issued before its conv's
+# dgrad (so the two can overlap): bs128 1.88 -> 1.96-1.99 ms, bs1024 6.59 -> 6.88-6.93 ms (same
+# box) — each conv kernel holds its CUs' LDS / registers, so the branches do not co-reside; they
+# only serialise behind the cross-stream edges.
 _WGRAD_STREAM = os.environ.get("PCA_WGRAD_STREAM", "0") == "1"
 _side = {}          # device index -> torch.cuda.Stream
 _join_pending = {"on": False}
@@ -397,6 +400,23 @@ def set_fuse_bn_backward(on: bool) -> None:
     """Enable/disable the BN-backward reduce fusion into the consumer conv's dgrad epilogue."""
     global _FUSE_BN_BWD
     _FUSE_BN_BWD = bool(on)
+
+
+# A BatchNorm without activation (MobileNetV2 / EfficientNet-B0 block tails: the project conv's
+# BN, reference mobilenetv2.py:37, efficientnet.py:103) hands its consumer dgrad an all-ones
+# "ReLU mask": dz = dout * 1, so the same fused epilogue reduces its backward sums (PCA_FUSE_BN_NOACT=0
+# keeps the separate reduce + finalize passes). One persistent buffer per size (stable addresses
+# for hipGraph replay); the kernels read 1 bit per element of it.
+_FUSE_BN_NOACT = os.environ.get("PCA_FUSE_BN_NOACT", "1") != "0"
+_ONES_MASK = {}
+
+
+def _ones_mask(numel, device):
+    key = (int(numel), device.index if device.index is not None else torch.cuda.current_device())
+    m = _ONES_MASK.get(key)
+    if m is None:
+        m = _ONES_MASK[key] = torch.full(((int(numel) + 7) // 8,), 255, dtype=torch.uint8, device=device)
+    return m
 
 
 class _BNSrc:
@@ -1096,6 +1116,10 @@ class _BatchNormAct(torch.autograd.Function):
                 cfg.bacc is not None and aux is not None and aux.numel() >= 4 * y.shape[-1]:
             # swish: only a depthwise consumer can fuse it (z recomputed from y, aux scale|shift)
             ctx.bnsrc = cfg.src = _BNSrc(y, None, aux, cfg.bacc, act=2)
+        elif cfg.src is not None and ACT[cfg.act] == 0 and y2 is None and _FUSE_BN_NOACT and \
+                cfg.bacc is not None and y.shape[-1] % 8 == 0 and not _DETERMINISTIC:
+            # no activation: the consumer dgrad reduces dz = dout under an all-ones mask
+            ctx.bnsrc = cfg.src = _BNSrc(y, _ones_mask(y.numel(), y.device), aux, cfg.bacc)
         else:
             cfg.src = None
         return out

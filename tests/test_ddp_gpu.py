@@ -118,7 +118,8 @@ def test_native_rccl_world1_graph_step_matches_plain_step():
     """The real RCCL path the 8-GPU run takes — native RcclComm, bucket all-reduces and the BN-buffer
     broadcast on the communication stream, captured into the hipGraph with the step — at world 1,
     where every collective is the identity: three captured DDP steps must leave exactly the
-    parameters of three captured plain steps."""
+    parameters of three captured plain steps (deterministic mode: no fp32-atomic ordering noise)."""
+    import pytorch_cifar_amd
     from pytorch_cifar_amd import _native, models
     from pytorch_cifar_amd.data.loader import DeviceLoader
     from pytorch_cifar_amd.data.synthetic import synthetic_cifar10
@@ -133,6 +134,7 @@ def test_native_rccl_world1_graph_step_matches_plain_step():
     imgs, labs = synthetic_cifar10(256, seed=5)
     comm = C.RcclComm(C.rccl_unique_id(), 1, 0, 0)
     out = []
+    pytorch_cifar_amd.set_deterministic(True)
     try:
         for use_ddp in (False, True):
             torch.manual_seed(0)
@@ -154,6 +156,7 @@ def test_native_rccl_world1_graph_step_matches_plain_step():
             assert step.graph is not None, step.graph_error
             out.append((arena.param_flat.clone(), model.bn1.running_mean.clone()))
     finally:
+        pytorch_cifar_amd.set_deterministic(False)
         comm.destroy()
     (p0, r0), (p1, r1) = out
     assert torch.equal(p0, p1), f"max |diff| {(p0 - p1).abs().max().item():.3e}"
