@@ -83,16 +83,17 @@ __device__ __forceinline__ void bn_fuse_acc(const uint4& v, const bf16* y, uint8
   }
 }
 
-// dual-BN third sum: dz * xhat2 of the projection-shortcut BN input y2
-__device__ __forceinline__ void bn_fuse_acc3(const uint4& v, const bf16* y2, uint8_t m,
-                                             const float* aux2, int ch, int Co, float* s3) {
+// dual-BN third sum from mean2 / istd2 already in LDS or registers (m2, i2: this vector's 8
+// channels)
+__device__ __forceinline__ void bn_fuse_acc3s(const uint4& v, const bf16* y2, uint8_t m,
+                                              const float* m2, const float* i2, float* s3) {
   float f[8], yy[8];
   unpack8(v, f);
   unpack8(*reinterpret_cast<const uint4*>(y2), yy);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
-    s3[q] += dz * (yy[q] - aux2[ch + q]) * aux2[Co + ch + q];
+    s3[q] += dz * (yy[q] - m2[q]) * i2[q];
   }
 }
 
@@ -178,7 +179,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
   static_assert(BM * CST * 2 <= STAGES * STAGE, "C tile must fit the LDS ring");
   static_assert((BM * (BN / 8)) % NT == 0, "epilogue store loop");
 
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+  // (one LDS array — a second __shared__ object can cost a vmcnt(0) per K-step; dgrad: its tail
+  // holds the dual BN's mean2 | istd2 of this block's channels, read by the epilogue)
+  constexpr int AUX2_OFF = STAGES * STAGE;
+  // (only where the tail costs no workgroup per CU: 160 KiB / LDS unchanged)
+  constexpr bool AUX2_LDS = MODE != 0 && STAGES * STAGE + 2 * BN * 4 <= 160 * 1024 &&
+                            (160 * 1024) / (STAGES * STAGE + 2 * BN * 4) == (160 * 1024) / (STAGES * STAGE);
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE + (AUX2_LDS ? 2 * BN * 4 : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -256,6 +263,16 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         bmean[q] = g.bn_aux[ch + q];
         bistd[q] = g.bn_aux[g.Co + ch + q];
       }
+    }
+  }
+  if constexpr (AUX2_LDS) {
+    if (bnf && g.bn_y2 != nullptr) {   // (block-uniform) the dual BN's mean2 | istd2 into LDS
+      float* aux2s = reinterpret_cast<float*>(smem + AUX2_OFF);
+      for (int i = tid; i < 2 * BN; i += NT) {
+        const int c = n0 + (i % BN);
+        aux2s[i] = c < g.Cn ? g.bn_aux2[(i >= BN ? g.Co : 0) + grp * g.Cn + c] : 0.f;
+      }
+      __syncthreads();
     }
   }
 
@@ -609,7 +626,15 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
           v = pack8(a);
         }
         if (bnf) bn_fuse_acc(v, g.bn_y + o, g.bn_mask[o >> 3], bmean, bistd, bs1, bs2);
-        if (dual) bn_fuse_acc3(v, g.bn_y2 + o, g.bn_mask[o >> 3], g.bn_aux2, grp * g.Cn + gc, g.Co, bs3);
+        if (dual) {
+          if constexpr (AUX2_LDS) {
+            const float* aux2s = reinterpret_cast<const float*>(smem + AUX2_OFF) + c8 * 8;
+            bn_fuse_acc3s(v, g.bn_y2 + o, g.bn_mask[o >> 3], aux2s, aux2s + BN, bs3);
+          } else {   // (configs whose LDS would cost occupancy: from global, L1-cached)
+            const float* a2 = g.bn_aux2 + grp * g.Cn + gc;
+            bn_fuse_acc3s(v, g.bn_y2 + o, g.bn_mask[o >> 3], a2, a2 + g.Co, bs3);
+          }
+        }
         *reinterpret_cast<uint4*>(Y + o) = v;
       }
     }
@@ -1387,12 +1412,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
   const size_t plane = (size_t)M * Co;
-  float bs1[8], bs2[8], bs3[8], bmean[8], bistd[8];
+  float bs1[8], bs2[8], bs3[8], bmean[8], bistd[8], bmean2[8], bistd2[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     bs1[q] = bs2[q] = bs3[q] = 0.f;
     bmean[q] = bnp && active ? bn_aux[cg * 8 + q] : 0.f;
     bistd[q] = bnp && active ? bn_aux[Co + cg * 8 + q] : 0.f;
+    bmean2[q] = bnp && bn_y2 && active ? bn_aux2[cg * 8 + q] : 0.f;
+    bistd2[q] = bnp && bn_y2 && active ? bn_aux2[Co + cg * 8 + q] : 0.f;
   }
   if (active) {
     for (int r = r0 + rr; r < r1; r += RP) {
@@ -1422,7 +1449,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       }
       const uint4 pv = pack8(a);
       if (bnp) bn_fuse_acc(pv, bn_y + o, bn_mask[o >> 3], bmean, bistd, bs1, bs2);
-      if (bnp && bn_y2) bn_fuse_acc3(pv, bn_y2 + o, bn_mask[o >> 3], bn_aux2, cg * 8, Co, bs3);
+      if (bnp && bn_y2) bn_fuse_acc3s(pv, bn_y2 + o, bn_mask[o >> 3], bmean2, bistd2, bs3);
       *reinterpret_cast<uint4*>(Y + o) = pv;
     }
   }
