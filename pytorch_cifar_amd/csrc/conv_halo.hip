@@ -35,6 +35,7 @@ struct HaloGeom {
   int chunk, splits, atomic;
   int ablate;             // diagnostics (PCA_HALO_ABLATE): 1 = no DMA, 2 = no MFMA phase, 4 = no epilogue
   int xcd;                // XCD-aware block order (PCA_HALO_XCD=1; default: dispatch order)
+  int ilv;                // next stage's DMA pieces issued between this stage's MFMAs (PCA_HALO_ILV)
   uint32_t x_bytes, dy_bytes;
   FastDiv fd_hw, fd_w;
 };
@@ -180,15 +181,15 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
     }
   }
 
-  auto issue = [&](int pbase, int buf) {
+  // DMA slot j of the stage starting at pixel pbase into ring buffer buf
+  auto issue_slot = [&](int pbase, int buf, int j) {
     if (g.ablate & 1) return;
     char* S = smem + buf * STAGE;
     const bool live = pbase < p_end;
     // first image / row of the stage (W power of two: shifts)
     const int n0 = pbase / (W * W);
     const int h0 = (pbase / W) % W;
-#pragma unroll
-    for (int j = 0; j < SLOTS; ++j) {
+    {
       const int t = wid + NW * j;                // wave-uniform slot kind
       uint32_t off = kOOB;
       if (t < SH::HI) {
@@ -208,6 +209,10 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
         dma16(rsD, S + J_OFF, kOOB);              // keeps vmcnt per wave uniform
       }
     }
+  };
+  auto issue = [&](int pbase, int buf) {
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j) issue_slot(pbase, buf, j);
   };
 
   // ---- per-lane B-fragment addressing: halo rows of this lane's two pixel rows ----
@@ -247,7 +252,11 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   for (int kt = 0; kt < KT; ++kt) {
     wait_vmcnt<(STAGES - 2) * SLOTS>();   // stage kt landed (the STAGES - 2 after it may not have)
     raw_barrier();
-    issue(p_begin + (kt + STAGES - 1) * KP, (kt + STAGES - 1) % STAGES);
+    const int pnext = p_begin + (kt + STAGES - 1) * KP, bnext = (kt + STAGES - 1) % STAGES;
+    // the next stage's pieces: all at once here, or (g.ilv, wave-uniform) spread over this
+    // stage's MFMAs — issued as a block they kept the matrix pipe idle (the DMA-only and MFMA-only
+    // ablations of this kernel added up instead of overlapping)
+    if (!g.ilv || (g.ablate & 2)) issue(pnext, bnext);
     if (g.ablate & 2) continue;
     const char* S = smem + (kt % STAGES) * STAGE;
 #pragma unroll
@@ -274,6 +283,12 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfv, acc[mi][ni], 0, 0, 0);
+        if (g.ilv) {
+          // slot j after MFMA group (ks, ni) = j * KS * TN / SLOTS (compile-time after unrolling)
+#pragma unroll
+          for (int j = 0; j < SLOTS; ++j)
+            if (ks * TN + ni == (j * KS * TN) / SLOTS) issue_slot(pnext, bnext, j);
+        }
       }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -516,6 +531,11 @@ static bool halo_geom(HaloGeom& g, int N, int H, int W, int Cin, int Cout, int g
     return e && e[0] == '1' ? 1 : 0;
   }();
   g.xcd = xcd;
+  static const int ilv = [] {
+    const char* e = getenv("PCA_HALO_ILV");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  g.ilv = ilv;
   return true;
 }
 

@@ -113,51 +113,3 @@ def test_pending_buffer_broadcast_joined_by_state_dict():
     assert not ddp._bcast_pending
     assert all(k.startswith("module.") for k in sd)
 
-
-def test_native_rccl_world1_graph_step_matches_plain_step():
-    """The real RCCL path the 8-GPU run takes — native RcclComm, bucket all-reduces and the BN-buffer
-    broadcast on the communication stream, captured into the hipGraph with the step — at world 1,
-    where every collective is the identity: three captured DDP steps must leave exactly the
-    parameters of three captured plain steps (deterministic mode: no fp32-atomic ordering noise)."""
-    import pytorch_cifar_amd
-    from pytorch_cifar_amd import _native, models
-    from pytorch_cifar_amd.data.loader import DeviceLoader
-    from pytorch_cifar_amd.data.synthetic import synthetic_cifar10
-    from pytorch_cifar_amd.engine.arena import ParamArena
-    from pytorch_cifar_amd.engine.optim import SGD
-    from pytorch_cifar_amd.engine.trainer import TrainStep
-    from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
-    from pytorch_cifar_amd.parallel.launcher import DistContext
-
-    C = _native.lib()
-    dev = torch.device("cuda", 0)
-    imgs, labs = synthetic_cifar10(256, seed=5)
-    comm = C.RcclComm(C.rccl_unique_id(), 1, 0, 0)
-    out = []
-    pytorch_cifar_amd.set_deterministic(True)
-    try:
-        for use_ddp in (False, True):
-            torch.manual_seed(0)
-            model = models.build_model("ResNet18").to(dev)
-            arena = ParamArena(model.parameters())
-            opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4).attach_arena(arena)
-            net, ddp = model, None
-            if use_ddp:
-                ctx = DistContext(rank=0, world=1, local_rank=0, device=dev, backend="nccl", comm=comm)
-                ddp = net = DistributedDataParallel(model, ctx, bucket_cap_mb=4.0, arena=arena,
-                                                    force_collectives=True)
-            loader = DeviceLoader(imgs, labs, 64, dev, train=True, crop_pad=0, flip=False, seed=0,
-                                  drop_last=True)
-            step = TrainStep(net, opt, loader, 64, ddp=ddp, graph=True)
-            idx = list(loader.batch_indices())
-            for k in range(3):
-                step(idx[k])
-            torch.cuda.synchronize()
-            assert step.graph is not None, step.graph_error
-            out.append((arena.param_flat.clone(), model.bn1.running_mean.clone()))
-    finally:
-        pytorch_cifar_amd.set_deterministic(False)
-        comm.destroy()
-    (p0, r0), (p1, r1) = out
-    assert torch.equal(p0, p1), f"max |diff| {(p0 - p1).abs().max().item():.3e}"
-    assert torch.equal(r0, r1)
