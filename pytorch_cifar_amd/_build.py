@@ -65,6 +65,8 @@ def _common_flags(incs, abi):
         f"-I{CSRC}",
         f"-I{py_inc}",
     ]
+    # build-time kernel variants for same-box A/B trees (e.g. -DPCA_IGEMM_DMA_SPREAD=1)
+    flags += os.environ.get("PCA_EXTRA_HIPCC_FLAGS", "").split()
     flags += [f"-I{p}" for p in incs]
     return flags
 

@@ -32,6 +32,10 @@
 #include <type_traits>
 #include <vector>
 
+#ifndef PCA_IGEMM_DMA_SPREAD
+#define PCA_IGEMM_DMA_SPREAD 0
+#endif
+
 namespace pca {
 
 bool deterministic_conv();   // conv_halo.hip
@@ -487,7 +491,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       const int rel = kt - kt_begin;
       wait_vmcnt<(STAGES - 2) * LPS>();
       raw_barrier();
-      issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);   // past-the-end stages load zeros
+      // PCA_IGEMM_DMA_SPREAD=1 (build-time: as a runtime branch it cost the 128x128 forward its
+      // second workgroup per CU): the next stage's DMA pieces go out after the first quarter of
+      // this step's MFMAs instead of before its fragment reads (their issue cycles then overlap
+      // the matrix pipe)
+      constexpr bool dspread = PCA_IGEMM_DMA_SPREAD != 0;
+      if constexpr (!dspread) issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);   // past-the-end stages load zeros
       const char* As = smem + (rel % STAGES) * STAGE;
       const char* Bs = As + A_BYTES;
       // all fragments of the K-step are read up front into distinct registers (the compiler
@@ -515,8 +524,15 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < TN; ++ni)
+          for (int ni = 0; ni < TN; ++ni) {
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][mi], bfv[kk][ni], acc[mi][ni], 0, 0, 0);
+            constexpr int NMF = (BK / 32) * TM * TN;
+            if constexpr (dspread) if ((kk * TM + mi) * TN + ni == (NMF / 4 > 0 ? NMF / 4 - 1 : 0)) {
+              __builtin_amdgcn_sched_barrier(0);
+              issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
       __builtin_amdgcn_s_setprio(0);
     }
     wait_vmcnt<0>();
