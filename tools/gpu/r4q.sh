@@ -17,7 +17,8 @@ for rep in 1 2; do
     for v in 0 1; do
       PCA_HALO_ILV=$v timeout -k 10 300 python bench.py --batch $b --steps 30 --warmup 10 > $O/ilv${v}_${b}_$rep.json 2>$O/err.log || { tail -5 $O/err.log; exit 1; }
     done
-    echo "rep$rep bs$b r3 $(ms $O/r3_${b}_$rep.json) cur $(ms $O/ilv0_${b}_$rep.json) halo-ilv $(ms $O/ilv1_${b}_$rep.json)"
+    (cd variant_sp && timeout -k 10 300 python bench.py --batch $b --steps 30 --warmup 10) > $O/sp_${b}_$rep.json 2>$O/sp.err || { tail -5 $O/sp.err; exit 1; }
+    echo "rep$rep bs$b r3 $(ms $O/r3_${b}_$rep.json) cur $(ms $O/ilv0_${b}_$rep.json) halo-ilv $(ms $O/ilv1_${b}_$rep.json) igemm-dma-spread $(ms $O/sp_${b}_$rep.json)"
   done
 done
 PCA_HALO_ILV=1 PCA_TUNE_LOG=1 timeout -k 10 300 python bench.py --batch 1024 --steps 5 --warmup 2 > $O/tune1.json 2> $O/tune1.log || exit 1
