@@ -35,7 +35,7 @@ struct HaloGeom {
   int chunk, splits, atomic;
   int ablate;             // diagnostics (PCA_HALO_ABLATE): 1 = no DMA, 2 = no MFMA phase, 4 = no epilogue
   int xcd;                // XCD-aware block order (PCA_HALO_XCD=1; default: dispatch order)
-  int ilv;                // next stage's DMA pieces issued between this stage's MFMAs (PCA_HALO_ILV)
+  int ilv;                // next stage's DMA pieces issued between this stage's MFMAs (PCA_HALO_ILV=0: off)
   uint32_t x_bytes, dy_bytes;
   FastDiv fd_hw, fd_w;
 };
@@ -531,9 +531,11 @@ static bool halo_geom(HaloGeom& g, int N, int H, int W, int Cin, int Cout, int g
     return e && e[0] == '1' ? 1 : 0;
   }();
   g.xcd = xcd;
+  // (default on: ResNet-18 3x3 wgrads 4-8 % faster per call, step 6.49 -> 6.41 ms at bs1024 and
+  // 1.885 -> 1.86 ms at bs128, same box; PCA_HALO_ILV=0 issues each stage's pieces as a block)
   static const int ilv = [] {
     const char* e = getenv("PCA_HALO_ILV");
-    return e && e[0] == '1' ? 1 : 0;
+    return e && e[0] == '0' ? 0 : 1;
   }();
   g.ilv = ilv;
   return true;
