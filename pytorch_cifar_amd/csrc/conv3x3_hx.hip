@@ -52,6 +52,10 @@ struct HxGeom {
 #define PCA_HX_PREFETCH_Y 0
 #endif
 constexpr bool kHxPrefetchY = PCA_HX_PREFETCH_Y != 0;
+#ifndef PCA_HX_DMA_AFTER_READ
+#define PCA_HX_DMA_AFTER_READ 0
+#endif
+constexpr bool kHxDmaAfterRead = PCA_HX_DMA_AFTER_READ != 0;   // (forward only: the dgrad spills more)
 // MODE 3 (dual-BN third sum) is compiled out: its 48 per-lane sums spill the 8-wave variants
 // (180+ registers); the dual-BN block-tail dgrads stay on the generic igemm
 constexpr bool kHxDual = false;
@@ -259,12 +263,17 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
           }
         }
         raw_barrier();
-        // next tap's weights (past the last tile: harmless re-load of real rows)
-        if (tap < TAPS - 1) b_tile(tap + 1, ch, (bc + 1) & 1);
-        else b_tile(0, last_chunk ? 0 : ch + 1, (bc + 1) & 1);
+        // next tap's weights (past the last tile: harmless re-load of real rows), then this tap's
+        // halo pieces of the next chunk (the vmcnt waits above count on that order)
+        auto tap_dma = [&]() {
+          if (tap < TAPS - 1) b_tile(tap + 1, ch, (bc + 1) & 1);
+          else b_tile(0, last_chunk ? 0 : ch + 1, (bc + 1) & 1);
 #pragma unroll
-        for (int k = 0; k < SH::HS; ++k)
-          if (k % (TAPS - 1) == tap) halo_piece(h_t, h_ch, (hc + 1) & 1, k);   // wave-uniform
+          for (int k = 0; k < SH::HS; ++k)
+            if (k % (TAPS - 1) == tap) halo_piece(h_t, h_ch, (hc + 1) & 1, k);   // wave-uniform
+        };
+        constexpr bool dma_after = kHxDmaAfterRead && MODE == 0;
+        if constexpr (!dma_after) tap_dma();
         if constexpr (DGRAD) {
           if (last_chunk && tap == TAPS - 1) {
             // epilogue operands (residual-gradient addend; BN input y + ReLU mask), read
@@ -312,6 +321,15 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
         for (int h = 0; h < 2; ++h) {
           bf16x8 fa[4], fb[4];
           load_half(h, fa, fb);
+          if constexpr (dma_after) {
+            // (build-time PCA_HX_DMA_AFTER_READ: the first half's fragment reads go out before the
+            // tap's DMA pieces, whose issue cycles then cover the reads' LDS latency)
+            if (h == 0) {
+              __builtin_amdgcn_sched_barrier(0);
+              tap_dma();
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
           mfma_half(fa, fb);
         }
       }

@@ -495,8 +495,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       // second workgroup per CU): the next stage's DMA pieces go out after the first quarter of
       // this step's MFMAs instead of before its fragment reads (their issue cycles then overlap
       // the matrix pipe)
-      constexpr bool dspread = PCA_IGEMM_DMA_SPREAD != 0;
-      if constexpr (!dspread) issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);   // past-the-end stages load zeros
+      // PCA_IGEMM_DMA_SPREAD=2: issued after this step's fragment reads, before its MFMAs (the
+      // reads' LDS latency then runs under the DMA issue)
+      constexpr bool dspread = PCA_IGEMM_DMA_SPREAD == 1;
+      constexpr bool dafter = PCA_IGEMM_DMA_SPREAD == 2;
+      if constexpr (!dspread && !dafter) issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);   // past-the-end stages load zeros
       const char* As = smem + (rel % STAGES) * STAGE;
       const char* Bs = As + A_BYTES;
       // all fragments of the K-step are read up front into distinct registers (the compiler
@@ -518,6 +521,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (dafter) {
+        issue(kt + STAGES - 1, (rel + STAGES - 1) % STAGES);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk)
