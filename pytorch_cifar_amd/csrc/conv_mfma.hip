@@ -109,10 +109,12 @@ __device__ __forceinline__ void bn_fuse_flush(float* red, const float* s1, const
                                               int CG, int ch0, int cvalid, int Co, float* part,
                                               int row, int shards, int NS = 2) {
   const int tid = threadIdx.x;
+  // planar [16][NT] (consecutive lanes write / read consecutive words: no bank conflicts; the
+  // interleaved [NT][16] form was 16-way)
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    red[tid * 16 + q] = s1[q];
-    red[tid * 16 + 8 + q] = s2[q];
+    red[q * NT + tid] = s1[q];
+    red[(8 + q) * NT + tid] = s2[q];
   }
   __syncthreads();
   if (tid < CG && tid * 8 < cvalid) {
@@ -121,7 +123,7 @@ __device__ __forceinline__ void bn_fuse_flush(float* red, const float* s1, const
     for (int q = 0; q < 16; ++q) a[q] = 0.f;
     for (int j = tid; j < NT; j += CG)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) a[q] += red[j * 16 + q];
+      for (int q = 0; q < 16; ++q) a[q] += red[q * NT + j];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       stat_out(part, row, shards, NS * Co, ch0 + tid * 8 + q, a[q]);
@@ -137,7 +139,7 @@ __device__ __forceinline__ void bn_fuse_flush3(float* red, const float* s3, int 
                                                int shards) {
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) red[tid * 8 + q] = s3[q];
+  for (int q = 0; q < 8; ++q) red[q * NT + tid] = s3[q];   // (planar: conflict-free)
   __syncthreads();
   if (tid < CG && tid * 8 < cvalid) {
     float a[8];
@@ -145,7 +147,7 @@ __device__ __forceinline__ void bn_fuse_flush3(float* red, const float* s3, int 
     for (int q = 0; q < 8; ++q) a[q] = 0.f;
     for (int j = tid; j < NT; j += CG)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) a[q] += red[j * 8 + q];
+      for (int q = 0; q < 8; ++q) a[q] += red[q * NT + j];
 #pragma unroll
     for (int q = 0; q < 8; ++q) stat_out(part, row, shards, 3 * Co, 2 * Co + ch0 + tid * 8 + q, a[q]);
   }
@@ -1476,21 +1478,29 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       *reinterpret_cast<uint4*>(Y + o) = pv;
     }
   }
+  // block reductions below: planes [sum][RP x Co] written as float4 pairs (consecutive lanes,
+  // consecutive 32-byte runs) and read with consecutive lanes on consecutive channels — the
+  // interleaved [row][channel][sum] layout was 12-19 extra LDS cycles per access
+  constexpr int PL = 2048;   // RP * Co = 256 / CG * 8 * CG
+  auto put8 = [&](int plane, const float* v) {
+    float4* d = reinterpret_cast<float4*>(red + plane * PL + rr * Co + cg * 8);
+    d[0] = make_float4(v[0], v[1], v[2], v[3]);
+    d[1] = make_float4(v[4], v[5], v[6], v[7]);
+  };
   if (bnp) {   // fused BN-backward reduce: one slab row per block (rows = gridDim.x)
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      red[(rr * Co + cg * 8 + q) * 3 + 0] = active ? bs1[q] : 0.f;
-      red[(rr * Co + cg * 8 + q) * 3 + 1] = active ? bs2[q] : 0.f;
-      red[(rr * Co + cg * 8 + q) * 3 + 2] = active ? bs3[q] : 0.f;
+    if (active) {
+      put8(0, bs1);
+      put8(1, bs2);
+      put8(2, bs3);
     }
     __syncthreads();
     for (int c = tid; c < Co; c += 256) {
       float s0 = 0.f, q0 = 0.f, t0 = 0.f;
       for (int k = 0; k < RP; ++k) {
-        s0 += red[(k * Co + c) * 3 + 0];
-        q0 += red[(k * Co + c) * 3 + 1];
-        t0 += red[(k * Co + c) * 3 + 2];
+        s0 += red[k * Co + c];
+        q0 += red[PL + k * Co + c];
+        t0 += red[2 * PL + k * Co + c];
       }
       stat_out(bnp, blockIdx.x, shards, NSB * Co, c, s0);
       stat_out(bnp, blockIdx.x, shards, NSB * Co, Co + c, q0);
@@ -1500,18 +1510,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
   if constexpr (STATS) {
     if (active) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        red[(rr * Co + cg * 8 + q) * 2 + 0] = sm[q];
-        red[(rr * Co + cg * 8 + q) * 2 + 1] = sq[q];
-      }
+      put8(0, sm);
+      put8(1, sq);
     }
     __syncthreads();
     for (int c = tid; c < Co; c += 256) {
       float s0 = 0.f, q0 = 0.f;
       for (int k = 0; k < RP; ++k) {
-        s0 += red[(k * Co + c) * 2 + 0];
-        q0 += red[(k * Co + c) * 2 + 1];
+        s0 += red[k * Co + c];
+        q0 += red[PL + k * Co + c];
       }
       stat_out(stats, blockIdx.x, shards, 2 * Co, c, s0);
       stat_out(stats, blockIdx.x, shards, 2 * Co, Co + c, q0);
