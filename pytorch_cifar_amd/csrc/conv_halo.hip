@@ -56,21 +56,6 @@ __device__ __forceinline__ bf16x8 tr_frag_rows(const char* base, int r0, int r1,
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// Halo-image chunk swizzle. The four 8-pixel lane groups of a transposed B-fragment read sit 8
-// pixels apart: on the 32 / 16-wide maps that is +8 / +8..+24 halo rows (bit 3 of the row flips:
-// tr_swz spreads them), on the 8 / 4-wide maps +16 / +16..+48 rows, which leave bits 0-3 — and so
-// tr_swz — unchanged: all four groups hit the same banks (85-138 % extra LDS cycles per access in
-// the round-4 counters). There bits 4-6 of the row are folded into the swizzle as well (the group
-// offsets 0/16/32/48 rows on the 8-wide map and 0/16/48/64 across the 4-wide map's image slots
-// then land on four different chunk pairs).
-template <int W>
-__device__ __forceinline__ int halo_swz(int R) {
-  if constexpr (W <= 8)
-    return 2 * ((((R >> 1) ^ (R >> 4)) & 1) | ((((R >> 3) ^ (R >> 5) ^ (R >> 6)) & 1) << 1));
-  else
-    return tr_swz<128>(R);
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vmcnt_rt(int n) {
   // counted wait with a wave-uniform runtime count (n <= N)
@@ -184,7 +169,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
       const int jr = rem / W2P, c = rem - jr * W2P;
       const bool ok = hr < SH::HR && c < W + 2;
       s_a[j] = (ok << 24) | (img << 16) | (jr << 8) | c;
-      s_b[j] = (((lane & 7) ^ halo_swz<W>(hr)) << 4) + (grp * g.cin_g + cib * 64) * 2;
+      s_b[j] = (((lane & 7) ^ tr_swz<128>(hr)) << 4) + (grp * g.cin_g + cib * 64) * 2;
     } else if (t < T) {
       const int q = t - SH::HI;
       const int r = 8 * (q % DYI) + row8;
@@ -235,11 +220,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   //   row R = prow + kh*W2P + kw,  byte = R*128 + ((c0/8 ^ swz(R)) << 4) + L
   // and swz(R) = swz(prow + kw) ^ (kh*W2P/8 odd ? 4 : 0) because W2P % 8 == 0. K-step ks of a
   // stage covers the stage pixels 32*ks .. 32*ks + 31.
-  // (W <= 8: halo_swz mixes bits the tap shift kh*W2P carries into, so the swizzle is computed
-  // per read from the full row R = prow + kh*W2P + kw instead)
-  constexpr bool RSWZ = W <= 8;
-  int rbase[KS][2], swk[KS][2][3], prw[KS][2];
-  const int Lb = (((lane & 3) >> 1) << 4) + ((lane & 1) << 3);
+  int rbase[KS][2], swk[KS][2][3];
   {
     const int q = (lane & 15) >> 2, pq = lane & 3;
     const int L = ((pq >> 1) << 4) + ((pq & 1) << 3);
@@ -252,9 +233,8 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
         const int jj = rr / W, ow = rr - jj * W;
         const int prow = img * (SH::RS + 2) * W2P + jj * W2P + ow;
         rbase[ks][h] = prow * 128 + L;
-        prw[ks][h] = prow;
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) swk[ks][h][kw] = RSWZ ? 0 : tr_swz<128>(prow + kw) << 4;
+        for (int kw = 0; kw < 3; ++kw) swk[ks][h][kw] = tr_swz<128>(prow + kw) << 4;
       }
   }
 
@@ -293,19 +273,12 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
         const int n = wn * WTN + ni * 16;
         const int tap = tap0 + (n >> 6), kh = tap / 3, kw = tap % 3;
         const int c0 = n & 63;
-        int a0, a1;
-        if constexpr (RSWZ) {
-          const int R0 = prw[ks][0] + kh * W2P + kw, R1 = prw[ks][1] + kh * W2P + kw;
-          a0 = R0 * 128 + Lb + (((c0 >> 3) ^ halo_swz<W>(R0)) << 4);
-          a1 = R1 * 128 + Lb + (((c0 >> 3) ^ halo_swz<W>(R1)) << 4);
-        } else {
-          const int cx = ((c0 >> 3) ^ (((kh * W2P / 8) & 1) ? 4 : 0)) << 4;
-          const int rsh = (kh * W2P + kw) * 128;
-          a0 = rbase[ks][0] + rsh + (cx ^ swk[ks][0][kw]);
-          a1 = rbase[ks][1] + rsh + (cx ^ swk[ks][1][kw]);
-        }
-        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(S + a0));
-        const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(S + a1));
+        const int cx = ((c0 >> 3) ^ (((kh * W2P / 8) & 1) ? 4 : 0)) << 4;
+        const int rsh = (kh * W2P + kw) * 128;
+        const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_i16x4*)(S + rbase[ks][0] + rsh + (cx ^ swk[ks][0][kw])));
+        const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_i16x4*)(S + rbase[ks][1] + rsh + (cx ^ swk[ks][1][kw])));
         const bf16x8 bfv = __builtin_bit_cast(bf16x8, (i16x8)__builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
