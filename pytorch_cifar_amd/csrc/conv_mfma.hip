@@ -35,6 +35,12 @@
 #ifndef PCA_IGEMM_DMA_SPREAD
 #define PCA_IGEMM_DMA_SPREAD 0
 #endif
+// rows per thread whose epilogue operands are loaded together (store-loop chunk). 1: the
+// operands of a row go out together (the per-operand waits are gone); 2 and 4 hold more rows'
+// operands at once and spilled the 256x128 dgrad (2 and 4: 7 and 38 VGPRs), measured slower.
+#ifndef PCA_IGEMM_EU
+#define PCA_IGEMM_EU 1
+#endif
 
 namespace pca {
 
@@ -87,6 +93,33 @@ __device__ __forceinline__ void bn_fuse_acc(const uint4& v, const bf16* y, uint8
   }
 }
 
+// the same with y already in registers (the batched store loop of the igemm epilogue)
+__device__ __forceinline__ void bn_fuse_acc_v(const uint4& v, const uint4& yv, uint8_t m,
+                                              const float* mean, const float* istd, float* s1,
+                                              float* s2) {
+  float f[8], yy[8];
+  unpack8(v, f);
+  unpack8(yv, yy);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
+    s1[q] += dz;
+    s2[q] += dz * (yy[q] - mean[q]) * istd[q];
+  }
+}
+
+__device__ __forceinline__ void bn_fuse_acc3_v(const uint4& v, const uint4& y2v, uint8_t m,
+                                               const float* m2, const float* i2, float* s3) {
+  float f[8], yy[8];
+  unpack8(v, f);
+  unpack8(y2v, yy);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
+    s3[q] += dz * (yy[q] - m2[q]) * i2[q];
+  }
+}
+
 // dual-BN third sum from mean2 / istd2 already in LDS or registers (m2, i2: this vector's 8
 // channels)
 __device__ __forceinline__ void bn_fuse_acc3s(const uint4& v, const bf16* y2, uint8_t m,
@@ -101,55 +134,35 @@ __device__ __forceinline__ void bn_fuse_acc3s(const uint4& v, const bf16* y2, ui
   }
 }
 
-// block reduction of the per-thread (s1, s2) of channel group c8 = tid % CG (NT % CG == 0) into
-// slab row `row`; channel base ch0 of group 0 (red: NT * 16 floats of LDS); NS = row stride in
-// units of Co (2, or 3 for a dual BN's accumulator)
-template <int NT>
-__device__ __forceinline__ void bn_fuse_flush(float* red, const float* s1, const float* s2,
-                                              int CG, int ch0, int cvalid, int Co, float* part,
-                                              int row, int shards, int NS = 2) {
-  const int tid = threadIdx.x;
-  // planar [16][NT] (consecutive lanes write / read consecutive words: no bank conflicts; the
-  // interleaved [NT][16] form was 16-way)
+// block reduction of NSUM per-thread 8-channel sums v[NSUM*8] of channel group c8 = tid % CG
+// (CG | 64) into slab row `row`, sums s0 .. s0+NSUM-1 of a row of NS sums per channel (row stride
+// NS * Co); channel base ch0 of group 0. The lanes of a wave that share a group (lane % CG) are
+// folded by a butterfly first, so LDS holds one row per wave ([NW][NSUM*8][CG]) and each output
+// is an NW-term sum by its own thread (the per-thread planar form left CG threads summing
+// NT/CG rows each while the block waited).
+template <int NT, int CG, int NSUM>
+__device__ __forceinline__ void bn_flush_block(float* red, float* v, int ch0, int cvalid, int Co,
+                                               float* part, int row, int shards, int NS, int s0) {
+  constexpr int NW = NT / 64, NV = NSUM * 8;
+  static_assert(CG >= 1 && CG <= 64 && (64 % CG) == 0, "channel groups per wave");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    red[q * NT + tid] = s1[q];
-    red[(8 + q) * NT + tid] = s2[q];
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int x = CG; x < 64; x <<= 1) v[i] += __shfl_xor(v[i], x, 64);
+  if (lane < CG) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[(w * NV + i) * CG + lane] = v[i];
   }
   __syncthreads();
-  if (tid < CG && tid * 8 < cvalid) {
-    float a[16];
+  for (int j = tid; j < NV * CG; j += NT) {   // j = i * CG + c8
+    const int i = j / CG, c = (j % CG) * 8 + (i & 7);
+    if (c < cvalid) {
+      float a = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) a[q] = 0.f;
-    for (int j = tid; j < NT; j += CG)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) a[q] += red[q * NT + j];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      stat_out(part, row, shards, NS * Co, ch0 + tid * 8 + q, a[q]);
-      stat_out(part, row, shards, NS * Co, Co + ch0 + tid * 8 + q, a[8 + q]);
+      for (int ww = 0; ww < NW; ++ww) a += red[ww * NV * CG + j];
+      stat_out(part, row, shards, (size_t)NS * Co, (s0 + (i >> 3)) * Co + ch0 + c, a);
     }
-  }
-}
-
-// per-tile flush of the dual third sum (accumulator mode: atomics into shard row % shards)
-template <int NT>
-__device__ __forceinline__ void bn_fuse_flush3(float* red, const float* s3, int CG, int ch0,
-                                               int cvalid, int Co, float* part, int row,
-                                               int shards) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) red[q * NT + tid] = s3[q];   // (planar: conflict-free)
-  __syncthreads();
-  if (tid < CG && tid * 8 < cvalid) {
-    float a[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) a[q] = 0.f;
-    for (int j = tid; j < NT; j += CG)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) a[q] += red[q * NT + j];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) stat_out(part, row, shards, 3 * Co, 2 * Co + ch0 + tid * 8 + q, a[q]);
   }
 }
 
@@ -625,12 +638,26 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
 #pragma unroll
     for (int q = 0; q < 8; ++q) bs3[q] = 0.f;
     const bool dual = bnf && g.bn_y2 != nullptr;
+    // Store loop in chunks of EU rows per thread: every global operand of a chunk (addend, y,
+    // mask, y2) is loaded before any is used, so a chunk costs one memory round trip instead of
+    // one per row and operand (the per-row guarded form waited vmcnt(0) up to 3x per row:
+    // addend, then y + mask, then y2).
+    // Rows past M / channels past Cn load from offset 0 (always valid) and are never stored.
+    constexpr int EIT = (BM * CG) / NT;
+    constexpr int EU = EIT >= PCA_IGEMM_EU ? PCA_IGEMM_EU : EIT;
+    static_assert(EIT % EU == 0, "store loop chunks");
+    const int c8 = tid % CG;   // (NT % CG == 0: fixed per thread)
+    const int gc = n0 + c8 * 8;
+#pragma unroll 1
+    for (int it0 = 0; it0 < EIT; it0 += EU) {
+      size_t o[EU];
+      bool ok[EU];
+      uint4 av[EU], yv[EU], y2v[EU];
+      uint8_t mk[EU];
 #pragma unroll
-    for (int it = 0; it < (BM * CG) / NT; ++it) {
-      const int idx = tid + it * NT;
-      const int r = idx / CG, c8 = idx % CG;
-      const int gm = m0 + r, gc = n0 + c8 * 8;
-      if (gm < Mrows && gc < g.Cn) {
+      for (int u = 0; u < EU; ++u) {
+        const int gm = m0 + (tid + (it0 + u) * NT) / CG;
+        ok[u] = gm < Mrows && gc < g.Cn;
         size_t pix = gm;
         if constexpr (PARITY) {
           const uint32_t n = fdiv(gm, g.fd_hw);
@@ -639,35 +666,55 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
           const uint32_t w = rem - h * rows_w;
           pix = ((size_t)n * g.Ho + 2 * h + ph) * g.Wo + 2 * w + pw;
         }
+        o[u] = ok[u] ? pix * g.Co + (size_t)grp * g.Cn + gc : 0;
+      }
+      if (addend) {
+#pragma unroll
+        for (int u = 0; u < EU; ++u) av[u] = *reinterpret_cast<const uint4*>(addend + o[u]);
+      }
+      if (bnf) {
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+          yv[u] = *reinterpret_cast<const uint4*>(g.bn_y + o[u]);
+          mk[u] = g.bn_mask[o[u] >> 3];
+        }
+      }
+      if (dual) {
+#pragma unroll
+        for (int u = 0; u < EU; ++u) y2v[u] = *reinterpret_cast<const uint4*>(g.bn_y2 + o[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int r = (tid + (it0 + u) * NT) / CG;
         uint4 v = *reinterpret_cast<const uint4*>(Cs + r * CST + c8 * 8);
-        const size_t o = pix * g.Co + (size_t)grp * g.Cn + gc;
         if (addend) {
           // fused gradient accumulation (dgrad): dX = conv^T(dY) + the other branch's dX
           float a[8], b[8];
           unpack8(v, a);
-          unpack8(*reinterpret_cast<const uint4*>(addend + o), b);
+          unpack8(av[u], b);
 #pragma unroll
           for (int q = 0; q < 8; ++q) a[q] += b[q];
           v = pack8(a);
         }
-        if (bnf) bn_fuse_acc(v, g.bn_y + o, g.bn_mask[o >> 3], bmean, bistd, bs1, bs2);
+        const uint8_t m = ok[u] ? mk[u] : 0;   // (masked-off rows add nothing to the sums)
+        if (bnf) bn_fuse_acc_v(v, yv[u], m, bmean, bistd, bs1, bs2);
         if (dual) {
           if constexpr (AUX2_LDS) {
             const float* aux2s = reinterpret_cast<const float*>(smem + AUX2_OFF) + c8 * 8;
-            bn_fuse_acc3s(v, g.bn_y2 + o, g.bn_mask[o >> 3], aux2s, aux2s + BN, bs3);
+            bn_fuse_acc3_v(v, y2v[u], m, aux2s, aux2s + BN, bs3);
           } else {   // (configs whose LDS would cost occupancy: from global, L1-cached)
             const float* a2 = g.bn_aux2 + grp * g.Cn + gc;
-            bn_fuse_acc3s(v, g.bn_y2 + o, g.bn_mask[o >> 3], a2, a2 + g.Co, bs3);
+            bn_fuse_acc3_v(v, y2v[u], m, a2, a2 + g.Co, bs3);
           }
         }
-        *reinterpret_cast<uint4*>(Y + o) = v;
+        if (ok[u]) *reinterpret_cast<uint4*>(Y + o[u]) = v;
       }
     }
     __syncthreads();   // the C tile aliases the ring the next tile's prologue refills
     if constexpr (DGRAD && !SPLITK) {
       if (dual) {   // (epilogue-local: no accumulator registers live across the K loop)
-        bn_fuse_flush3<NT>(reinterpret_cast<float*>(smem), bs3, CG_, grp * g.Cn + n0, g.Cn - n0,
-                           g.Co, g.bn_part, (int)blockIdx.x, g.shards);
+        bn_flush_block<NT, CG_, 1>(reinterpret_cast<float*>(smem), bs3, grp * g.Cn + n0,
+                                   g.Cn - n0, g.Co, g.bn_part, (int)blockIdx.x, g.shards, 3, 2);
         __syncthreads();
       }
     }
@@ -676,8 +723,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
   if constexpr (DGRAD && !SPLITK) {
     if (bnf) {   // slab row per (M-walker, parity class); channels of this block's N tile
       const int row = PARITY ? (int)blockIdx.x * 4 + cls : (int)blockIdx.x;
-      bn_fuse_flush<NT>(reinterpret_cast<float*>(smem), bs1, bs2, CG_, grp * g.Cn + n0,
-                        g.Cn - n0, g.Co, g.bn_part, row, g.shards, g.bn_y2 ? 3 : 2);
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        v[q] = bs1[q];
+        v[8 + q] = bs2[q];
+      }
+      bn_flush_block<NT, CG_, 2>(reinterpret_cast<float*>(smem), v, grp * g.Cn + n0, g.Cn - n0,
+                                 g.Co, g.bn_part, row, g.shards, g.bn_y2 ? 3 : 2, 0);
     }
   }
   if constexpr (STATS && !SPLITK) {
