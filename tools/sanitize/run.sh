@@ -1,13 +1,14 @@
 #!/bin/bash
 # Host-only AddressSanitizer + UBSan build of the kernel library's planning code and the harness
-# (device code compiled as usual, uninstrumented; nothing is launched). CPU only.
+# (device code compiled as usual at -O3, uninstrumented: the -O1 device build of the halo wgrad
+# DMA issue hits a gfx950 backend register-class error; nothing is launched). CPU only.
 set -e
 ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
 OUT=${SAN_OUT:-/tmp/pca_sanitize}
 mkdir -p "$OUT"
 CSRC="$ROOT/pytorch_cifar_amd/csrc"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
-FLAGS="-x hip --offload-arch=gfx950 -O1 -g -std=c++17 -fno-omit-frame-pointer \
+FLAGS="-x hip --offload-arch=gfx950 -O3 -Xarch_host -O1 -Xarch_host -g -std=c++17 -fno-omit-frame-pointer \
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
   -I$CSRC -Wno-unused-result -Wno-unused-command-line-argument"
 objs=()
