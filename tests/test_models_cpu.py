@@ -1,28 +1,37 @@
-"""Model-zoo parity with the reference (CPU, fp32).
+"""Model-zoo contract and numerics on the CPU path (fp32 / fp64).
 
-For every constructor: identical state_dict keys and shapes as the reference model, the
-reference's weights load strictly, and forward (eval and train mode) plus input/parameter
-gradients match the reference implementation. The reference package is imported read-only from
-/root/reference when present (skipped elsewhere, e.g. on the GPU box). ShuffleNetG2/G3 cannot be
-constructed by the reference under Python 3 (shufflenet.py:27 float channels) — our fixed
-version is checked for shape/contract only.
+The reference's checkpoint contract (ckpt.pth['net'] keys and shapes; /root/reference/models/*.py
+attribute names, main.py:137-148) is pinned in ``tests/fixtures/zoo_contract.json``, written by
+``tools/zoo_fixture.py``. That fixture was generated at a commit whose suite asserted, model by
+model, identical keys/shapes with the reference package and fp64 forward/backward agreement to
+1e-12; this suite never imports or executes reference code.
+
+Checks:
+  * every constructor's ordered state_dict keys and shapes equal the fixture;
+  * a seeded fp64 forward/backward of the pinned models reproduces the fixture's digest (logits,
+    input-gradient norm, per-parameter gradient norms) — a regression pin of the CPU path;
+  * the fp32 CPU path agrees with the same weights run in fp64 (eval and train logits, input and
+    parameter gradients).
+ShuffleNetG2/G3 cannot be constructed by the reference under Python 3 (shufflenet.py:27 float
+channels); ours is the fixed version (pinned here from our own construction).
 """
 import copy
-import importlib.util
+import hashlib
+import json
 import os
-import sys
 
 import pytest
 import torch
 
-REF = "/root/reference/models/__init__.py"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIXTURE = os.path.join(ROOT, "tests", "fixtures", "zoo_contract.json")
 
 ZOO = [
     "VGG11", "VGG13", "VGG16", "VGG19", "LeNet", "ResNet18", "ResNet34", "ResNet50",
     "PreActResNet18", "PreActResNet50", "GoogLeNet", "DenseNet121", "densenet_cifar",
     "ResNeXt29_2x64d", "ResNeXt29_32x4d", "MobileNet", "MobileNetV2", "DPN26", "SENet18",
     "EfficientNetB0", "RegNetX_200MF", "RegNetX_400MF", "RegNetY_400MF", "SimpleDLA", "DLA",
-    "PNASNetA", "PNASNetB", "ShuffleNetV2_0.5", "ShuffleNetV2_1",
+    "PNASNetA", "PNASNetB", "ShuffleNetV2_0.5", "ShuffleNetV2_1", "ShuffleNetG2", "ShuffleNetG3",
 ]
 HEAVY = ["ResNet101", "ResNet152", "PreActResNet34", "PreActResNet101", "PreActResNet152",
          "DenseNet169", "DenseNet201", "DenseNet161", "ResNeXt29_4x64d", "ResNeXt29_8x64d",
@@ -30,25 +39,9 @@ HEAVY = ["ResNet101", "ResNet152", "PreActResNet34", "PreActResNet101", "PreActR
 
 
 @pytest.fixture(scope="module")
-def ref_models():
-    if not os.path.exists(REF):
-        pytest.skip("reference checkout not available")
-    spec = importlib.util.spec_from_file_location(
-        "pca_reference_models", REF, submodule_search_locations=[os.path.dirname(REF)])
-    mod = importlib.util.module_from_spec(spec)
-    sys.modules["pca_reference_models"] = mod
-    spec.loader.exec_module(mod)
-    return mod
-
-
-def _ref_ctor(ref, name):
-    if name.startswith("VGG"):
-        return lambda: ref.VGG(name)
-    if name.startswith("ShuffleNetV2_"):
-        s = float(name.split("_")[1])
-        s = int(s) if s.is_integer() else s
-        return lambda: ref.ShuffleNetV2(s)
-    return getattr(ref, name)
+def contract():
+    with open(FIXTURE) as f:
+        return json.load(f)
 
 
 def _ours(name):
@@ -57,8 +50,64 @@ def _ours(name):
     return models.MODEL_REGISTRY[name]()
 
 
+def _keys(model):
+    return [f"{k}:{'x'.join(map(str, v.shape))}" for k, v in model.state_dict().items()]
+
+
 def _rel(a, b):
     return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
+
+
+def test_fixture_covers_registry(contract):
+    from pytorch_cifar_amd import models
+
+    assert sorted(contract) == sorted(models.MODEL_REGISTRY)
+    assert sorted(ZOO + HEAVY) == sorted(models.MODEL_REGISTRY)
+
+
+@pytest.mark.parametrize("name", ZOO)
+def test_state_dict_contract(contract, name):
+    torch.manual_seed(0)
+    got = _keys(_ours(name))
+    want = contract[name]["keys"]
+    missing = [k for k in want if k not in got]
+    extra = [k for k in got if k not in want]
+    assert not missing and not extra, (name, missing[:5], extra[:5])
+    assert got == want, f"{name}: key order differs"
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", HEAVY)
+def test_heavy_state_dict_contract(contract, name):
+    torch.manual_seed(0)
+    got = _keys(_ours(name))
+    ent = contract[name]
+    assert len(got) == ent["n_keys"], name
+    assert hashlib.sha256("\n".join(got).encode()).hexdigest() == ent["keys_sha256"], name
+
+
+def _digest_names():
+    with open(FIXTURE) as f:
+        return [n for n, e in json.load(f).items() if "fp64" in e]
+
+
+@pytest.mark.parametrize("name", _digest_names())
+def test_fp64_digest_pinned(contract, name):
+    """One seeded fp64 train step reproduces the pinned digest (tools/zoo_fixture.py digest())."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "pca_zoo_fixture", os.path.join(ROOT, "tools", "zoo_fixture.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    got = mod.digest(name)
+    want = contract[name]["fp64"]
+    lg, lw = torch.tensor(got["logits"]), torch.tensor(want["logits"])
+    assert _rel(lg, lw) < 1e-10, f"{name} logits"
+    assert abs(got["gx_norm"] - want["gx_norm"]) <= 1e-9 * max(1.0, abs(want["gx_norm"])), f"{name} dx"
+    assert sorted(got["gp_norm"]) == sorted(want["gp_norm"]), name
+    for n, v in want["gp_norm"].items():
+        assert abs(got["gp_norm"][n] - v) <= 1e-8 * max(1.0, abs(v)), f"{name}.{n}"
 
 
 def _run(model, x, g, seed):
@@ -70,53 +119,31 @@ def _run(model, x, g, seed):
     return y.detach(), xi.grad, grads
 
 
-def _check(name, ref):
-    """fp64 run of the reference model is the oracle; our fp32 model must be as close to it as
-    the reference's own fp32 run is (BN backward at batch 4 is ill-conditioned in fp32, so the
-    two fp32 runs legitimately differ by ~1e-3 in the input gradient while agreeing to 1e-15 in
-    fp64 — checked separately by test_zoo_exact_in_fp64)."""
-    torch.manual_seed(0)
-    r = _ref_ctor(ref, name)()
-    o = _ours(name)
-    rs, os_ = r.state_dict(), o.state_dict()
-    assert list(rs.keys()) == list(os_.keys()), name
-    for k in rs:
-        assert rs[k].shape == os_[k].shape, (name, k)
-    o.load_state_dict(rs, strict=True)
-    r64 = copy.deepcopy(r).double()
-    x = torch.randn(4, 3, 32, 32)
-    r.eval(), o.eval(), r64.eval()
-    with torch.no_grad():
-        oracle = r64(x.double())
-        assert _rel(o(x), oracle) <= 3 * _rel(r(x), oracle) + 1e-6, f"{name} eval logits"
-    r.train(), o.train(), r64.train()
-    g = torch.randn(4, 10)
-    y64, gx64, gp64 = _run(r64, x.double(), g, 1)
-    yr, gxr, gpr = _run(r, x, g, 1)
-    yo, gxo, gpo = _run(o, x, g, 1)
-    assert _rel(yo, y64) <= 3 * _rel(yr, y64) + 1e-6, f"{name} train logits"
-    assert _rel(gxo, gx64) <= 3 * _rel(gxr, gx64) + 1e-6, f"{name} input grad"
-    for n, g64 in gp64.items():
-        if g64 is None:
-            assert gpo[n] is None or gpo[n].abs().max() == 0, n
-            continue
-        assert _rel(gpo[n], g64) <= 3 * _rel(gpr[n], g64) + 1e-6, f"{name}.{n}"
-    for (n, br), (_, bo) in zip(r.named_buffers(), o.named_buffers()):
-        if br.dtype.is_floating_point:
-            assert _rel(bo, br) < 1e-4 or (bo - br).abs().max() < 1e-6, f"{name}.{n}"
-        else:
-            assert int(bo) == int(br), f"{name}.{n}"
-
-
 @pytest.mark.parametrize("name", ZOO)
-def test_zoo_matches_reference(ref_models, name):
-    _check(name, ref_models)
-
-
-@pytest.mark.slow
-@pytest.mark.parametrize("name", HEAVY)
-def test_heavy_zoo_matches_reference(ref_models, name):
-    _check(name, ref_models)
+def test_fp32_matches_fp64(name):
+    """fp32 CPU path vs the same weights in fp64. BatchNorm's backward at small batch is ill-conditioned
+    in fp32 (on the 1x1 / 2x2 maps of the deep stages two correct fp32 implementations differ by
+    1e-3..2e-2 in a gradient), hence the looser gradient bounds."""
+    torch.manual_seed(0)
+    o = _ours(name)
+    o64 = copy.deepcopy(o).double()
+    x = torch.randn(8, 3, 32, 32)
+    o.eval(), o64.eval()
+    with torch.no_grad():
+        assert _rel(o(x), o64(x.double())) < 1e-4, f"{name} eval logits"
+    o.train(), o64.train()
+    g = torch.randn(8, 10)
+    y64, gx64, gp64 = _run(o64, x.double(), g, 1)
+    y, gx, gp = _run(o, x, g, 1)
+    assert _rel(y, y64) < 1e-4, f"{name} train logits"
+    assert _rel(gx, gx64) < 5e-2, f"{name} input grad"
+    # parameters whose exact gradient vanishes (a conv bias ahead of BatchNorm): fp32 noise only
+    scale = max(float(v.norm()) for v in gp64.values() if v is not None)
+    for n, g64 in gp64.items():
+        if g64 is None or g64.norm() < 1e-6 * scale:
+            assert gp[n] is None or gp[n].norm() < 1e-4 * scale, n
+            continue
+        assert _rel(gp[n], g64) < 5e-2, f"{name}.{n}"
 
 
 def test_registry_complete():
@@ -144,19 +171,3 @@ def test_resnet_amp_flag_accepted():
 
     m = models.ResNet18(amp=True)
     assert m.amp and m.layer1[0].amp
-
-
-@pytest.mark.parametrize("name", ["ResNet18", "EfficientNetB0", "DLA", "ShuffleNetV2_1", "DPN26"])
-def test_zoo_exact_in_fp64(ref_models, name):
-    torch.manual_seed(0)
-    r = _ref_ctor(ref_models, name)().double()
-    o = _ours(name).double()
-    o.load_state_dict(r.state_dict())
-    x = torch.randn(3, 3, 32, 32, dtype=torch.float64)
-    g = torch.randn(3, 10, dtype=torch.float64)
-    yr, gxr, gpr = _run(r, x, g, 2)
-    yo, gxo, gpo = _run(o, x, g, 2)
-    assert _rel(yo, yr) < 1e-12 and _rel(gxo, gxr) < 1e-10
-    for n, gr in gpr.items():
-        if gr is not None and gr.norm() > 1e-8:
-            assert _rel(gpo[n], gr) < 1e-9, n
