@@ -118,9 +118,16 @@ def lib():
 
 
 def _tune_cache(mod):
-    """PCA_TUNE_CACHE=<file.json>: restore the conv autotuner's choices at load and save them at
-    exit (the reference's cudnn.benchmark re-times every run; here a cache skips the trials, and
-    profiled runs reuse the choices an un-profiled run made)."""
+    """Kernel selection at load: the shipped MI355X tune table (engine/tuning.py; PCA_TUNE_TABLE=0
+    skips it), then PCA_TUNE_CACHE=<file.json>: restore the conv autotuner's choices at load and
+    save them at exit (the reference's cudnn.benchmark re-times every run; here a cache skips the
+    trials, and profiled runs reuse the choices an un-profiled run made)."""
+    try:
+        from .engine.tuning import load_table
+
+        load_table(mod)
+    except Exception:
+        pass
     path = os.environ.get("PCA_TUNE_CACHE")
     if not path or not hasattr(mod, "tune_import"):
         return

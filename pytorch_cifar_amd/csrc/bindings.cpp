@@ -47,6 +47,7 @@ void wgrad_clear_tuned();
 std::vector<std::vector<int>> tune_export();
 void c64_set_prof(int64_t* p);
 int c64_grid_size(int N, int H);
+int c64_version(int v);
 int tune_import(const std::vector<std::vector<int>>& rows);
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
@@ -1830,7 +1831,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
   }, "diagnostics: record c64 per-wave tile stamps into t ([grid][4][16][4] int64) or stop");
   m.def("c64_grid_size", &pca::c64_grid_size);
+  m.def("c64_version", &pca::c64_version,
+        "layer-1 c64 kernel version (2: 16x16x32 MFMA, 3: 32x32x16 plane layout); v < 0 only "
+        "queries; returns the previous version");
   m.def("tune_export", &pca::tune_export, "autotuned conv / wgrad choices as int rows");
+  // bump when a kernel candidate set or a cfg numbering changes: shipped tune tables
+  // (engine/tuning.py) made for another set are then ignored
+  m.def("tune_version", []() { return 5; }, "version of the autotuner's candidate sets");
   m.def("tune_import", &pca::tune_import, "restore rows from tune_export (returns rows taken)");
   m.def("src_digest", []() { return std::string(pca_src_digest); },
         "sha256 of the csrc sources this library was built from (_build.source_digest)");

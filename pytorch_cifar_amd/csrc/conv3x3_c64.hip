@@ -657,6 +657,363 @@ void conv3x3_c64_v1_kernel(const bf16* __restrict__ A, const bf16* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
+// Versions 3 / 4 (opt-in, PCA_C64_V): the same tile plan on v_mfma_f32_32x32x16_bf16.
+//
+// Why: with one wave per SIMD every non-MFMA instruction of the wave (fragment reads, halo DMA
+// pieces, the deferred epilogue's BN sums / packs / stores) has to issue in the MFMA shadow. A
+// 16x16x32 MFMA runs 16 cycles and blocks vector issue for 8 of them (8 free cycles per MFMA);
+// a 32x32x16 runs 32 and blocks 8 (24 free) at the same MACs per cycle
+// (MI355X_MICROARCH.md, vector-instruction issue cost row). The fragment bytes per MAC are the
+// same (a 64x64 wave tile reads 2 A + 2 B fragments per 16-deep K step for 4 MFMAs).
+//   * D[channel][pixel] = W x X^T per 32x32 tile: lane l holds pixel (l & 31) of its tile and,
+//     with the weight rows staged in the permuted order perm32, output channels
+//     32*ct + 16*(l >> 5) + [0, 16) — two 16-byte stores per (pixel tile, channel tile);
+//   * a wave owns two output rows (pixel tiles pt = one 32-wide image row each) x 64 channels;
+//   * LDS "planes": the halo and the weights are stored as 16-channel (32-byte) planes, one per
+//     16-deep K step, so a K step moves a fragment read by an immediate offset (an XOR-swizzled
+//     128-byte row layout needs a separate address register per K step: the compiler hoisted
+//     144 of them and the forward spilled). A 32x32x16 operand read touches 16 consecutive rows per
+//     ds_read_b128 lane group; with 32-byte rows and the two 16-byte halves swapped on rows with
+//     bit 3 set, those 16 rows cover all 64 banks once.
+namespace c64w {
+constexpr int HP = 11;                           // 1 KiB DMA pieces per halo plane (340 rows x 32 B)
+constexpr int HPB = HP * 1024;                   // bytes per halo plane
+constexpr int HB = 4 * HPB;                      // one halo buffer: 4 planes (64 channels)
+constexpr int HI = 4 * HP;                       // 44 pieces per tile: 11 per wave
+constexpr int SLOTS = HI / c64::NW;
+static_assert(c64::BBYTES + 2 * HB <= 160 * 1024, "LDS budget");
+// LDS weight row r (within a 32-row tile) holds output channel perm32(r): accumulator register
+// e of lane half h is D row (e & 3) + 8 (e >> 2) + 4 h -> channel 16 h + e
+__device__ __forceinline__ int perm32(int r) { return ((r >> 2) & 1) * 16 + (r >> 3) * 4 + (r & 3); }
+__device__ __forceinline__ int swz(int r) { return (r >> 3) & 1; }
+}  // namespace c64w
+
+// HPLANE: halo as 16-channel planes (true) or as 128-byte pixel rows with the 16-byte chunks
+// XOR-swizzled by (row >> 1) & 7 (false: each DMA piece moves 8 whole 128-byte lines; a K step
+// is then an XOR of the fragment offset, recomputed per tile instead of hoisted)
+template <bool DGRAD, bool STATS, bool HPLANE = true>
+__global__ __launch_bounds__(256)
+void conv3x3_c64w_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
+                         bf16* __restrict__ Y, float* __restrict__ stats,
+                         const bf16* __restrict__ addend, const C64Geom g) {
+  using c64::W;
+  using c64::W2;
+  using c64::ROWS;
+  using c64::HROWS;
+  using c64::NW;
+  using c64::BBYTES;
+  using c64::BI;
+  using namespace c64w;
+  __shared__ __attribute__((aligned(16))) char smem[2 * HB + BBYTES];
+  char* const Bs = smem + 2 * HB;
+  typedef __attribute__((address_space(3))) const char lds_char;
+  typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+  lds_char* const lds_base = (lds_char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid;                            // output rows 2*wm + pt of the 8-row tile
+  const int h = lane >> 5;                       // 8-channel half of a K step / 16-channel group
+  const int px = lane & 31;                      // x of the lane's pixel
+  const int tiles_per_img = g.H / ROWS;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A, g.a_bytes);
+
+  // ---- halo DMA piece k of a wave: piece i = wid + NW*k = (plane i / HP, rows 32*(i % HP) + l/2),
+  // lane half (l & 1) fetching the 8 channels 16*plane + 8*((l & 1) ^ swz(row)) ----
+  auto issue_piece = [&](int n, int h0, int buf, int k) {
+    const int i = wid + NW * k;
+    int R, ch;
+    if constexpr (HPLANE) {
+      const int plane = i / HP;
+      R = (i - plane * HP) * 32 + (lane >> 1);
+      ch = 16 * plane + 8 * ((lane & 1) ^ swz(R));
+    } else {
+      R = 8 * i + (lane >> 3);
+      ch = 8 * ((lane & 7) ^ ((R >> 1) & 7));
+    }
+    const int j = R / W2, c = R - j * W2;
+    const int ih = h0 + j - 1, iw = c - 1;
+    const bool ok = (R < HROWS) & ((uint32_t)ih < (uint32_t)g.H) & ((uint32_t)iw < (uint32_t)W);
+    const uint32_t off = ok ? (uint32_t)((((n * g.H + ih) * W + iw) * 64 + ch) * 2) : kOOB;
+    dma16(rsA, smem + buf * HB + i * 1024, off);
+  };
+  if (blockIdx.x < g.tiles) {
+    const int n0 = blockIdx.x / tiles_per_img;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) issue_piece(n0, (blockIdx.x - n0 * tiles_per_img) * ROWS, 0, k);
+  }
+  // ---- resident weights: plane P = tap*4 + k (2 KiB) holds the K values tap*64 + 16k + [0,16)
+  // of LDS row n = 32*ct + r (channel 32*ct + perm32(r)), halves swapped on rows with swz(n) ----
+  {
+    const __amdgpu_buffer_rsrc_t rsW = make_rsrc(Wm, BBYTES);
+    for (int i = wid; i < BI; i += NW) {
+      const int P = i >> 1, n = (i & 1) * 32 + (lane >> 1);
+      const int tap = P >> 2, k = P & 3;
+      const int src_tap = DGRAD ? 8 - tap : tap;
+      const int ch = (n & 32) + perm32(n & 31);
+      const int kv = src_tap * 64 + 16 * k + 8 * ((lane & 1) ^ swz(n));
+      dma16(rsW, Bs + i * 1024, (uint32_t)((ch * 576 + kv) * 2));
+    }
+  }
+
+  // fragment byte offsets within a plane: halo row R of tap (kh, kw) for (pt, px); weight row n
+  int aoff[9][2], boff[2];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const int R = (2 * wm + pt + tap / 3) * W2 + px + tap % 3;
+      aoff[tap][pt] = HPLANE ? R * 32 + ((h ^ swz(R)) << 4) : R * 128 + ((h ^ ((R >> 1) & 7)) << 4);
+    }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int n = ct * 32 + px;
+    boff[ct] = n * 32 + ((h ^ swz(n)) << 4);
+  }
+
+  // per-lane BN sums. dgrad (fused BN-backward reduce): channels 32*ct + 16*h + e, kk = that BN's
+  // mean. Forward statistics (shifted by kk = K): lanes 2j and 2j+1 hold the same channels of
+  // different pixels, so each half-part folds the pair with one DPP swap and lane parity o keeps
+  // channels 32*ct + 16*h + 8*eh + 4*o + e (e < 4): 16 channels, index ct*8 + eh*4 + e — 48 fewer
+  // registers than 32 channels of sums + shifts, which spilled the two-accumulator forward.
+  const bool bnf = DGRAD && g.bn_part != nullptr;
+  const int odd = lane & 1;
+  constexpr int NS = DGRAD ? 32 : 16;
+  float st_s[NS], st_q[NS], kk[NS];
+  float bistd[DGRAD ? 32 : 1];
+  auto sum_ch = [&](int i) {   // channel of sum slot i
+    return DGRAD ? 32 * (i >> 4) + 16 * h + (i & 15) : 32 * (i >> 3) + 16 * h + 8 * ((i >> 2) & 1) + 4 * odd + (i & 3);
+  };
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int c = sum_ch(i);
+    st_s[i] = st_q[i] = 0.f;
+    kk[i] = (STATS && g.kshift) ? g.kshift[c] : (bnf ? g.bn_aux[c] : 0.f);
+    if constexpr (DGRAD) bistd[i] = bnf ? g.bn_aux[64 + c] : 0.f;
+  }
+
+  constexpr int STORES = 8;                      // global stores per lane per tile
+  uint4 pre_a[2][2][2], pre_y[2][2][2];
+  uint32_t pre_m[2][2];
+  auto pix_of = [&](size_t pix0p, int pt) { return pix0p + (size_t)(2 * wm + pt) * W + px; };
+  auto pre_load = [&](size_t pix0p) {
+    if constexpr (DGRAD) {
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const size_t o = pix_of(pix0p, pt) * 64 + 32 * ct + 16 * h;
+          if (addend) {
+            pre_a[pt][ct][0] = *reinterpret_cast<const uint4*>(addend + o);
+            pre_a[pt][ct][1] = *reinterpret_cast<const uint4*>(addend + o + 8);
+          }
+          if (bnf) {
+            pre_y[pt][ct][0] = *reinterpret_cast<const uint4*>(g.bn_y + o);
+            pre_y[pt][ct][1] = *reinterpret_cast<const uint4*>(g.bn_y + o + 8);
+            pre_m[pt][ct] = *reinterpret_cast<const uint16_t*>(g.bn_mask + (o >> 3));
+          }
+        }
+    }
+  };
+  // one 8-channel half-part q = (pt, ct, eh) of a finished tile
+  auto epi_part = [&](f32x16 (&Acc)[2][2], int q, size_t pix0p) {
+    const int pt = q >> 2, ct = (q >> 1) & 1, eh = q & 1;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = Acc[pt][ct][eh * 8 + e];
+    if constexpr (STATS) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float keep = odd ? v[4 + e] : v[e];
+        const float send = odd ? v[e] : v[4 + e];
+        // quad_perm [1,0,3,2]: the partner lane's value
+        const float recv = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0xB1, 0xF, 0xF, true));
+        const int i = ct * 8 + eh * 4 + e;
+        const float d1 = keep - kk[i], d2 = recv - kk[i];
+        st_s[i] += d1 + d2;
+        st_q[i] += d1 * d1 + d2 * d2;
+      }
+    }
+    uint4 o = pack8(v);
+    if constexpr (DGRAD) {
+      if (addend) {
+        float a2[8], b2[8];
+        unpack8(o, a2);
+        unpack8(pre_a[pt][ct][eh], b2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a2[e] += b2[e];
+        o = pack8(a2);
+      }
+      if (bnf) {
+        float f[8], yy[8];
+        unpack8(o, f);
+        unpack8(pre_y[pt][ct][eh], yy);
+        const uint32_t m = pre_m[pt][ct] >> (8 * eh);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = ct * 16 + eh * 8 + e;
+          const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
+          st_s[i] += dz;
+          st_q[i] += dz * (yy[e] - kk[i]) * bistd[i];
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(Y + pix_of(pix0p, pt) * 64 + 32 * ct + 16 * h + 8 * eh) = o;
+  };
+
+  constexpr bool DEFER = !DGRAD;
+  auto pix0_of = [&](int t) {
+    const int n = t / tiles_per_img, h0 = (t - n * tiles_per_img) * ROWS;
+    return ((size_t)n * g.H + h0) * W;
+  };
+  auto tile_body = [&](int t, int it, f32x16 (&Acc)[2][2], f32x16 (&Prev)[2][2], bool have_prev,
+                       size_t pix0p) {
+    const int buf = it & 1;
+    wait_vmcnt<STORES>();                        // this tile's halo (the previous stores may fly)
+    raw_barrier();
+    lds_char* const Sb = lds_base + buf * HB;
+    lds_char* const Wb = lds_base + 2 * HB;
+    const int tn = t + (int)gridDim.x;
+    const int nn_img = tn / tiles_per_img, nn_h0 = (tn - nn_img * tiles_per_img) * ROWS;
+    if (DEFER && have_prev) pre_load(pix0p);
+    if (!DEFER) pre_load(pix0_of(t));
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) Acc[pt][ct][e] = 0.f;
+    // step st = (tap st >> 1, K steps 2 (st & 1) + kk2): 8 MFMAs; the next step's 8 fragments
+    // are read in their shadow, one ds_read per MFMA (plane = immediate offset)
+    int ao[9][2];   // (HPLANE = false: laundered per tile so the per-step XORs stay in the loop)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        ao[tap][pt] = aoff[tap][pt];
+        if constexpr (!HPLANE) asm volatile("" : "+v"(ao[tap][pt]));
+      }
+    auto load_step = [&](int st, bf16x8 (&xa)[2][2], bf16x8 (&wb)[2][2]) {
+      const int tap = st >> 1;
+#pragma unroll
+      for (int kk2 = 0; kk2 < 2; ++kk2) {
+        const int k = (st & 1) * 2 + kk2;
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+          xa[kk2][pt] = *reinterpret_cast<const lds_bf16x8*>(
+              HPLANE ? Sb + k * HPB + ao[tap][pt] : Sb + (ao[tap][pt] ^ (k << 5)));
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+          wb[kk2][ct] = *reinterpret_cast<const lds_bf16x8*>(Wb + (tap * 4 + k) * 2048 + boff[ct]);
+      }
+    };
+    bf16x8 fx[2][2][2], fw[2][2][2];
+    load_step(0, fx[0], fw[0]);
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {
+      const int cur = st & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (st < SLOTS) issue_piece(nn_img, nn_h0, buf ^ 1, st);
+      if (st + 1 < 18) load_step(st + 1, fx[cur ^ 1], fw[cur ^ 1]);
+#pragma unroll
+      for (int kk2 = 0; kk2 < 2; ++kk2)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+            Acc[pt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[cur][kk2][ct], fx[cur][kk2][pt],
+                                                                 Acc[pt][ct], 0, 0, 0);
+      if (st + 1 < 18) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one ds_read
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (DEFER && st >= 10 && have_prev) epi_part(Prev, st - 10, pix0p);
+    }
+    if constexpr (!DEFER) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) epi_part(Acc, q, pix0_of(t));
+    }
+  };
+  f32x16 accA[2][2], accB[2][2];
+  wait_vmcnt<0>();                                // weights + first halo
+  {
+    int t = blockIdx.x, it = 0;
+    bool have_prev = false;
+    size_t pix0p = 0;
+    while (t < g.tiles) {
+      tile_body(t, it, accA, accB, have_prev, pix0p);
+      have_prev = true;
+      pix0p = pix0_of(t);
+      t += gridDim.x;
+      ++it;
+      if (t >= g.tiles) {
+        if constexpr (DEFER) {
+          pre_load(pix0p);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) epi_part(accA, q, pix0p);
+        }
+        break;
+      }
+      if constexpr (DEFER) {
+        tile_body(t, it, accB, accA, have_prev, pix0p);
+      } else {
+        tile_body(t, it, accA, accB, have_prev, pix0p);
+      }
+      pix0p = pix0_of(t);
+      t += gridDim.x;
+      ++it;
+      if (t >= g.tiles) {
+        if constexpr (DEFER) {
+          pre_load(pix0p);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) epi_part(accB, q, pix0p);
+        }
+        break;
+      }
+    }
+  }
+
+  // ---- per-block channel sums: lanes with the same h (and, forward, the same parity) share
+  // their sum slots' channels ----
+  if (STATS || bnf) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+#pragma unroll
+      for (int x = DGRAD ? 1 : 2; x < 32; x <<= 1) {
+        st_s[i] += __shfl_xor(st_s[i], x, 64);
+        st_q[i] += __shfl_xor(st_q[i], x, 64);
+      }
+    wait_vmcnt<0>();
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [4 waves][64 ch][2]
+    if (px < (DGRAD ? 1 : 2)) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        red[(wm * 64 + sum_ch(i)) * 2 + 0] = st_s[i];
+        red[(wm * 64 + sum_ch(i)) * 2 + 1] = st_q[i];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {   // fixed order: deterministic per block
+        a += red[(w * 64 + tid) * 2 + 0];
+        b += red[(w * 64 + tid) * 2 + 1];
+      }
+      float* dst = STATS ? stats : g.bn_part;
+      stat_out(dst, blockIdx.x, g.shards, 128, tid, a);
+      stat_out(dst, blockIdx.x, g.shards, 128, 64 + tid, b);
+    }
+    if constexpr (STATS) stat_krow(stats, g.shards, 128, g.kshift, 64);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 static int c64_grid(int tiles) {
   static int cus = 0;
   if (cus == 0) {
@@ -674,6 +1031,18 @@ static int c64_grid(int tiles) {
 static int64_t* g_c64_prof = nullptr;
 void c64_set_prof(int64_t* p) { g_c64_prof = p; }
 int c64_grid_size(int N, int H) { return c64_grid(N * H / 8); }
+
+// kernel version: PCA_C64_V (default 2; 3 / 4 are the 32x32x16 variants, measured slower:
+// README round 5), or set at run time (tests compare the versions)
+static int g_c64_ver = [] {
+  const char* e = getenv("PCA_C64_V");
+  return e ? atoi(e) : 2;
+}();
+int c64_version(int v) {
+  const int prev = g_c64_ver;
+  if (v >= 1 && v <= 4) g_c64_ver = v;
+  return prev;
+}
 
 bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                          int pad, int groups) {
@@ -703,10 +1072,7 @@ void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const 
   g.kshift = (!dgrad && stats) ? stat_shift() : nullptr;
   g.prof = nullptr;
   const dim3 grid(c64_grid(g.tiles)), block(256);
-  static const int ver = [] {
-    const char* e = getenv("PCA_C64_V");
-    return e ? atoi(e) : 2;
-  }();
+  const int ver = c64_version(-1);
   g.prof = g_c64_prof;
   if (g.prof) {
     if (dgrad)
@@ -727,6 +1093,30 @@ void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const 
     else
       hipLaunchKernelGGL((conv3x3_c64_v1_kernel<false, false>), grid, block, 0, st, a, w, y, nullptr,
                          addend, g);
+    return;
+  }
+  if (ver == 3) {
+    if (dgrad)
+      hipLaunchKernelGGL((conv3x3_c64w_kernel<true, false>), grid, block, 0, st, a, w, y, nullptr,
+                         addend, g);
+    else if (stats)
+      hipLaunchKernelGGL((conv3x3_c64w_kernel<false, true>), grid, block, 0, st, a, w, y, stats,
+                         addend, g);
+    else
+      hipLaunchKernelGGL((conv3x3_c64w_kernel<false, false>), grid, block, 0, st, a, w, y, nullptr,
+                         addend, g);
+    return;
+  }
+  if (ver == 4) {
+    if (dgrad)
+      hipLaunchKernelGGL((conv3x3_c64w_kernel<true, false, false>), grid, block, 0, st, a, w, y,
+                         nullptr, addend, g);
+    else if (stats)
+      hipLaunchKernelGGL((conv3x3_c64w_kernel<false, true, false>), grid, block, 0, st, a, w, y,
+                         stats, addend, g);
+    else
+      hipLaunchKernelGGL((conv3x3_c64w_kernel<false, false, false>), grid, block, 0, st, a, w, y,
+                         nullptr, addend, g);
     return;
   }
   if (dgrad)

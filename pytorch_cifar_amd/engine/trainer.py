@@ -62,6 +62,7 @@ class TrainStep:
         self.static_idx = torch.zeros(batch_size, dtype=torch.int64, device=self.device)
         self.last_loss = None
         self.graph_error = None
+        self.selection_hash = None   # kernel selection after the first (tuning) step
 
     def close(self):
         """Give the optimizer back its own gradient semantics (step() leaves .grad as computed)."""
@@ -86,7 +87,22 @@ class TrainStep:
         with trace_range("optimizer"):
             self.opt.step()
         self._grads_clean = bool(getattr(self.opt, "_zeroed_grads", False))
+        if self.selection_hash is None and self.device.type == "cuda" and not getattr(self.opt, "capturing", False):
+            self._sync_selection()
         return loss
+
+    def _sync_selection(self):
+        """After the first step (the one that autotuned every conv geometry): every rank adopts
+        rank 0's kernel selection (engine/tuning.py), and its hash is recorded."""
+        from .. import _native
+        from .tuning import selection_hash, selection_rows, sync_selection
+
+        lib = _native.lib()
+        ctx = getattr(self.ddp, "ctx", None)
+        if ctx is not None and ctx.world > 1:
+            self.selection_hash = sync_selection(ctx, lib)
+        else:
+            self.selection_hash = selection_hash(selection_rows(lib))
 
     def _fresh_operands(self):
         """A captured step with the fused optimizer has no prep pass: when the masters changed
@@ -287,8 +303,12 @@ def build_bench_step(model_name, per_rank_batch, device, ctx, graph=True, baseli
     meta = {"buckets_mib": ddp.bucket_sizes_mib() if ddp else None}
 
     def info():
+        from .tuning import table_rows_loaded
+
         return {"graph_captured": step.graph is not None,
-                "graph_error": repr(step.graph_error) if step.graph_error else None}
+                "graph_error": repr(step.graph_error) if step.graph_error else None,
+                "kernel_selection": step.selection_hash,
+                "tune_table_rows": table_rows_loaded()}
 
     run.info = info
     return run, meta

@@ -640,7 +640,11 @@ class _ConvMFMA(torch.autograd.Function):
         else:
             y, stats = C.conv_fwd(x, wb, bias, stride, padding, groups, want_stats, None, 0, pilot)
             if pilot is not None and stats is not None and stats.numel():
-                stats._pca_kin = pilot    # the slab's sums are of x - pilot (finalize adds it back)
+                # the slab's sums are of x - pilot (finalize adds it back). A snapshot, not the live
+                # pilot: a finalize writes the new batch mean into the pilot, and a second finalize
+                # of these sums (one conv output read by two BNs, or the conv called twice before
+                # its BN finalizes) must still add back the K its sums were taken against
+                stats._pca_kin = pilot.clone()
         ctx.geom = (stride, padding, groups, cin_pad, x.shape[1], x.shape[2])
         ctx.save_for_backward(x, wt if need_dx else None)
         ctx.weight = weight

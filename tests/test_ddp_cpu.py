@@ -225,3 +225,73 @@ def test_ddp_bf16_compressed_buckets():
         assert d < 1e-2, (n, d)
         ds.append(d)
     assert max(ds) > 0, "the bf16 path was not taken"
+
+
+def _train_one_step_tail(ctx):
+    r = _train_steps(ctx, compress="bf16_tail", steps=1)
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.parallel.ddp import DistributedDataParallel
+
+    # which parameters the tail bucket (the one whose all-reduce is launched last) holds
+    torch.manual_seed(0)
+    m = models.LeNet()
+    ddp = DistributedDataParallel(m, ctx, bucket_cap_mb=0.01, first_bucket_mb=0.01, grad_compress="bf16_tail")
+    names = {id(p): n for n, p in m.named_parameters()}
+    r["tail"] = sorted(names[id(p)] for p in ddp.buckets[-1].params)
+    r["n_buckets"] = len(ddp.buckets)
+    r["low"] = [b.low is not None for b in ddp.buckets]
+    return r
+
+
+def _train_one_step_exact(ctx):
+    return _train_steps(ctx, compress=None, steps=1)
+
+
+def test_ddp_bf16_tail_bucket_only():
+    """--grad_compress bf16_tail: only the last bucket (the last all-reduce of the backward, the
+    one exposed after it) travels in bf16. After one step, parameters of every other bucket are
+    bitwise equal to the exact fp32 run; the tail bucket's differ, by at most bf16 rounding."""
+    t0, t1 = run_ranks(_train_one_step_tail)
+    e0, _ = run_ranks(_train_one_step_exact)
+    assert t0["n_buckets"] > 1
+    assert t0["low"] == [False] * (t0["n_buckets"] - 1) + [True]
+    for n in t0["params"]:
+        assert torch.equal(t0["params"][n], t1["params"][n]), n
+    diff_tail = []
+    for n in t0["params"]:
+        if n in t0["tail"]:
+            d = (t0["params"][n] - e0["params"][n]).abs().max().item()
+            step = (e0["params"][n] - e0["init"][n]).abs().max().item()
+            assert d <= 2 ** -7 * step + 1e-7, (n, d, step)
+            diff_tail.append(d)
+        else:
+            assert torch.equal(t0["params"][n], e0["params"][n]), n
+    assert max(diff_tail) > 0, "the tail bucket was not rounded to bf16"
+
+
+def _tune_sync(ctx):
+    from pytorch_cifar_amd import _native
+    from pytorch_cifar_amd.engine.tuning import selection_rows, sync_selection
+
+    lib = _native.lib()
+    lib.conv_clear_tuned()
+    # each rank "tuned" differently: same geometries, rank-dependent tile / split choices, plus a
+    # geometry only rank 1 saw
+    rows = [[0] + [64, 32, 32, 64, 128, 3, 3, 1, 1, 1, 32, 32, 0] + [3 + ctx.rank, 1 + ctx.rank],
+            [1] + [64, 16, 16, 128, 128, 3, 3, 1, 1, 1, 16, 16, 0] + [35, 8 * (ctx.rank + 1)]]
+    if ctx.rank == 1:
+        rows.append([0] + [64, 8, 8, 256, 256, 3, 3, 1, 1, 1, 8, 8, 0] + [12, 1])
+    lib.tune_import(rows)
+    before = selection_rows(lib)
+    h = sync_selection(ctx, lib)
+    return {"before": before, "after": selection_rows(lib), "hash": h}
+
+
+def test_rank_consistent_kernel_selection():
+    """Ranks that autotuned to different kernel choices adopt rank 0's selection (engine/tuning.py
+    sync_selection): identical tables and selection hashes afterwards (reference main_dist.py:
+    140-147, replicated model under cudnn.benchmark)."""
+    r0, r1 = run_ranks(_tune_sync)
+    assert r0["before"] != r1["before"]
+    assert r0["after"] == r1["after"] == r0["before"]
+    assert r0["hash"] == r1["hash"]

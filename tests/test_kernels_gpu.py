@@ -176,6 +176,71 @@ def test_conv3x3_halo_kernel(C, case):
         C.set_conv_tile(0, -1)
 
 
+@pytest.mark.parametrize("ver", [2, 3, 4])
+@pytest.mark.parametrize("N", [4, 9])
+def test_conv3x3_c64_versions(C, ver, N):
+    """Layer-1 c64 kernel (conv3x3_c64.hip): v2 (16x16x32 MFMA) and v3 (32x32x16, plane LDS
+    layout, DPP-paired forward sums) — forward with slab and shifted-accumulator statistics, dgrad
+    with the residual addend + fused BatchNorm-backward reduce (slab and accumulator), vs fp32.
+    N = 9: 36 tiles, so some persistent workgroups run an odd number of tiles (deferred epilogue
+    of the last tile from either accumulator set)."""
+    H, Cc = 32, 64
+    torch.manual_seed(7)
+    x = bf(torch.randn(N, Cc, H, H, device="cuda")).requires_grad_(True)
+    w = bf(torch.randn(Cc, Cc, 3, 3, device="cuda") * (2.0 / (Cc * 9)) ** 0.5)
+    ref = F.conv2d(x, w, padding=1)
+    dy = bf(torch.randn_like(ref))
+    ref.backward(dy)
+    x_n = nhwc(x.detach()).to(torch.bfloat16)
+    wb, wt = C.weight_prep(w.permute(0, 2, 3, 1).contiguous(), 1, True)
+    dy_n = nhwc(dy).to(torch.bfloat16)
+    ybn = torch.randn(N, H, H, Cc, device="cuda").to(torch.bfloat16)
+    mask_b = torch.rand(N, H, H, Cc, device="cuda") > 0.4
+    bits = (mask_b.view(-1, 8).to(torch.int32) << torch.arange(8, device="cuda")).sum(1).to(torch.uint8)
+    mean, istd = torch.randn(Cc, device="cuda") * 0.1, torch.rand(Cc, device="cuda") + 0.5
+    aux = torch.cat([mean, istd])
+    add = torch.randn(N, H, H, Cc, device="cuda").to(torch.bfloat16)
+    r = ref.detach()
+    prev = C.c64_version(ver)
+    try:
+        y, stats = C.conv_fwd(x_n, wb, None, 1, 1, 1, True)
+        assert rel_err(nchw(y), r) < 2e-2
+        assert rel_err(stats[:, 0, :].sum(0), r.sum((0, 2, 3))) < 1e-2
+        assert rel_err(stats[:, 1, :].sum(0), (r ** 2).sum((0, 2, 3))) < 1e-2
+        # shifted sums into a 4-row accumulator (+ its K row)
+        K = torch.randn(Cc, device="cuda")
+        R = 4
+        acc = torch.zeros(R * 2 * Cc + Cc, device="cuda")
+        y2, _ = C.conv_fwd(x_n, wb, None, 1, 1, 1, True, acc, R, K)
+        assert torch.equal(y2, y)
+        a = acc[:R * 2 * Cc].view(R, 2, Cc).sum(0)
+        yf = y.float().reshape(-1, Cc)
+        d = r.permute(0, 2, 3, 1).reshape(-1, Cc) - K
+        assert rel_err(a[0], d.sum(0)) < 1e-2
+        assert rel_err(a[1], (d ** 2).sum(0)) < 1e-2
+        assert torch.equal(acc[R * 2 * Cc:], K)
+        dx = C.conv_dgrad(dy_n, wt, H, H, 1, 1, 1)
+        assert rel_err(nchw(dx), x.grad) < 2e-2
+        full = nhwc(x.grad) + add.float()
+        dz_ref = None
+        for use_acc in (False, True):
+            if use_acc:
+                bacc = torch.zeros(R * 2 * Cc, device="cuda")
+                dx2, part = C.conv_dgrad_bn(dy_n, wt, H, H, 1, 1, 1, add, ybn, bits, aux, bacc, R)
+                part = bacc.view(R, 2, Cc)
+            else:
+                dx2, part = C.conv_dgrad_bn(dy_n, wt, H, H, 1, 1, 1, add, ybn, bits, aux)
+            assert rel_err(dx2, full) < 2e-2
+            dz = torch.where(mask_b, dx2.float(), torch.zeros_like(full))
+            s1 = dz.sum((0, 1, 2))
+            s2 = (dz * (ybn.float() - mean) * istd).sum((0, 1, 2))
+            assert part.numel() > 0
+            assert rel_err(part[:, 0, :].sum(0), s1) < 1e-2 and rel_err(part[:, 1, :].sum(0), s2) < 1e-2
+        del yf, dz_ref
+    finally:
+        C.c64_version(prev)
+
+
 @pytest.mark.parametrize("case", [(4, 64, 32, 128), (8, 128, 16, 256), (16, 256, 8, 512),
                                   (8, 32, 16, 64), (4, 96, 32, 64)])
 def test_conv3x3_s2_dgrad_halo_kernel(C, case):

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Measure and write the shipped kernel-selection table (pytorch_cifar_amd/tune/mi355x.json).
+
+Runs each BASELINE configuration's bench step once with the table disabled and a fresh tune cache
+(every conv geometry autotuned on this box), then writes the union of the selections, stamped with
+the extension's candidate-set version (engine/tuning.py ignores a table of another version).
+
+  python tools/tune_table.py [--out pytorch_cifar_amd/tune/mi355x.json]     # on a GPU box
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONFIGS = [("ResNet18", 1024), ("ResNet18", 512), ("ResNet18", 256), ("ResNet18", 128),
+           ("MobileNetV2", 1024), ("EfficientNetB0", 1024), ("EfficientNetB0", 128)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "pytorch_cifar_amd", "tune", "mi355x.json"))
+    args = ap.parse_args()
+    rows, runs = {}, []
+    for model, batch in CONFIGS:
+        with tempfile.TemporaryDirectory() as d:
+            cache = os.path.join(d, "tune.json")
+            env = dict(os.environ, PCA_TUNE_TABLE="0", PCA_TUNE_CACHE=cache)
+            cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", model, "--batch", str(batch),
+                   "--steps", "3", "--warmup", "2"]
+            p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+            if p.returncode != 0:
+                sys.exit(f"{model} bs{batch} failed:\n{p.stderr[-2000:]}")
+            with open(cache) as fh:
+                got = json.load(fh)
+            for r in got:
+                rows[tuple(r[:14])] = r
+            runs.append({"model": model, "batch": batch, "rows": len(got)})
+            print(model, batch, len(got), flush=True)
+    from pytorch_cifar_amd import _native
+    from pytorch_cifar_amd.engine.tuning import selection_hash
+
+    lib = _native.lib()
+    out = {"version": lib.tune_version(), "arch": "gfx950", "configs": runs,
+           "rows": sorted(rows.values()), "hash": selection_hash(rows.values())}
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as fh:
+        json.dump(out, fh, indent=0)
+    print("wrote", args.out, len(rows), "rows, hash", out["hash"])
+
+
+if __name__ == "__main__":
+    main()
