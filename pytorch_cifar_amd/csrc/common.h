@@ -41,11 +41,14 @@ __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
   }
 }
 
+// one v_cvt_pk_bf16_f32 (round to nearest even, NaN kept) per pair: converting the two floats
+// separately and or-ing the halves let the SLP vectorizer pair elements across calls and emit
+// and / shift / or_sdwa fix-ups (6 VALU per 4 values in the conv epilogues instead of 2)
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  bf16 ha = f2bf(a), hb = f2bf(b);
-  uint16_t ua = __builtin_bit_cast(uint16_t, ha);
-  uint16_t ub = __builtin_bit_cast(uint16_t, hb);
-  return (uint32_t)ua | ((uint32_t)ub << 16);
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t h = __builtin_convertvector((f32x2_t){a, b}, bf16x2_t);
+  return __builtin_bit_cast(uint32_t, h);
 }
 
 __device__ __forceinline__ uint4 pack8(const float* f) {

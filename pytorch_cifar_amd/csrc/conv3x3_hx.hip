@@ -365,19 +365,17 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
           s2[e] += d * d;
         }
       }
-      uint4 o0 = pack8(v), o1 = pack8(v + 8);
       if constexpr (DGRAD) {
-        if (addend) {
-          float a2[16], b2[16];
-          unpack8(o0, a2);
-          unpack8(o1, a2 + 8);
+        if (addend) {   // dX = conv^T(dY) + addend in fp32, rounded to bf16 once
+          float b2[16];
           unpack8(pre_a[mi][0], b2);
           unpack8(pre_a[mi][1], b2 + 8);
 #pragma unroll
-          for (int e = 0; e < 16; ++e) a2[e] += b2[e];
-          o0 = pack8(a2);
-          o1 = pack8(a2 + 8);
+          for (int e = 0; e < 16; ++e) v[e] += b2[e];
         }
+      }
+      uint4 o0 = pack8(v), o1 = pack8(v + 8);
+      if constexpr (DGRAD) {
         if (bnf) {
           float f[16], yy[16];
           unpack8(o0, f);
