@@ -24,6 +24,21 @@ static const float* g_stat_shift = nullptr;
 const float* stat_shift() { return g_stat_shift; }
 void set_stat_shift(const float* k) { g_stat_shift = k; }
 
+// Row strides (elements between consecutive NHWC pixels) of the tensors the next BN launch
+// touches, 0 = dense (the channel count): a channel slice of a wider concat slab is a row-strided
+// [M][C] matrix, so concatenation can be zero-copy (producers write their slice, consumers read a
+// channel range; models/densenet.py, googlenet.py, dla*.py). Set by the host bindings around a
+// launch (like stat_shards); only the row-tiled kernels (C % 8 == 0) take strides.
+//   y: BN input, out: forward output, dout: backward input gradient, dx: backward output
+//   (dx_acc: the backward adds into dx instead of overwriting it)
+static BnLd g_bn_ld{};
+BnLd bn_ld() { return g_bn_ld; }
+void set_bn_ld(const BnLd& ld) { g_bn_ld = ld; }
+static bool bn_ld_dense() {
+  return g_bn_ld.y == 0 && g_bn_ld.out == 0 && g_bn_ld.dout == 0 && g_bn_ld.dx == 0 && !g_bn_ld.dx_acc;
+}
+__host__ __device__ __forceinline__ int ld_or(int ld, int C) { return ld ? ld : C; }
+
 // Row-parallel geometry for an [M][C] NHWC matrix: TPR threads cover a row's granules
 // (VEC channels each), RPP rows are processed per pass by one 256-thread block.
 struct RowPar {
@@ -81,7 +96,7 @@ template <int VEC>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ x, int M,
                                                        RowPar rp, int rows_per_block,
                                                        float* __restrict__ partial, int shards,
-                                                       float* __restrict__ krow) {
+                                                       float* __restrict__ krow, int ldx) {
   __shared__ float red[256 * VEC * 2];
   const int t = threadIdx.x;
   const int gx = t % rp.TPR, ry = t / rp.TPR;
@@ -98,7 +113,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ 
     if (ry < rp.RPP && gi < rp.G) {
       for (int r = r0 + ry; r < r1; r += rp.RPP) {
         float f[VEC];
-        load_vec<VEC>(x + (size_t)r * rp.C + gi * VEC, f);
+        load_vec<VEC>(x + (size_t)r * ldx + gi * VEC, f);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
           const float d = f[v] - k[v];
@@ -282,11 +297,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 }
 
 // dz from the incoming gradient: relu uses the saved output as mask; swish/sigmoid recompute z.
+// (e: element offset in the dense [M][C] indexing of out / mask; ed, ey: of dout, y)
 template <int VEC>
 __device__ __forceinline__ void compute_dz(const bf16* dout, const bf16* out, const uint8_t* mask,
                                            const bf16* y, const float* aux, int C, int c0, size_t e,
-                                           int act, float* dz) {
-  load_vec<VEC>(dout + e, dz);
+                                           int act, float* dz, size_t ed, size_t ey) {
+  load_vec<VEC>(dout + ed, dz);
   if (act == ACT_RELU && VEC == 8 && mask) {
     const uint32_t b = mask[e >> 3];
 #pragma unroll
@@ -298,7 +314,7 @@ __device__ __forceinline__ void compute_dz(const bf16* dout, const bf16* out, co
     for (int v = 0; v < VEC; ++v) dz[v] = o[v] > 0.f ? dz[v] : 0.f;
   } else if (act != ACT_NONE) {
     float yy[VEC];
-    load_vec<VEC>(y + e, yy);
+    load_vec<VEC>(y + ey, yy);
 #pragma unroll
     for (int v = 0; v < VEC; ++v) {
       const float z = yy[v] * aux[2 * C + c0 + v] + aux[3 * C + c0 + v];
@@ -321,7 +337,8 @@ __device__ __forceinline__ void bwd_reduce_rows(const bf16* __restrict__ dout,
                                                 const bf16* __restrict__ y,
                                                 const uint8_t* __restrict__ mask,
                                                 const float* __restrict__ aux, int C, int c0, int r,
-                                                int r1, int rpp, float (&acc)[2][8]) {
+                                                int r1, int rpp, float (&acc)[2][8], int ldd,
+                                                int ldy) {
   uint4 dr[kBwdRows], yr[kBwdRows];
   uint32_t mr[kBwdRows];
   float wgt[kBwdRows];
@@ -329,9 +346,10 @@ __device__ __forceinline__ void bwd_reduce_rows(const bf16* __restrict__ dout,
   for (int k = 0; k < kBwdRows; ++k) {
     const int rk = r + k * rpp;
     wgt[k] = rk < r1 ? 1.f : 0.f;
-    const size_t e = (size_t)min(rk, r1 - 1) * C + c0;
-    dr[k] = *reinterpret_cast<const uint4*>(dout + e);
-    yr[k] = *reinterpret_cast<const uint4*>(y + e);
+    const size_t rr = (size_t)min(rk, r1 - 1);
+    const size_t e = rr * C + c0;
+    dr[k] = *reinterpret_cast<const uint4*>(dout + rr * ldd + c0);
+    yr[k] = *reinterpret_cast<const uint4*>(y + rr * ldy + c0);
     mr[k] = MASK ? mask[e >> 3] : 0xffu;
   }
   // aux = [mean | istd | scale | shift] x C (scale / shift: the BN affine as used by the act)
@@ -370,7 +388,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16* __restrict__ dout, const bf16* __restrict__ out, const uint8_t* __restrict__ mask,
     const bf16* __restrict__ y, const float* __restrict__ aux, const bf16* __restrict__ y2,
     const float* __restrict__ aux2, int act, int M, RowPar rp, int rows_per_block,
-    float* __restrict__ partial, int shards) {
+    float* __restrict__ partial, int shards, int ldd, int ldy) {
   __shared__ float red[256 * VEC * NS];
   const int t = threadIdx.x;
   const int gx = t % rp.TPR, ry = t / rp.TPR;
@@ -401,22 +419,23 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         // masked-ReLU / no-act / swish fast path (bwd_reduce_rows)
         if (mask)
           for (; r < r1; r += kBwdRows * rp.RPP)
-            bwd_reduce_rows<true, 0>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+            bwd_reduce_rows<true, 0>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc, ldd, ldy);
         else if (act == ACT_SWISH)
           for (; r < r1; r += kBwdRows * rp.RPP)
-            bwd_reduce_rows<false, ACT_SWISH>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+            bwd_reduce_rows<false, ACT_SWISH>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc, ldd, ldy);
         else if (act == ACT_RELU_Y)
           for (; r < r1; r += kBwdRows * rp.RPP)
-            bwd_reduce_rows<false, ACT_RELU_Y>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+            bwd_reduce_rows<false, ACT_RELU_Y>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc, ldd, ldy);
         else if (act == ACT_NONE)
           for (; r < r1; r += kBwdRows * rp.RPP)
-            bwd_reduce_rows<false, 0>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc);
+            bwd_reduce_rows<false, 0>(dout, y, mask, aux, C, c0, r, r1, rp.RPP, acc, ldd, ldy);
       }
       for (; r < r1; r += rp.RPP) {
         const size_t e = (size_t)r * C + c0;
         float dz[VEC], yy[VEC];
-        compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz);
-        load_vec<VEC>(y + e, yy);
+        compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz, (size_t)r * ldd + c0,
+                        (size_t)r * ldy + c0);
+        load_vec<VEC>(y + (size_t)r * ldy + c0, yy);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
           acc[0][v] += dz[v];
@@ -529,7 +548,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const size_t e = i * VEC;
     const int c0 = (int)(e % C);
     float dz[VEC], yy[VEC], o[VEC];
-    compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz);
+    compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz, e, e);
     load_vec<VEC>(y + e, yy);
 #pragma unroll
     for (int v = 0; v < VEC; ++v) o[v] = coef[c0 + v] * dz[v] + coef[C + c0 + v] * yy[v] + coef[2 * C + c0 + v];
@@ -561,7 +580,8 @@ template <bool RES, bool DUAL, int ACT>
 __device__ __forceinline__ void bn_apply_rows_body(
     const bf16* __restrict__ y, const float* scale, const float* shift, int C, int M,
     const bf16* __restrict__ res, const bf16* __restrict__ y2, const float* scale2,
-    const float* shift2, bf16* __restrict__ out, uint8_t* __restrict__ mask) {
+    const float* shift2, bf16* __restrict__ out, uint8_t* __restrict__ mask, BnLd ld) {
+  const int ldy = ld_or(ld.y, C), ldo = ld_or(ld.out, C);
   constexpr int U = kRowsInFlight;
   const int TPR = C >> 3, RPB = 256 / TPR;
   const int g = threadIdx.x % TPR, ro = threadIdx.x / TPR;
@@ -581,11 +601,13 @@ __device__ __forceinline__ void bn_apply_rows_body(
   for (int r0 = blockIdx.x * RPB + ro; r0 < M; r0 += U * rstep) {
     uint4 vy[U], vt[U];
     size_t e[U];
+    int rr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = min(r0 + u * rstep, M - 1);
+      rr[u] = r;
       e[u] = (size_t)r * C + c0;
-      vy[u] = *reinterpret_cast<const uint4*>(y + e[u]);
+      vy[u] = *reinterpret_cast<const uint4*>(y + (size_t)r * ldy + c0);
       if constexpr (RES) vt[u] = *reinterpret_cast<const uint4*>(res + e[u]);
       if constexpr (DUAL) vt[u] = *reinterpret_cast<const uint4*>(y2 + e[u]);
     }
@@ -605,7 +627,7 @@ __device__ __forceinline__ void bn_apply_rows_body(
         f[v] = a;
       }
       if (r0 + u * rstep < M) {
-        *reinterpret_cast<uint4*>(out + e[u]) = pack8(f);
+        *reinterpret_cast<uint4*>(out + (size_t)rr[u] * ldo + c0) = pack8(f);
         if (mask) mask[e[u] >> 3] = (uint8_t)b;
       }
     }
@@ -616,10 +638,10 @@ template <bool RES, bool DUAL, int ACT>
 __global__ __launch_bounds__(256) void bn_apply_rows_kernel(
     const bf16* __restrict__ y, const float* __restrict__ aux, int C, int M,
     const bf16* __restrict__ res, const bf16* __restrict__ y2, const float* __restrict__ aux2,
-    bf16* __restrict__ out, uint8_t* __restrict__ mask) {
+    bf16* __restrict__ out, uint8_t* __restrict__ mask, BnLd ld) {
   bn_apply_rows_body<RES, DUAL, ACT>(y, aux + 2 * C, aux + 3 * C, C, M, res, y2,
                                      DUAL ? aux2 + 2 * C : nullptr, DUAL ? aux2 + 3 * C : nullptr,
-                                     out, mask);
+                                     out, mask, ld);
 }
 
 // KIND: 0 = no activation, 1 = ReLU through the 1-bit mask, 2 = swish (z recomputed from y),
@@ -629,8 +651,9 @@ template <bool RES, bool DUAL, int KIND>
 __device__ __forceinline__ void bn_bwd_apply_rows_body(
     const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
     const float* coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
-    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux) {
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux, BnLd ld) {
   constexpr bool MASK = KIND == 1;
+  const int ldd = ld_or(ld.dout, C), ldy = ld_or(ld.y, C), ldx = ld_or(ld.dx, C);
   constexpr int U = kRowsInFlight;
   const int TPR = C >> 3, RPB = 256 / TPR;
   const int g = threadIdx.x % TPR, ro = threadIdx.x / TPR;
@@ -654,15 +677,18 @@ __device__ __forceinline__ void bn_bwd_apply_rows_body(
   }
   const int rstep = gridDim.x * RPB;
   for (int r0 = blockIdx.x * RPB + ro; r0 < M; r0 += U * rstep) {
-    uint4 vd[U], vy[U], v2[U];
+    uint4 vd[U], vy[U], v2[U], vx[U];
     uint32_t vm[U];
     size_t e[U];
+    int rr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = min(r0 + u * rstep, M - 1);
+      rr[u] = r;
       e[u] = (size_t)r * C + c0;
-      vd[u] = *reinterpret_cast<const uint4*>(dout + e[u]);
-      vy[u] = *reinterpret_cast<const uint4*>(y + e[u]);
+      vd[u] = *reinterpret_cast<const uint4*>(dout + (size_t)r * ldd + c0);
+      vy[u] = *reinterpret_cast<const uint4*>(y + (size_t)r * ldy + c0);
+      if (ld.dx_acc) vx[u] = *reinterpret_cast<const uint4*>(dy + (size_t)r * ldx + c0);
       if constexpr (MASK) vm[u] = mask[e[u] >> 3];
       if constexpr (DUAL) v2[u] = *reinterpret_cast<const uint4*>(y2 + e[u]);
     }
@@ -682,8 +708,14 @@ __device__ __forceinline__ void bn_bwd_apply_rows_body(
       }
 #pragma unroll
       for (int v = 0; v < 8; ++v) o[v] = ca[v] * dz[v] + cb[v] * yy[v] + cd[v];
+      if (ld.dx_acc) {   // (concat slab: the other readers' gradients are already there)
+        float xa[8];
+        unpack8(vx[u], xa);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) o[v] += xa[v];
+      }
       const bool live = r0 + u * rstep < M;
-      if (live) *reinterpret_cast<uint4*>(dy + e[u]) = pack8(o);
+      if (live) *reinterpret_cast<uint4*>(dy + (size_t)rr[u] * ldx + c0) = pack8(o);
       if constexpr (RES) {
         if (live) *reinterpret_cast<uint4*>(dres + e[u]) = pack8(dz);
       }
@@ -701,8 +733,8 @@ template <bool RES, bool DUAL, int KIND>
 __global__ __launch_bounds__(256) void bn_bwd_apply_rows_kernel(
     const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
     const float* __restrict__ coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
-    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux) {
-  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, coef, C, M, dy, dres, y2, dy2, aux);
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux, BnLd ld) {
+  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, coef, C, M, dy, dres, y2, dy2, aux, ld);
 }
 
 // ---- fused finalize + apply (sharded accumulators, no finalize launch) ----
@@ -831,28 +863,28 @@ __device__ __forceinline__ void bn_fin_zero(const BnFin& f) {
 template <bool RES, bool DUAL, int ACT>
 __global__ __launch_bounds__(256) void bn_apply_acc_rows_kernel(
     const bf16* __restrict__ y, BnFin f, BnFin f2, int C, int M, const bf16* __restrict__ res,
-    const bf16* __restrict__ y2, bf16* __restrict__ out, uint8_t* __restrict__ mask) {
+    const bf16* __restrict__ y2, bf16* __restrict__ out, uint8_t* __restrict__ mask, BnLd ld) {
   extern __shared__ float lds[];   // [sc | sh | sc2 | sh2][C]
   bn_fin_forward(f, C, lds, lds + C);
   if constexpr (DUAL) bn_fin_forward(f2, C, lds + 2 * C, lds + 3 * C);
   bn_fin_zero(f);
   __syncthreads();
   bn_apply_rows_body<RES, DUAL, ACT>(y, lds, lds + C, C, M, res, y2, lds + 2 * C, lds + 3 * C,
-                                     out, mask);
+                                     out, mask, ld);
 }
 
 template <bool RES, bool DUAL, int KIND>
 __global__ __launch_bounds__(256) void bn_bwd_apply_acc_rows_kernel(
     const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
     BnFin f, BnFin f2, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
-    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux) {
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux, BnLd ld) {
   extern __shared__ float lds[];   // coef [3|6][C]
   constexpr int NS = DUAL ? 3 : 2;
   bn_fin_backward<NS>(f, f2, C, lds);
   bn_fin_zero(f);
   bn_fin_zero(f2);
   __syncthreads();
-  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, lds, C, M, dy, dres, y2, dy2, aux);
+  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, lds, C, M, dy, dres, y2, dy2, aux, ld);
 }
 
 static bool rows_enabled() {
@@ -901,7 +933,7 @@ void bn_stats_launch(const bf16* x, int M, int C, float* partial, int P, hipStre
 #define PCA_STATS(V)                                                                              \
   case V: {                                                                                       \
     RowPar rp = make_rowpar(C, V);                                                                \
-    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial, g_stat_shards, krow); \
+    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial, g_stat_shards, krow, ld_or(g_bn_ld.y, C)); \
     break;                                                                                        \
   }
     PCA_STATS(8) PCA_STATS(4) PCA_STATS(2) PCA_STATS(1)
@@ -937,7 +969,7 @@ void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const
     const int M = (int)(total / C);
     const dim3 gr(rows_grid(M, C)), bl(256);
 #define PCA_APPLY(R, D, A) \
-    hipLaunchKernelGGL((bn_apply_rows_kernel<R, D, A>), gr, bl, 0, st, y, aux, C, M, res, y2, aux2, out, mask)
+    hipLaunchKernelGGL((bn_apply_rows_kernel<R, D, A>), gr, bl, 0, st, y, aux, C, M, res, y2, aux2, out, mask, g_bn_ld)
     if (act == ACT_SWISH) {
       PCA_APPLY(false, false, ACT_SWISH);
     } else if (act == ACT_RELU) {
@@ -951,6 +983,10 @@ void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const
     }
 #undef PCA_APPLY
     return;
+  }
+  if (!bn_ld_dense()) {
+    fprintf(stderr, "pca: strided BatchNorm apply needs the row-tiled kernel (C %% 8 == 0)\n");
+    abort();
   }
   switch (bn_vec(C)) {
     case 8:
@@ -978,10 +1014,12 @@ void bn_bwd_reduce_launch(const bf16* dout, const bf16* out, const uint8_t* mask
     RowPar rp = make_rowpar(C, V);                                                                 \
     if (y2)                                                                                        \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<V, 3>), dim3(P), dim3(256), 0, st, dout, out, mask, \
-                         y, aux, y2, aux2, act, M, rp, rows, partial, g_stat_shards);              \
+                         y, aux, y2, aux2, act, M, rp, rows, partial, g_stat_shards,               \
+                         ld_or(g_bn_ld.dout, C), ld_or(g_bn_ld.y, C));                             \
     else                                                                                           \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<V, 2>), dim3(P), dim3(256), 0, st, dout, out, mask, \
-                         y, aux, y2, aux2, act, M, rp, rows, partial, g_stat_shards);              \
+                         y, aux, y2, aux2, act, M, rp, rows, partial, g_stat_shards,               \
+                         ld_or(g_bn_ld.dout, C), ld_or(g_bn_ld.y, C));                             \
     break;                                                                                         \
   }
     PCA_RED(8) PCA_RED(4) PCA_RED(2) PCA_RED(1)
@@ -1015,7 +1053,7 @@ void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask,
     const int M = (int)(total / C);
     const dim3 gr(rows_grid(M, C)), bl(256);
 #define PCA_BWD(R, D, K) \
-    hipLaunchKernelGGL((bn_bwd_apply_rows_kernel<R, D, K>), gr, bl, 0, st, dout, mask, y, coef, C, M, dy, dres, y2, dy2, aux)
+    hipLaunchKernelGGL((bn_bwd_apply_rows_kernel<R, D, K>), gr, bl, 0, st, dout, mask, y, coef, C, M, dy, dres, y2, dy2, aux, g_bn_ld)
     if (masked) {
       if (dres && y2) PCA_BWD(true, true, 1);
       else if (dres) PCA_BWD(true, false, 1);
@@ -1033,6 +1071,10 @@ void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask,
     }
 #undef PCA_BWD
     return;
+  }
+  if (!bn_ld_dense()) {
+    fprintf(stderr, "pca: strided BatchNorm backward needs the row-tiled kernel (C %% 8 == 0)\n");
+    abort();
   }
   switch (bn_vec(C)) {
     case 8:
@@ -1073,7 +1115,7 @@ bool bn_apply_acc_launch(const bf16* y, int C, int M, float count, float* acc, i
   const dim3 gr(acc_rows_grid(M, C)), bl(256);
   const size_t lds = (size_t)(y2 ? 4 : 2) * C * sizeof(float);
 #define PCA_APPLY(R_, D, A) \
-  hipLaunchKernelGGL((bn_apply_acc_rows_kernel<R_, D, A>), gr, bl, lds, st, y, f, f2, C, M, res, y2, out, mask)
+  hipLaunchKernelGGL((bn_apply_acc_rows_kernel<R_, D, A>), gr, bl, lds, st, y, f, f2, C, M, res, y2, out, mask, g_bn_ld)
   if (act == ACT_SWISH) {
     PCA_APPLY(false, false, ACT_SWISH);
   } else if (act == ACT_RELU) {
@@ -1106,7 +1148,7 @@ bool bn_bwd_apply_acc_launch(const bf16* dout, const uint8_t* mask, const bf16* 
   const dim3 gr(acc_rows_grid(M, C)), bl(256);
   const size_t lds = (size_t)(y2 ? 6 : 3) * C * sizeof(float);
 #define PCA_BWD(R_, D, K) \
-  hipLaunchKernelGGL((bn_bwd_apply_acc_rows_kernel<R_, D, K>), gr, bl, lds, st, dout, mask, y, f, f2, C, M, dy, dres, y2, dy2, aux)
+  hipLaunchKernelGGL((bn_bwd_apply_acc_rows_kernel<R_, D, K>), gr, bl, lds, st, dout, mask, y, f, f2, C, M, dy, dres, y2, dy2, aux, g_bn_ld)
   if (masked) {
     if (dres && y2) PCA_BWD(true, true, 1);
     else if (dres) PCA_BWD(true, false, 1);

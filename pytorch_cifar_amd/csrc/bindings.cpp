@@ -47,6 +47,12 @@ void wgrad_clear_tuned();
 std::vector<std::vector<int>> tune_export();
 void c64_set_prof(int64_t* p);
 int c64_grid_size(int N, int H);
+// batchnorm.hip: row strides of the next BN launches' tensors (0 = dense; common.h BnLd)
+struct BnLd {
+  int y, out, dout, dx, dx_acc;
+};
+BnLd bn_ld();
+void set_bn_ld(const BnLd& ld);
 int c64_version(int v);
 int tune_import(const std::vector<std::vector<int>>& rows);
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
@@ -232,6 +238,31 @@ void check_bf16(const Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous (NHWC)");
 }
+// NHWC bf16 [N,H,W,C] whose pixels may be strided rows (a channel slice of a wider concat slab:
+// stride(3) = 1, stride(2) = ld >= C, outer strides dense over ld): returns ld (C when dense)
+int rows_ld(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  const int C = t.size(-1);
+  if (t.is_contiguous()) return C;
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.stride(2) >= C && C % 8 == 0 &&
+                  t.stride(1) == t.size(2) * t.stride(2) && t.stride(0) == t.size(1) * t.stride(1),
+              name, " must be contiguous NHWC or a row-strided channel slice with C % 8 == 0");
+  return (int)t.stride(2);
+}
+
+// RAII: the row strides (0 = dense) the BatchNorm launches in scope read / write with
+struct BnLdScope {
+  pca::BnLd prev;
+  explicit BnLdScope(int C, int y, int out, int dout = 0, int dx = 0, bool dx_acc = false)
+      : prev(pca::bn_ld()) {
+    pca::BnLd ld{y == C ? 0 : y, out == C ? 0 : out, dout == C ? 0 : dout, dx == C ? 0 : dx,
+                 dx_acc ? 1 : 0};
+    pca::set_bn_ld(ld);
+  }
+  ~BnLdScope() { pca::set_bn_ld(prev); }
+};
+
 void check_f32(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be fp32");
@@ -609,11 +640,12 @@ void weight_prep_multi(const Tensor& desc, const Tensor& chunks) {
 
 // ------------------------------------------------------------------------------- BN
 Tensor bn_stats(const Tensor& x) {
-  check_bf16(x, "x");
+  const int ldx = rows_ld(x, "x");
   const int C = x.size(-1);
   const int M = x.numel() / C;
   const int P = pca::bn_row_blocks(M, C);
   auto partial = at::empty({P, 2, C}, x.options().dtype(at::kFloat));
+  BnLdScope lds(C, ldx, C);
   pca::bn_stats_launch(ptr<bf16>(x), M, C, ptr<float>(partial), P, cur_stream());
   return partial;
 }
@@ -621,8 +653,9 @@ Tensor bn_stats(const Tensor& x) {
 // centered form (robust variance): sums of x - K with K = x's first row, K returned alongside
 // -> {partial [P][2][C], K [C]} (the finalize's kin)
 std::vector<Tensor> bn_stats_centered(const Tensor& x) {
-  check_bf16(x, "x");
+  const int ldx = rows_ld(x, "x");
   const int C = x.size(-1);
+  BnLdScope lds(C, ldx, C);
   const int M = x.numel() / C;
   const int P = pca::bn_row_blocks(M, C);
   auto buf = at::empty({(int64_t)P * 2 * C + C}, x.options().dtype(at::kFloat));
@@ -653,8 +686,9 @@ static int64_t acc_max_elems() {
 // per-channel (sum, sumsq) of a bare tensor added into a zeroed sharded accumulator [R][2][C];
 // returns false (nothing launched) when the tensor is too large for the accumulator form
 bool bn_stats_acc(const Tensor& x, const Tensor& acc, int R) {
-  check_bf16(x, "x");
+  const int ldx = rows_ld(x, "x");
   const int C = x.size(-1);
+  BnLdScope lds(C, ldx, C);
   const int M = x.numel() / C;
   check_acc(acc, R, 2, C);
   if ((int64_t)M * C > acc_max_elems()) return false;
@@ -724,10 +758,11 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
   return aux;
 }
 
+// out: optional destination (a row-strided channel slice of a concat slab), else a new tensor
 std::vector<Tensor> bn_apply(const Tensor& y, const Tensor& aux, const optional<Tensor>& res,
                              const optional<Tensor>& y2, const optional<Tensor>& aux2, int act,
-                             bool want_mask) {
-  check_bf16(y, "y");
+                             bool want_mask, const optional<Tensor>& out_opt) {
+  const int ldy = rows_ld(y, "y");
   const int C = y.size(-1);
   TORCH_CHECK(aux.size(1) == C, "aux channel mismatch");
   if (res.has_value() && res->defined()) {
@@ -738,11 +773,20 @@ std::vector<Tensor> bn_apply(const Tensor& y, const Tensor& aux, const optional<
     check_bf16(*y2, "y2");
     TORCH_CHECK(y2->sizes() == y.sizes(), "second BN input shape mismatch");
   }
-  auto out = at::empty_like(y);
+  Tensor out;
+  int ldo = C;
+  if (out_opt.has_value() && out_opt->defined()) {
+    out = *out_opt;
+    ldo = rows_ld(out, "out");
+    TORCH_CHECK(out.sizes() == y.sizes(), "out shape mismatch");
+  } else {
+    out = at::empty(y.sizes(), y.options());
+  }
   // ReLU sign bits (1 byte / 8 channels) for the backward, when C allows the 8-wide path
   Tensor mask;
   if (want_mask && act == 1 && C % 8 == 0)
     mask = at::empty({(int64_t)(y.numel() / 8)}, y.options().dtype(at::kByte));
+  BnLdScope lds(C, ldy, ldo);
   pca::bn_apply_launch(ptr<bf16>(y), ptr<float>(aux), C, y.numel(), optr<bf16>(res), optr<bf16>(y2),
                        optr<float>(aux2), act, ptr<bf16>(out),
                        mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
@@ -764,8 +808,8 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
                                  const optional<Tensor>& nbt2, double momentum2, double eps2,
                                  int act, bool want_mask, const optional<Tensor>& zero,
                                  bool shifted, const optional<Tensor>& pilot, bool shifted2,
-                                 const optional<Tensor>& pilot2) {
-  check_bf16(y, "y");
+                                 const optional<Tensor>& pilot2, const optional<Tensor>& out_opt) {
+  const int ldy = rows_ld(y, "y");
   const int C = y.size(-1);
   const int M = y.numel() / C;
   check_acc(acc, R, 2, C);
@@ -791,11 +835,20 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
     TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
   }
   auto fopt = y.options().dtype(at::kFloat);
-  auto out = at::empty_like(y);
+  Tensor out;
+  int ldo = C;
+  if (out_opt.has_value() && out_opt->defined()) {
+    out = *out_opt;
+    ldo = rows_ld(out, "out");
+    TORCH_CHECK(out.sizes() == y.sizes(), "out shape mismatch");
+  } else {
+    out = at::empty(y.sizes(), y.options());
+  }
   Tensor mask;
   if (want_mask && act == 1 && C % 8 == 0)
     mask = at::empty({(int64_t)(y.numel() / 8)}, y.options().dtype(at::kByte));
   auto aux = at::empty({4, C}, fopt);
+  BnLdScope lds(C, ldy, ldo);
   const float* k1 = shifted ? ptr<float>(acc) + (size_t)R * 2 * C : nullptr;
   const float* k2 = (dual && shifted2) ? ptr<float>(*acc2) + (size_t)R2 * 2 * C : nullptr;
   Tensor aux2;
@@ -842,10 +895,23 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
                                 const optional<Tensor>& dbeta2_acc,
                                 const optional<Tensor>& partial_in,
                                 const optional<Tensor>& acc_in, int acc_rows, bool acc_filled,
-                                const optional<Tensor>& zero1, const optional<Tensor>& zero2) {
-  check_bf16(dout, "dout");
-  check_bf16(y, "y");
+                                const optional<Tensor>& zero1, const optional<Tensor>& zero2,
+                                const optional<Tensor>& dx_out, bool dx_acc) {
+  // dout / y may be row-strided channel slices of concat slabs; dx_out (optional) receives dy
+  // (added into it with dx_acc), else dy is a new tensor
+  const int ldd = rows_ld(dout, "dout");
+  const int ldy = rows_ld(y, "y");
   const int C = y.size(-1);
+  TORCH_CHECK(dout.sizes() == y.sizes(), "dout shape mismatch");
+  int ldx = C;
+  const bool has_dx = dx_out.has_value() && dx_out->defined();
+  if (has_dx) {
+    ldx = rows_ld(*dx_out, "dx_out");
+    TORCH_CHECK(dx_out->sizes() == y.sizes(), "dx_out shape mismatch");
+  }
+  TORCH_CHECK(has_dx || !dx_acc, "dx_acc needs dx_out");
+  BnLdScope lds(C, ldy, C, ldd, ldx, dx_acc);
+  auto new_dy = [&]() { return has_dx ? *dx_out : at::empty(y.sizes(), y.options()); };
   const int M = y.numel() / C;
   const bool dual = y2.has_value() && y2->defined();
   const int NS = dual ? 3 : 2;
@@ -917,10 +983,10 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
                                   ptr<float>(dbeta), dual ? ptr<float>(dgamma2) : nullptr,
                                   dual ? ptr<float>(dbeta2) : nullptr, ptr<float>(coef), 1, st,
                                   zp1, zn1, zp2, zn2);
-      auto dy = at::empty_like(y);
+      auto dy = new_dy();
       Tensor dres, dy2;
-      if (need_dres) dres = at::empty_like(y);
-      if (dual) dy2 = at::empty_like(y);
+      if (need_dres) dres = at::empty(y.sizes(), y.options());
+      if (dual) dy2 = at::empty(y.sizes(), y.options());
       pca::bn_bwd_apply_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
                                ptr<float>(coef), act, C, y.numel(), ptr<bf16>(dy),
                                need_dres ? ptr<bf16>(dres) : nullptr, optr<bf16>(y2),
@@ -933,10 +999,10 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
       dgamma2 = pick(dgamma2_acc);
       dbeta2 = pick(dbeta2_acc);
     }
-    auto dy = at::empty_like(y);
+    auto dy = new_dy();
     Tensor dres, dy2;
-    if (need_dres) dres = at::empty_like(y);
-    if (dual) dy2 = at::empty_like(y);
+    if (need_dres) dres = at::empty(y.sizes(), y.options());
+    if (dual) dy2 = at::empty(y.sizes(), y.options());
     const bool fused = pca::bn_bwd_apply_acc_launch(
         ptr<bf16>(dout), mk, ptr<bf16>(y), C, M, (float)M, ptr<float>(acc), acc_rows,
         ptr<float>(aux), optr<float>(gamma), ptr<float>(dgamma), ptr<float>(dbeta),
@@ -1002,10 +1068,10 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
                               dual ? ptr<float>(dbeta2) : nullptr, ptr<float>(coef), 1, st,
                               nz1 ? ptr<float>(*zero1) : nullptr, nz1 ? (int)zero1->numel() : 0,
                               nz2 ? ptr<float>(*zero2) : nullptr, nz2 ? (int)zero2->numel() : 0);
-  auto dy = at::empty_like(y);
+  auto dy = new_dy();
   Tensor dres, dy2;
-  if (need_dres) dres = at::empty_like(y);
-  if (dual) dy2 = at::empty_like(y);
+  if (need_dres) dres = at::empty(y.sizes(), y.options());
+  if (dual) dy2 = at::empty(y.sizes(), y.options());
   pca::bn_bwd_apply_launch(ptr<bf16>(dout), optr<bf16>(out), mk, ptr<bf16>(y), ptr<float>(aux),
                            ptr<float>(coef), act, C, y.numel(), ptr<bf16>(dy),
                            need_dres ? ptr<bf16>(dres) : nullptr, optr<bf16>(y2),
@@ -1866,14 +1932,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("momentum"),
         py::arg("eps"), py::arg("training"), py::arg("update_running"), py::arg("kin") = py::none(),
         py::arg("pilot_out") = py::none(), py::arg("zero") = py::none());
-  m.def("bn_apply", &bn_apply);
+  m.def("bn_apply", &bn_apply, py::arg("y"), py::arg("aux"), py::arg("res"), py::arg("y2"),
+        py::arg("aux2"), py::arg("act"), py::arg("want_mask"), py::arg("out") = py::none());
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("mask"), py::arg("y"),
         py::arg("aux"), py::arg("gamma"), py::arg("y2"), py::arg("aux2"), py::arg("gamma2"),
         py::arg("act"), py::arg("training"), py::arg("need_dres"), py::arg("dgamma_acc"),
         py::arg("dbeta_acc"), py::arg("dgamma2_acc"), py::arg("dbeta2_acc"),
         py::arg("partial_in") = py::none(), py::arg("acc") = py::none(), py::arg("acc_rows") = 0,
         py::arg("acc_filled") = false, py::arg("zero1") = py::none(),
-        py::arg("zero2") = py::none());
+        py::arg("zero2") = py::none(), py::arg("dx_out") = py::none(), py::arg("dx_acc") = false);
   m.def("bn_apply_acc", &bn_apply_acc, py::arg("y"), py::arg("acc"), py::arg("R"),
         py::arg("count"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
         py::arg("nbt"), py::arg("momentum"), py::arg("eps"), py::arg("res"), py::arg("y2"),
@@ -1881,6 +1948,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rvar2"), py::arg("nbt2"), py::arg("momentum2"), py::arg("eps2"), py::arg("act"),
         py::arg("want_mask"), py::arg("zero") = py::none(), py::arg("shifted") = false,
         py::arg("pilot") = py::none(), py::arg("shifted2") = false, py::arg("pilot2") = py::none(),
+        py::arg("out") = py::none(),
         "training BN(+act/+res/+BN2) with the finalize folded in from sharded accumulators");
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("nhwc_to_nchw", &nhwc_to_nchw);

@@ -97,6 +97,14 @@ __device__ __forceinline__ void stat_out(float* base, int row, int shards, size_
     base[(size_t)row * rowlen + col] = v;
 }
 
+// Row strides of the BatchNorm kernels' tensors (batchnorm.hip set_bn_ld; 0 = dense [M][C]):
+// y input, out forward output, dout / dx backward input / output (dx_acc: add into dx)
+struct BnLd {
+  int y, out, dout, dx, dx_acc;
+};
+BnLd bn_ld();
+void set_bn_ld(const BnLd& ld);
+
 // Process-wide shard count the next producer launch writes with (0 = slab rows); set by the
 // host bindings around a launch (batchnorm.hip).
 int stat_shards();

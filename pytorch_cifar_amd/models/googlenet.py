@@ -21,7 +21,14 @@ class Inception(tnn.Module):
         self.b4 = Sequential(MaxPool2d(3, stride=1, padding=1), *_cbr(in_planes, pool_planes, 1))
 
     def forward(self, x):
-        return F.cat([self.b1(x), self.b2(x), self.b3(x), self.b4(x)], 1)
+        branches = (self.b1, self.b2, self.b3, self.b4)
+        widths = [b[-2].num_features for b in branches]
+        if F.ChannelSlab.usable(x, widths):
+            # zero-copy concat: each branch's final BN+ReLU writes its channel slice of
+            # the output slab; the slab's gradient reaches the branches as strided views
+            slab = F.ChannelSlab(x, widths)
+            return slab.cat([b(x, out=slab.dest(i)) for i, b in enumerate(branches)])
+        return F.cat([b(x) for b in branches], 1)
 
 
 class GoogLeNet(tnn.Module):

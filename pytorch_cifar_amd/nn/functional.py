@@ -5,6 +5,7 @@ import torch.nn.functional as TF
 from ..engine import grads
 from ..ops.functional import _ref
 from ..ops.functional import (  # noqa: F401
+    ChannelSlab,
     activation,
     adaptive_avg_pool2d,
     add_act,

@@ -64,13 +64,14 @@ class Conv2d(nn.Conv2d):
 
 
 class BatchNorm2d(nn.BatchNorm2d):
-    def forward(self, x, act=None, residual=None, residual_bn=None):
+    def forward(self, x, act=None, residual=None, residual_bn=None, out=None):
+        """``out``: a ChannelSlab destination slice (zero-copy concatenation), GPU path only."""
         stats = getattr(x, _STATS_ATTR, None) if self.training else None
         rb = None
         if residual_bn is not None:
             bn_b, xb = residual_bn
             rb = (bn_b, xb, getattr(xb, _STATS_ATTR, None) if bn_b.training else None)
-        return OF.batch_norm_act(self, x, act, residual, rb, stats)
+        return OF.batch_norm_act(self, x, act, residual, rb, stats, out=out)
 
 
 class Linear(nn.Linear):
@@ -96,17 +97,33 @@ class AvgPool2d(nn.AvgPool2d):
 
 
 class Sequential(nn.Sequential):
-    """nn.Sequential that fuses BatchNorm2d -> ReLU into one kernel pass."""
+    """nn.Sequential that fuses BatchNorm2d -> ReLU into one kernel pass.
 
-    def forward(self, x):
+    ``out`` (a ChannelSlab destination slice): the final BatchNorm(+ReLU) writes its result there
+    (zero-copy concatenation, googlenet.py Inception); a Sequential not ending in one cannot."""
+
+    def forward(self, x, out=None):
         mods = list(self._modules.values())
         i = 0
         while i < len(mods):
             m = mods[i]
             if isinstance(m, BatchNorm2d) and i + 1 < len(mods) and isinstance(mods[i + 1], (ReLU, nn.ReLU)):
-                x = m(x, act="relu")
+                last = i + 2 == len(mods)
+                x = m(x, act="relu", out=out if last else None)
                 i += 2
+                continue
+            if out is not None and i + 1 == len(mods):
+                if not isinstance(m, BatchNorm2d):
+                    raise ValueError("Sequential(out=...) needs a final BatchNorm2d(+ReLU)")
+                x = m(x, out=out)
+                i += 1
                 continue
             x = m(x)
             i += 1
         return x
+
+    def ends_in_bn(self):
+        mods = list(self._modules.values())
+        return bool(mods) and (isinstance(mods[-1], BatchNorm2d) or
+                               (len(mods) > 1 and isinstance(mods[-2], BatchNorm2d) and
+                                isinstance(mods[-1], (ReLU, nn.ReLU))))

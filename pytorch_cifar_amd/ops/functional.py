@@ -1003,10 +1003,12 @@ def add_bias(y_nhwc, bias):
 
 # -------------------------------------------------------------------------- batch norm
 class _BNCfg:
-    __slots__ = ("bn", "bn2", "act", "training", "count", "src", "bacc", "faccs", "pilot", "pilot2")
+    __slots__ = ("bn", "bn2", "act", "training", "count", "src", "bacc", "faccs", "pilot", "pilot2",
+                 "dest")
 
     def __init__(self, bn, bn2, act, training, count):
         self.bn, self.bn2, self.act, self.training, self.count = bn, bn2, act, training, count
+        self.dest = None      # NHWC channel slice of a concat slab the output is written into
         self.pilot = self.pilot2 = None   # the producers' pilots (receive this batch's means)
         self.src = None
         self.bacc = None      # the BN's backward StatAcc (sharded sums of dz, dz*xhat[, dz*xhat2])
@@ -1077,7 +1079,7 @@ class _BatchNormAct(torch.autograd.Function):
                 mom(bn2) if a2 is not None else 0.1, bn2.eps if a2 is not None else 1e-5,
                 ACT[cfg.act], relu, cfg.bacc.buf if cfg.bacc is not None else None,
                 stats.shifted, cfg.pilot, a2.shifted if a2 is not None else False,
-                cfg.pilot2 if a2 is not None else None)
+                cfg.pilot2 if a2 is not None else None, cfg.dest)
             if cfg.bacc is not None:
                 cfg.bacc.state = "clean"      # block 0 cleared this BN's backward accumulator
             stats.state = "used"
@@ -1096,7 +1098,7 @@ class _BatchNormAct(torch.autograd.Function):
             if y2 is not None:
                 aux2 = _bn_aux(C, bn2, y2, stats2 if isinstance(stats2, StatAcc) or (stats2 is not None and stats2.numel()) else None,
                                cfg.training, cfg.count, cfg.pilot2)
-            out, mask = C.bn_apply(y, aux, res, y2, aux2, ACT[cfg.act], relu)
+            out, mask = C.bn_apply(y, aux, res, y2, aux2, ACT[cfg.act], relu, cfg.dest)
             if cfg.bacc is not None:
                 cfg.bacc.ensure_clean()
             cfg.faccs = tuple(a for a in (stats, stats2) if isinstance(a, StatAcc))
@@ -1134,7 +1136,7 @@ class _BatchNormAct(torch.autograd.Function):
         y, out, mask, aux, y2, aux2 = ctx.saved_tensors
         cfg = ctx.cfg
         bn, bn2 = cfg.bn, cfg.bn2
-        dout = dout.contiguous()
+        dout = _rows_view(dout)        # (a concat slab's gradient slice stays a strided view)
 
         def acc(p):
             if p is None or not p.requires_grad or not p.is_leaf:
@@ -1224,11 +1226,13 @@ def _ref_act(x, act):
     raise ValueError(act)
 
 
-def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None):
+def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None, out=None):
     """act(BN(x) [+ residual] [+ BN_b(x_b)]) — the fused block tail of the model zoo.
 
     ``residual_bn=(bn_b, x_b, stats_b)`` fuses a projection-shortcut BatchNorm into the same pass
     (resnet.py:47-51 with the 1x1 conv shortcut of resnet.py:31-36).
+    ``out``: a :class:`ChannelSlab` destination (``slab.dest(i)``) the result is written into
+    (zero-copy concatenation); ignored on the CPU reference path.
     """
     training = bn.training
     if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None and _ref(x):
@@ -1255,6 +1259,8 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None)
         st2 = residual_bn[2] if len(residual_bn) > 2 else None
         y2 = to_nhwc(xb)
     cfg = _BNCfg(bn, bn2, act, training, N * H * W)
+    if out is not None:
+        cfg.dest = out
     if training and bn.running_mean is not None:
         # the producing MFMA conv(s) subtract this BN's pilot mean from their sums from now on
         p1 = getattr(x, "_pca_stats_src", None)
@@ -2036,6 +2042,76 @@ def cat_shuffle2(a, b):
     if _ref(a) or a.shape != b.shape or a.dtype != COMPUTE_DTYPE or b.dtype != COMPUTE_DTYPE:
         return channel_shuffle(cat([a, b], 1), 2)
     return to_nchw(_Interleave2.apply(to_nhwc(a), to_nhwc(b)))
+
+
+# ------------------------------------------------------------- zero-copy concatenation
+# a concatenation is a preallocated NHWC slab whose channel slices the producers
+# write directly (their BatchNorm+activation kernel takes the slice as a row-strided output:
+# batchnorm.hip BnLd), and whose gradient reaches each producer's backward as a row-strided view
+# of the slab's gradient — no gather copy forward, no split copy backward (reference
+# googlenet.py:53 torch.cat([y1, y2, y3, y4], 1), ...).
+def _rows_view(t):
+    """``t`` itself when it is a contiguous or row-strided NHWC [N,H,W,C] bf16 tensor whose channel
+    count allows the strided BatchNorm kernels (C % 8 == 0), else a contiguous copy."""
+    if t.is_contiguous():
+        return t
+    if (t.dim() == 4 and t.is_cuda and t.dtype == COMPUTE_DTYPE and t.stride(3) == 1 and
+            t.shape[3] % 8 == 0 and t.stride(2) >= t.shape[3] and
+            t.stride(1) == t.shape[2] * t.stride(2) and t.stride(0) == t.shape[1] * t.stride(1)):
+        return t
+    return t.contiguous()
+
+
+def _slab_alias(buf, c0, c1):
+    """A fresh tensor over channels [c0, c1) of the NHWC slab ``buf`` — not an autograd view of
+    it: slices are written by native kernels (no in-place op autograd could see), and each slice
+    is an independent output of its producer."""
+    t = torch.empty(0, dtype=buf.dtype, device=buf.device)
+    t.set_(buf.untyped_storage(), buf.storage_offset() + c0,
+           (buf.shape[0], buf.shape[1], buf.shape[2], c1 - c0), buf.stride())
+    return t
+
+
+class ChannelSlab:
+    """Destination of a channel concatenation: ``dest(i)`` is producer i's slice (pass it as the
+    ``out=`` of its final BatchNorm), ``cat(parts)`` returns the whole slab as the concat result."""
+
+    def __init__(self, like, widths):
+        N, _, H, W = like.shape
+        self.widths = list(widths)
+        self.offs = [0]
+        for w in self.widths:
+            self.offs.append(self.offs[-1] + w)
+        self.buf = torch.empty((N, H, W, self.offs[-1]), dtype=COMPUTE_DTYPE, device=like.device)
+
+    @staticmethod
+    def usable(x, widths):
+        return (not _ref(x) and x.dim() == 4 and all(w % 8 == 0 for w in widths)
+                and os.environ.get("PCA_ZERO_COPY_CAT", "1") != "0")
+
+    def dest(self, i):
+        return _slab_alias(self.buf, self.offs[i], self.offs[i + 1])
+
+    def cat(self, parts):
+        pns = [p.permute(0, 2, 3, 1) for p in parts]
+        for pn, o, w in zip(pns, self.offs, self.widths):
+            if (pn.untyped_storage().data_ptr() != self.buf.untyped_storage().data_ptr()
+                    or pn.storage_offset() != self.buf.storage_offset() + o or pn.shape[-1] != w):
+                raise RuntimeError("ChannelSlab.cat: part was not produced into its slab slice")
+        return to_nchw(_SlabCat.apply(self, *pns))
+
+
+class _SlabCat(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, slab, *parts):
+        ctx.offs = slab.offs
+        return _slab_alias(slab.buf, 0, slab.offs[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        # dy: NHWC-shaped gradient of the slab; producer i gets its channel range as a view
+        o = ctx.offs
+        return (None,) + tuple(dy[..., o[i]:o[i + 1]] for i in range(len(o) - 1))
 
 
 def cat(xs, dim=1):

@@ -1,0 +1,98 @@
+"""Zero-copy channel concatenation (ops/functional.py ChannelSlab).
+
+Producers write their channel slices of a preallocated NHWC slab (row-strided BatchNorm outputs,
+batchnorm.hip BnLd) and the slab's gradient reaches them as strided views (row-strided BatchNorm
+backward inputs / outputs). The arithmetic is unchanged, so against the copying concat
+(PCA_ZERO_COPY_CAT=0: native gather + split kernels) forward outputs, input gradients, parameter
+gradients and running statistics must be bitwise equal.
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(model, x, g, zero_copy, monkeypatch):
+    monkeypatch.setenv("PCA_ZERO_COPY_CAT", "1" if zero_copy else "0")
+    xi = x.clone().requires_grad_(True)
+    y = model(xi)
+    y.backward(g)
+    torch.cuda.synchronize()
+    grads = {n: (p.grad.clone() if p.grad is not None else None) for n, p in model.named_parameters()}
+    bufs = {n: b.clone() for n, b in model.named_buffers()}
+    return y.detach().float(), xi.grad.float(), grads, bufs
+
+
+@pytest.fixture
+def deterministic():
+    """Deterministic reductions (slab wgrads, ordered BN sums): run-to-run bitwise reproducible,
+    so the two concat implementations can be compared bitwise (fp32-atomic wgrads are not)."""
+    from pytorch_cifar_amd import _native
+
+    C = _native.lib()
+    det = C.deterministic()
+    C.set_deterministic(True)
+    yield
+    C.set_deterministic(det)
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_inception_slab_bitwise(train, monkeypatch, deterministic):
+    from pytorch_cifar_amd.models.googlenet import Inception
+
+    torch.manual_seed(0)
+    m0 = Inception(192, 64, 96, 128, 16, 32, 32).cuda().to(memory_format=torch.channels_last)
+    m0.train(train)
+    m1 = copy.deepcopy(m0)
+    x = torch.randn(8, 192, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(8, 256, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a = _step(m0, x, g, True, monkeypatch)
+    b = _step(m1, x, g, False, monkeypatch)
+    assert torch.equal(a[0], b[0]), "forward"
+    assert torch.equal(a[1], b[1]), "input gradient"
+    for n in a[2]:
+        if a[2][n] is None:
+            assert b[2][n] is None, n
+        else:
+            assert torch.equal(a[2][n], b[2][n]), n
+    for n in a[3]:
+        assert torch.equal(a[3][n], b[3][n]), n
+
+
+def test_slab_cat_rejects_foreign_part():
+    from pytorch_cifar_amd.ops.functional import ChannelSlab
+
+    x = torch.randn(2, 8, 4, 4, device="cuda").to(torch.bfloat16)
+    slab = ChannelSlab(x, [8, 8])
+    with pytest.raises(RuntimeError, match="slab slice"):
+        slab.cat([x, x])
+
+
+def test_strided_bn_backward_accumulates(monkeypatch):
+    """bn_backward writing into a strided destination with dx_acc adds onto what is there."""
+    from pytorch_cifar_amd import _native
+
+    C = _native.lib()
+    torch.manual_seed(1)
+    N, H, W, Cc, Ct = 4, 8, 8, 32, 96
+    slab = torch.randn(N, H, W, Ct, device="cuda").to(torch.bfloat16)
+    y = slab[..., 16:48]                                   # row-strided BN input
+    gslab = torch.randn(N, H, W, Ct, device="cuda").to(torch.bfloat16)
+    dout = gslab[..., 40:72]                               # row-strided incoming gradient
+    aux = torch.cat([torch.randn(Cc, device="cuda") * 0.1, torch.rand(Cc, device="cuda") + 0.5,
+                     torch.rand(Cc, device="cuda") + 0.5, torch.randn(Cc, device="cuda") * 0.1]).view(4, Cc)
+    gamma = torch.rand(Cc, device="cuda") + 0.5
+    ref = C.bn_backward(dout.contiguous(), None, None, y.contiguous(), aux, gamma, None, None, None,
+                        0, True, False, None, None, None, None)[0]
+    got = C.bn_backward(dout, None, None, y, aux, gamma, None, None, None, 0, True, False, None,
+                        None, None, None)[0]
+    assert torch.equal(got, ref)
+    dst_all = torch.randn(N, H, W, Ct, device="cuda").to(torch.bfloat16)
+    before = dst_all.clone()
+    C.bn_backward(dout, None, None, y, aux, gamma, None, None, None, 0, True, False, None, None,
+                  None, None, dx_out=dst_all[..., 8:40], dx_acc=True)
+    want = (before[..., 8:40].float() + ref.float()).to(torch.bfloat16).float()
+    assert (dst_all[..., 8:40].float() - want).abs().max() <= 1e-2 * want.abs().max()
+    assert torch.equal(dst_all[..., :8], before[..., :8]) and torch.equal(dst_all[..., 40:], before[..., 40:])
