@@ -47,6 +47,7 @@ void wgrad_clear_tuned();
 std::vector<std::vector<int>> tune_export();
 void c64_set_prof(int64_t* p);
 int c64_grid_size(int N, int H);
+void copy_rows_launch(const bf16* src, int lds, bf16* dst, int ldd, int P, int C, hipStream_t st);
 // batchnorm.hip: row strides of the next BN launches' tensors (0 = dense; common.h BnLd)
 struct BnLd {
   int y, out, dout, dx, dx_acc;
@@ -249,6 +250,16 @@ int rows_ld(const Tensor& t, const char* name) {
                   t.stride(1) == t.size(2) * t.stride(2) && t.stride(0) == t.size(1) * t.stride(1),
               name, " must be contiguous NHWC or a row-strided channel slice with C % 8 == 0");
   return (int)t.stride(2);
+}
+
+// dst <- src for NHWC [N,H,W,C] tensors of the same shape, either of them row-strided (a channel
+// slice of a concat slab), C % 8 == 0
+void copy_rows(const Tensor& src, const Tensor& dst) {
+  const int ls = rows_ld(src, "src"), ld = rows_ld(dst, "dst");
+  TORCH_CHECK(src.sizes() == dst.sizes() && src.dim() == 4, "copy_rows: shape mismatch");
+  const int C = src.size(3);
+  TORCH_CHECK(C % 8 == 0, "copy_rows needs C % 8 == 0");
+  pca::copy_rows_launch(ptr<bf16>(src), ls, ptr<bf16>(dst), ld, (int)(src.numel() / C), C, cur_stream());
 }
 
 // RAII: the row strides (0 = dense) the BatchNorm launches in scope read / write with
@@ -1951,6 +1962,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none(),
         "training BN(+act/+res/+BN2) with the finalize folded in from sharded accumulators");
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("copy_rows", &copy_rows, "dst <- src for NHWC tensors, either a row-strided channel slice");
   m.def("nhwc_to_nchw", &nhwc_to_nchw);
   m.def("augment", &augment);
   m.def("augment_packed", &augment_packed);

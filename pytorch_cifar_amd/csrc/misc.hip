@@ -436,6 +436,25 @@ void cat_nhwc_launch(const CatArgs& a, bf16* whole, int P, bool split, hipStream
 #undef PCA_CAT
 }
 
+// ---- row copy between NHWC matrices with their own row strides (zero-copy concatenation: a
+// producer's output into its channel slice of a slab, a slab slice's gradient out to a dense
+// tensor): dst[p * ldd + c] = src[p * lds + c], c < C (C % 8 == 0), 16-byte vectors
+__global__ __launch_bounds__(256) void copy_rows_kernel(const bf16* __restrict__ src, int lds,
+                                                        bf16* __restrict__ dst, int ldd, int P,
+                                                        int C) {
+  const int G = C / 8;
+  const size_t total = (size_t)P * G;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t p = i / G, c = (i - p * G) * 8;
+    *reinterpret_cast<uint4*>(dst + p * ldd + c) = *reinterpret_cast<const uint4*>(src + p * lds + c);
+  }
+}
+
+void copy_rows_launch(const bf16* src, int lds, bf16* dst, int ldd, int P, int C, hipStream_t st) {
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(grid_cap((size_t)P * C / 8)), dim3(256), 0, st, src,
+                     lds, dst, ldd, P, C);
+}
+
 // ---- ShuffleNetV2 join: shuffle(cat[a, b], groups=2) with equal widths C is the channel
 // interleave y[p][2i] = a[p][i], y[p][2i+1] = b[p][i] (shufflenetv2.py:49/73, ShuffleBlock
 // 10-19); one vectorized pass instead of a concat and a transposing copy. INV de-interleaves

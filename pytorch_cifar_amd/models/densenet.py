@@ -19,10 +19,27 @@ class Bottleneck(tnn.Module):
         self.bn2 = BatchNorm2d(4 * growth_rate)
         self.conv2 = Conv2d(4 * growth_rate, growth_rate, kernel_size=3, padding=1, bias=False)
 
-    def forward(self, x):
+    def forward(self, x, slab=None):
         out = self.conv1(self.bn1(x, act="relu"))
         out = self.conv2(self.bn2(out, act="relu"), want_stats=False)
+        if slab is not None:
+            return slab.append(out, x)     # zero-copy: x is the slab's suffix, out goes left of it
         return F.cat([out, x], 1)
+
+
+def dense_block(block, x):
+    """Run a dense block's layers; on the GPU the concatenations share one slab (F.DenseSlab)."""
+    layers = list(block)
+    g = layers[0].conv2.out_channels
+    if F.DenseSlab.usable(x, g, len(layers)):
+        slab = F.DenseSlab(x, g, len(layers))
+        x = slab.start(x)
+        for layer in layers:
+            x = layer(x, slab)
+        return x
+    for layer in layers:
+        x = layer(x)
+    return x
 
 
 class Transition(tnn.Module):
@@ -61,10 +78,10 @@ class DenseNet(tnn.Module):
 
     def forward(self, x):
         out = self.conv1(x, want_stats=False)
-        out = self.trans1(self.dense1(out))
-        out = self.trans2(self.dense2(out))
-        out = self.trans3(self.dense3(out))
-        out = self.dense4(out)
+        out = self.trans1(dense_block(self.dense1, out))
+        out = self.trans2(dense_block(self.dense2, out))
+        out = self.trans3(dense_block(self.dense3, out))
+        out = dense_block(self.dense4, out)
         return F.pool_linear(self.bn(out, act="relu"), 4, self.linear)
 
 

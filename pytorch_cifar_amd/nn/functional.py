@@ -6,6 +6,7 @@ from ..engine import grads
 from ..ops.functional import _ref
 from ..ops.functional import (  # noqa: F401
     ChannelSlab,
+    DenseSlab,
     activation,
     adaptive_avg_pool2d,
     add_act,

@@ -130,6 +130,16 @@ class GradSlot:
         return g
 
 
+class _DenseSlot(GradSlot):
+    """GradSlot of a dense-block slab suffix; ``claimed`` once a BatchNorm whose backward will
+    take it has read the suffix (only then may the append hand its gradient over)."""
+    __slots__ = ("claimed",)
+
+    def __init__(self):
+        super().__init__()
+        self.claimed = False
+
+
 def _slot_for_conv(x):
     """(slot, is_owner) for an MFMA conv reading the user-level activation ``x``."""
     if not (_FUSE_GRAD and x.requires_grad and torch.is_grad_enabled()):
@@ -1004,11 +1014,12 @@ def add_bias(y_nhwc, bias):
 # -------------------------------------------------------------------------- batch norm
 class _BNCfg:
     __slots__ = ("bn", "bn2", "act", "training", "count", "src", "bacc", "faccs", "pilot", "pilot2",
-                 "dest")
+                 "dest", "dslot")
 
     def __init__(self, bn, bn2, act, training, count):
         self.bn, self.bn2, self.act, self.training, self.count = bn, bn2, act, training, count
         self.dest = None      # NHWC channel slice of a concat slab the output is written into
+        self.dslot = None     # dense slab: GradSlot where the slab's gradient of the input waits
         self.pilot = self.pilot2 = None   # the producers' pilots (receive this batch's means)
         self.src = None
         self.bacc = None      # the BN's backward StatAcc (sharded sums of dz, dz*xhat[, dz*xhat2])
@@ -1110,6 +1121,8 @@ class _BatchNormAct(torch.autograd.Function):
         ctx.save_for_backward(y, out if (relu and not has_mask) else None, mask if has_mask else None,
                               aux, y2, aux2)
         ctx.bnsrc = None
+        if not y.is_contiguous():
+            cfg.src = None    # (the consumer dgrad's fused reduce reads y densely: not a slab slice)
         # (grad mode is off inside Function.forward: the caller decided it in cfg.src)
         if cfg.src is not None and relu and has_mask and y2 is None:
             ctx.bnsrc = cfg.src = _BNSrc(y, mask, aux, cfg.bacc)
@@ -1177,6 +1190,11 @@ class _BatchNormAct(torch.autograd.Function):
                     zeros[i] = fa.buf
                     fa.state = "clean"
             cfg.faccs = ()
+        # dense-block slab input: the slab's gradient of y (deposited by the append that also read
+        # y) is the destination, and this backward adds into it (no autograd sum of the two)
+        dgx = cfg.dslot.take() if cfg.dslot is not None else None
+        if dgx is not None:
+            dgx = _rows_view(dgx)
         dy, dres, dy2, dg, db, dg2, db2 = C.bn_backward(
             dout, out, mask, y, aux,
             bn.weight.detach() if bn.weight is not None else None,
@@ -1184,7 +1202,7 @@ class _BatchNormAct(torch.autograd.Function):
             bn2.weight.detach() if (bn2 is not None and bn2.weight is not None) else None,
             ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2, part,
             acc.buf if acc is not None else None, acc.R if acc is not None else 0, filled,
-            zeros[0], zeros[1])
+            zeros[0], zeros[1], dgx, dgx is not None)
         ret = {}
 
         def deliver(p, buf, val, slot):
@@ -1226,6 +1244,17 @@ def _ref_act(x, act):
     raise ValueError(act)
 
 
+def _bn_input(x):
+    """NHWC view of a BatchNorm input: a dense-block slab suffix stays a row-strided view
+    (the BN kernels take the row stride), anything else as ``to_nhwc``."""
+    v = x.permute(0, 2, 3, 1)
+    if not v.is_contiguous() and getattr(x, "_pca_dense_slot", None) is not None:
+        r = _rows_view(v)
+        if r is v:
+            return v
+    return to_nhwc(x)
+
+
 def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None, out=None):
     """act(BN(x) [+ residual] [+ BN_b(x_b)]) — the fused block tail of the model zoo.
 
@@ -1251,7 +1280,7 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None,
         out = batch_norm_act(bn, x, None, residual, residual_bn, stats)
         return activation(out, act)
     N, Cc, H, W = x.shape
-    y = to_nhwc(x)
+    y = _bn_input(x)
     res = to_nhwc(residual) if residual is not None else None
     y2 = st2 = bn2 = None
     if residual_bn is not None:
@@ -1261,6 +1290,9 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None,
     cfg = _BNCfg(bn, bn2, act, training, N * H * W)
     if out is not None:
         cfg.dest = out
+    cfg.dslot = getattr(x, "_pca_dense_slot", None)
+    if cfg.dslot is not None and torch.is_grad_enabled():
+        cfg.dslot.claimed = True
     if training and bn.running_mean is not None:
         # the producing MFMA conv(s) subtract this BN's pilot mean from their sums from now on
         p1 = getattr(x, "_pca_stats_src", None)
@@ -2112,6 +2144,82 @@ class _SlabCat(torch.autograd.Function):
         # dy: NHWC-shaped gradient of the slab; producer i gets its channel range as a view
         o = ctx.offs
         return (None,) + tuple(dy[..., o[i]:o[i + 1]] for i in range(len(o) - 1))
+
+
+class DenseSlab:
+    """One dense block's concatenations as a single slab (densenet.py:20 ``cat([out, x], 1)``,
+    new features first): x_0 sits at the slab's right end and layer l's g new channels go just
+    left of x_l, so every x_l is a channel suffix of the slab — read in place (row-strided) by the
+    next layer's BatchNorm, never re-copied: the block moves O(g) bytes per layer instead of the
+    O(C_l) gather + split of a copying concat. Gradients: x_l's gradient is a suffix view of the
+    slab gradient; the append deposits it in x_l's GradSlot and the BatchNorm that also read x_l
+    adds its own contribution into that memory (bn_backward dx_acc), so nothing is summed or split
+    by copies either."""
+
+    def __init__(self, x0, growth, layers):
+        N, C0, H, W = x0.shape
+        self.g = growth
+        self.C = C0 + growth * layers
+        self.buf = torch.empty((N, H, W, self.C), dtype=COMPUTE_DTYPE, device=x0.device)
+        self.c0 = self.C - C0      # first channel of the current suffix
+
+    @staticmethod
+    def usable(x0, growth, layers):
+        return (not _ref(x0) and x0.dim() == 4 and x0.dtype == COMPUTE_DTYPE and growth % 8 == 0
+                and x0.shape[1] % 8 == 0 and os.environ.get("PCA_ZERO_COPY_CAT", "1") != "0")
+
+    @staticmethod
+    def _suffix(t_nhwc, slot):
+        v = to_nchw(t_nhwc)
+        v._pca_dense_slot = slot
+        return v
+
+    def start(self, x0):
+        return self._suffix(_SlabPut.apply(to_nhwc(x0), self, self.c0), _DenseSlot())
+
+    def append(self, out, x):
+        """cat([out, x], 1) where x is this slab's current suffix."""
+        self.c0 -= self.g
+        xs, ys = x._pca_dense_slot, _DenseSlot()
+        return self._suffix(_DenseAppend.apply(to_nhwc(out), x.permute(0, 2, 3, 1), self, self.c0,
+                                               xs if xs.claimed else None, ys), ys)
+
+
+class _SlabPut(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, slab, c0):
+        dst = _slab_alias(slab.buf, c0, slab.C)
+        _C().copy_rows(x, dst)
+        return dst
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.empty(dy.shape, dtype=dy.dtype, device=dy.device)
+        _C().copy_rows(_rows_view(dy), dx)
+        return dx, None, None
+
+
+class _DenseAppend(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out, x, slab, c0, xslot, yslot):
+        ctx.g = out.shape[-1]
+        ctx.xslot, ctx.yslot = xslot, yslot
+        _C().copy_rows(out, _slab_alias(slab.buf, c0, c0 + ctx.g))
+        return _slab_alias(slab.buf, c0, slab.C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        g = ctx.g
+        if not ctx.yslot.claimed:
+            # dy came from outside (not a dense-block BatchNorm's fresh / slab-gradient tensor):
+            # it may be held elsewhere, so the in-place accumulation below works on a private copy
+            dy = dy.clone(memory_format=torch.contiguous_format)
+        dout = torch.empty(dy.shape[:-1] + (g,), dtype=dy.dtype, device=dy.device)
+        _C().copy_rows(_rows_view(dy[..., :g]), dout)     # dense copy for the conv's backward
+        dx = dy[..., g:]
+        if ctx.xslot is not None and ctx.xslot.offer(dx):
+            dx = None          # the BatchNorm that read x adds its gradient into this memory
+        return dout, dx, None, None, None, None
 
 
 def cat(xs, dim=1):

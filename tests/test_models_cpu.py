@@ -127,12 +127,12 @@ def test_fp32_matches_fp64(name):
     torch.manual_seed(0)
     o = _ours(name)
     o64 = copy.deepcopy(o).double()
-    x = torch.randn(8, 3, 32, 32)
+    x = torch.randn(16, 3, 32, 32)
     o.eval(), o64.eval()
     with torch.no_grad():
         assert _rel(o(x), o64(x.double())) < 1e-4, f"{name} eval logits"
     o.train(), o64.train()
-    g = torch.randn(8, 10)
+    g = torch.randn(16, 10)
     y64, gx64, gp64 = _run(o64, x.double(), g, 1)
     y, gx, gp = _run(o, x, g, 1)
     assert _rel(y, y64) < 1e-4, f"{name} train logits"

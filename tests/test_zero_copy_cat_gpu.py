@@ -96,3 +96,70 @@ def test_strided_bn_backward_accumulates(monkeypatch):
     want = (before[..., 8:40].float() + ref.float()).to(torch.bfloat16).float()
     assert (dst_all[..., 8:40].float() - want).abs().max() <= 1e-2 * want.abs().max()
     assert torch.equal(dst_all[..., :8], before[..., :8]) and torch.equal(dst_all[..., 40:], before[..., 40:])
+
+
+def _close(a, b, what, tol=2e-2):
+    scale = b.abs().max().clamp_min(1e-6)
+    err = (a - b).abs().max()
+    assert err <= tol * scale, f"{what}: max err {err.item():.3e} vs scale {scale.item():.3e}"
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_dense_block_slab(train, monkeypatch, deterministic):
+    """DenseNet block on one slab (F.DenseSlab) vs the copying concat: forward and running
+    statistics bitwise; gradients round once instead of twice where the two input-gradient
+    contributions meet (bn_backward dx_acc), so they agree to bf16 accumulation tolerance."""
+    from pytorch_cifar_amd.models.densenet import Bottleneck, dense_block
+    from pytorch_cifar_amd.nn import Sequential
+
+    torch.manual_seed(0)
+    c0, g, L = 64, 32, 4
+
+    class Block(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.dense = Sequential(*[Bottleneck(c0 + i * g, g) for i in range(L)])
+
+        def forward(self, x):
+            return dense_block(self.dense, x)
+
+    m0 = Block().cuda().to(memory_format=torch.channels_last)
+    m0.train(train)
+    m1 = copy.deepcopy(m0)
+    x = torch.randn(8, c0, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(8, c0 + L * g, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a = _step(m0, x, gy, True, monkeypatch)
+    b = _step(m1, x, gy, False, monkeypatch)
+    assert torch.equal(a[0], b[0]), "forward"
+    for n in a[3]:
+        assert torch.equal(a[3][n], b[3][n]), n
+    _close(a[1], b[1], "input gradient")
+    for n in a[2]:
+        if a[2][n] is None:
+            assert b[2][n] is None, n
+        else:
+            _close(a[2][n].float(), b[2][n].float(), n)
+
+
+def test_densenet121_slab_trace(monkeypatch):
+    """DenseNet121 training step on slabs: same loss as the copying concat and no concat / split
+    kernels left in the step (torch.profiler kernel names)."""
+    from pytorch_cifar_amd.models import DenseNet121
+
+    torch.manual_seed(0)
+    m0 = DenseNet121().cuda().to(memory_format=torch.channels_last)
+    m1 = copy.deepcopy(m0)
+    x = torch.randn(16, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(16, 10, device="cuda").to(torch.bfloat16)
+    a = _step(m0, x, gy, True, monkeypatch)
+    b = _step(m1, x, gy, False, monkeypatch)
+    assert torch.equal(a[0], b[0]), "logits"
+    for n in ("conv1.weight", "dense1.0.conv1.weight", "dense4.15.conv2.weight", "linear.weight"):
+        _close(a[2][n].float(), b[2][n].float(), n, tol=5e-2)
+    monkeypatch.setenv("PCA_ZERO_COPY_CAT", "1")
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        m0(x.clone().requires_grad_(True)).backward(gy)
+        torch.cuda.synchronize()
+    names = {e.name for e in prof.events()}
+    bad = [n for n in names if "cat_nhwc" in n or "split_nhwc" in n or "CatArray" in n]
+    assert not bad, bad
