@@ -910,6 +910,9 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
         if want_stats and acc is not None:
             return to_nchw(y), acc
         return to_nchw(y), (stats if want_stats else None)
+    S = _group_dense_width(Cin, Cout, Cg, cout_g, groups)
+    if S:
+        return _conv_group_dense(x, weight, bias, stride, padding, groups, S, want_stats, acc, pilot)
     if _GROUP_PAD:
         return _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats)
     y = _ConvDirect.apply(to_nhwc(x), weight, bias, stride, padding, groups)
@@ -925,6 +928,69 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
 # through them. Even where the padded group leaves most of a 64-wide MFMA tile empty (DPN's
 # 3-channel groups) this beats the scalar direct kernels by 10-30x (tools/zoo_bench.py).
 _GROUP_PAD = os.environ.get("PCA_GROUP_PAD", "1") != "0"
+
+
+# Narrow groups as block-diagonal super-groups: P = S / Cg neighbouring groups become one group of
+# S input channels whose weight is block-diagonal (zeros between the original groups). The
+# activations keep their layout (no pad / slice passes, and the conv keeps its fused BN
+# statistics / gradient hand-offs), the weight is expanded by one native remap per step and its
+# gradient's diagonal blocks are gathered back by the adjoint remap. It trades S / Cg x MFMA work
+# for tiles the implicit GEMM runs efficiently: DPN's 3..24-channel groups (dpn.py:15) ran at
+# ~15 TFLOP/s padded to 8 per group, plus two activation remap passes per conv each way.
+# PCA_GROUP_DENSE: 1 (default) for widths that are not multiples of 8, "all" also for multiples
+# of 8 below 64, 0 off.
+_GROUP_DENSE = os.environ.get("PCA_GROUP_DENSE", "1")
+
+
+def _group_dense_width(Cin, Cout, Cg, cout_g, groups):
+    """Super-group input width S for a grouped conv (0: keep the plain / padded path): the
+    smallest multiple of Cg that is >= 64, divides Cin and keeps both super-group widths
+    multiples of 8 (else the largest such)."""
+    if groups <= 1 or _GROUP_DENSE == "0" or (Cg % 8 == 0 and cout_g % 8 == 0 and
+                                               (_GROUP_DENSE != "all" or Cg >= 64)):
+        return 0
+    best = 0
+    for P in range(1, groups + 1):
+        if groups % P:
+            continue
+        S, So = P * Cg, P * cout_g
+        if S % 8 or So % 8:
+            continue
+        best = S
+        if S >= 64:
+            break
+    return best
+
+
+def _group_dense_remap(Cout, cout_g, Cg, S, K):
+    """Weight [Cout][K][Cg] (flat) -> block-diagonal [Cout][K][S] (flat)."""
+    def build():
+        P = S // Cg
+        cmap = []
+        for r in range(Cout):
+            lg = (r // cout_g) % P
+            for k in range(K):
+                base = (r * K + k) * Cg
+                cmap.extend(base + j - lg * Cg if lg * Cg <= j < (lg + 1) * Cg else -1
+                            for j in range(S))
+        m = Remap(cmap, Cout * K * Cg)
+        m.flat = True
+        return m
+    return Remap.get(("gdense", Cout, cout_g, Cg, S, K), build)
+
+
+def _conv_group_dense(x, weight, bias, stride, padding, groups, S, want_stats, acc, pilot):
+    Cout, Cg, KH, KW = weight.shape
+    Cin = x.shape[1]
+    remap = _group_dense_remap(Cout, Cout // groups, Cg, S, KH * KW)
+    wp = to_nchw(_remap_param(weight, remap, (Cout, KH, KW, S)))
+    slot, owner = _slot_for_conv(x)
+    bnsrc = getattr(x, "_pca_bnsrc", None) if x.requires_grad else None
+    y, stats = _ConvMFMA.apply(to_nhwc(x), wp, bias, stride, padding, Cin // S, want_stats, 0,
+                               slot, owner, bnsrc, acc if want_stats else None, pilot)
+    if want_stats and acc is not None:
+        return to_nchw(y), acc
+    return to_nchw(y), (stats if want_stats else None)
 
 
 def _group_pad_remap(groups, n, npad):
@@ -1925,6 +1991,7 @@ class Remap:
     hipGraph capture, on the warm-up steps — and reused by every replay."""
 
     _cache = {}
+    flat = False      # True: maps whole flattened tensors (one row of ``cin`` elements)
 
     def __init__(self, cmap, cin, rmap=None, rin=None, K=1):
         self.cmap, self.cin, self.rmap, self.rin, self.K = list(cmap), cin, rmap, rin, K
@@ -1974,16 +2041,18 @@ class _RemapFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, remap, out_shape, leaf):
         ctx.remap, ctx.in_shape, ctx.leaf = remap, x.shape, leaf
-        return remap.apply(x).view(out_shape)
+        return remap.apply(x.reshape(-1) if remap.flat else x).view(out_shape)
 
     @staticmethod
     def backward(ctx, dy):
         dy = dy.contiguous()
+        if ctx.remap.flat:
+            dy = dy.view(-1)
         leaf = ctx.leaf
         if leaf is not None:
             buf = G.grad_buffer(leaf)
             if buf is not None and tuple(buf.shape) == tuple(ctx.in_shape):
-                ctx.remap.apply(dy, inverse=True, acc=buf)
+                ctx.remap.apply(dy, inverse=True, acc=buf.view(-1) if ctx.remap.flat else buf)
                 G.fire(leaf)
                 return None, None, None, None
         return ctx.remap.apply(dy, inverse=True).view(ctx.in_shape), None, None, None

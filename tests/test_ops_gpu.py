@@ -383,13 +383,17 @@ def test_dual_bn_backward_reduce_fusion(batch):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("mode", ["1", "0", "all"])
 @pytest.mark.parametrize("Cin,Cout,G,k,s", [(200, 50, 2, 1, 1), (50, 176, 2, 1, 1), (96, 96, 32, 3, 2),
-                                           (128, 128, 32, 3, 1), (12, 44, 1, 3, 1), (3, 6, 1, 5, 1)])
-def test_group_padded_conv_matches_fp32(Cin, Cout, G, k, s):
-    """Odd per-group widths run on the MFMA GEMM with groups zero-padded to multiples of 8:
-    output, BN statistics, dX, dW against fp32 F.conv2d."""
+                                           (128, 128, 32, 3, 1), (12, 44, 1, 3, 1), (3, 6, 1, 5, 1),
+                                           (192, 192, 8, 3, 1), (96, 96, 32, 3, 1)])
+def test_group_padded_conv_matches_fp32(Cin, Cout, G, k, s, mode, monkeypatch):
+    """Narrow groups on the MFMA GEMM — as block-diagonal super-groups (PCA_GROUP_DENSE 1 / all)
+    or zero-padded to multiples of 8 (0): output, BN statistics, dX, dW against fp32 F.conv2d."""
     import torch.nn.functional as F
     from pytorch_cifar_amd.ops import functional as OF
+
+    monkeypatch.setattr(OF, "_GROUP_DENSE", mode)
 
     torch.manual_seed(7)
     p = k // 2
