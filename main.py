@@ -77,13 +77,25 @@ def _apply_runtime_flags(args, loaders):
             ld.fp32 = True
 
 def _data_parallel_ranks(args):
-    # torch.cuda.device_count() alone (amdsmi on ROCm) decides: torch.cuda.is_available() would
-    # start the HIP runtime in this launcher parent, which must stay off the GPU
+    # The launcher parent must stay off the GPU (it spawns the per-GPU ranks): --nproc or the
+    # visible-device list decide first; otherwise the devices are counted in a short-lived child
+    # process, since torch.cuda.device_count() may fall back to hipGetDeviceCount (a HIP
+    # initialisation) when amdsmi is unavailable.
     if args.nproc:
         return args.nproc
     if args.cpu:
         return 1
-    return max(1, torch.cuda.device_count())
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return max(1, len([d for d in v.split(",") if d.strip()]))
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True)
+    try:
+        return max(1, int(r.stdout.strip().splitlines()[-1]))
+    except (ValueError, IndexError):
+        return 1
 
 
 def main(argv=None):

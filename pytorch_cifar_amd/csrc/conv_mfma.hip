@@ -41,6 +41,10 @@
 #ifndef PCA_IGEMM_EU
 #define PCA_IGEMM_EU 1
 #endif
+// 1: software-pipelined epilogue store loop (next row's operands in flight), 0: chunked EU rows
+#ifndef PCA_IGEMM_EPF
+#define PCA_IGEMM_EPF 1
+#endif
 
 namespace pca {
 
@@ -270,20 +274,26 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
   constexpr int CG_ = BN / 8;
   static_assert(NT % CG_ == 0, "store loop channel group must be per-thread constant");
   const bool bnf = DGRAD && !SPLITK && g.bn_part != nullptr;
-  float bs1[8], bs2[8], bmean[8], bistd[8];
+  float bs1[8], bs2[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) bs1[q] = bs2[q] = bmean[q] = bistd[q] = 0.f;
-  if (bnf) {
-    const int gc = n0 + (tid % CG_) * 8;
-    if (gc < g.Cn) {
-      const int ch = grp * g.Cn + gc;
+  for (int q = 0; q < 8; ++q) bs1[q] = bs2[q] = 0.f;
+  // this thread's BN mean / istd: (re)loaded per tile at the epilogue (L2-resident), so their 16
+  // registers are not held across the K loop
+  auto load_bn_aux = [&](float* bmean, float* bistd) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        bmean[q] = g.bn_aux[ch + q];
-        bistd[q] = g.bn_aux[g.Co + ch + q];
+    for (int q = 0; q < 8; ++q) bmean[q] = bistd[q] = 0.f;
+    if (bnf) {
+      const int gc = n0 + (tid % CG_) * 8;
+      if (gc < g.Cn) {
+        const int ch = grp * g.Cn + gc;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          bmean[q] = g.bn_aux[ch + q];
+          bistd[q] = g.bn_aux[g.Co + ch + q];
+        }
       }
     }
-  }
+  };
   if constexpr (AUX2_LDS) {
     if (bnf && g.bn_y2 != nullptr) {   // (block-uniform) the dual BN's mean2 | istd2 into LDS
       float* aux2s = reinterpret_cast<float*>(smem + AUX2_OFF);
@@ -633,6 +643,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
           Cs[r * CST + c] = f2bf(acc[mi][ni][j]);
         }
     __syncthreads();
+    float bmean[8], bistd[8];
+    load_bn_aux(bmean, bistd);
     constexpr int CG = BN / 8;
     float bs3[8];
 #pragma unroll
@@ -648,6 +660,74 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
     static_assert(EIT % EU == 0, "store loop chunks");
     const int c8 = tid % CG;   // (NT % CG == 0: fixed per thread)
     const int gc = n0 + c8 * 8;
+#if PCA_IGEMM_EPF
+    // Software-pipelined store loop: row it+1's global operands (addend, y, mask, y2) are in
+    // flight while row it is combined and stored, so the tile's epilogue costs about one memory
+    // round trip instead of EIT of them (the one-workgroup-per-CU 256x128 dgrad otherwise idles
+    // its matrix cores for EIT latencies per tile). Two rows' operands live: 18 VGPRs.
+    struct EOp {
+      size_t o;
+      bool ok;
+      uint4 av, yv, y2v;
+      uint8_t mk;
+    };
+    auto eload = [&](int it, EOp& e) {
+      const int gm = m0 + (tid + it * NT) / CG;
+      e.ok = gm < Mrows && gc < g.Cn;
+      size_t pix = gm;
+      if constexpr (PARITY) {
+        const uint32_t n = fdiv(gm, g.fd_hw);
+        const uint32_t rem = gm - n * (rows_h * rows_w);
+        const uint32_t h = fdiv(rem, g.fd_w);
+        const uint32_t w = rem - h * rows_w;
+        pix = ((size_t)n * g.Ho + 2 * h + ph) * g.Wo + 2 * w + pw;
+      }
+      e.o = e.ok ? pix * g.Co + (size_t)grp * g.Cn + gc : 0;
+      if (addend) e.av = *reinterpret_cast<const uint4*>(addend + e.o);
+      if (bnf) {
+        e.yv = *reinterpret_cast<const uint4*>(g.bn_y + e.o);
+        e.mk = g.bn_mask[e.o >> 3];
+      }
+      if (dual) e.y2v = *reinterpret_cast<const uint4*>(g.bn_y2 + e.o);
+    };
+    auto eproc = [&](int it, const EOp& e) {
+      const int r = (tid + it * NT) / CG;
+      uint4 v = *reinterpret_cast<const uint4*>(Cs + r * CST + c8 * 8);
+      if (addend) {
+        float a[8], b[8];
+        unpack8(v, a);
+        unpack8(e.av, b);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] += b[q];
+        v = pack8(a);
+      }
+      const uint8_t m = e.ok ? e.mk : 0;
+      if (bnf) bn_fuse_acc_v(v, e.yv, m, bmean, bistd, bs1, bs2);
+      if (dual) {
+        if constexpr (AUX2_LDS) {
+          const float* aux2s = reinterpret_cast<const float*>(smem + AUX2_OFF) + c8 * 8;
+          bn_fuse_acc3_v(v, e.y2v, m, aux2s, aux2s + BN, bs3);
+        } else {
+          const float* a2 = g.bn_aux2 + grp * g.Cn + gc;
+          bn_fuse_acc3_v(v, e.y2v, m, a2, a2 + g.Co, bs3);
+        }
+      }
+      if (e.ok) *reinterpret_cast<uint4*>(Y + e.o) = v;
+    };
+    (void)EU;
+    EOp e0, e1;
+    eload(0, e0);
+#pragma unroll 1
+    for (int it = 0; it < EIT; it += 2) {
+      const bool has1 = it + 1 < EIT;
+      if (has1) eload(it + 1, e1);
+      eproc(it, e0);
+      if (has1) {
+        if (it + 2 < EIT) eload(it + 2, e0);
+        eproc(it + 1, e1);
+      }
+    }
+#else
 #pragma unroll 1
     for (int it0 = 0; it0 < EIT; it0 += EU) {
       size_t o[EU];
@@ -710,6 +790,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         if (ok[u]) *reinterpret_cast<uint4*>(Y + o[u]) = v;
       }
     }
+#endif
     __syncthreads();   // the C tile aliases the ring the next tile's prologue refills
     if constexpr (DGRAD && !SPLITK) {
       if (dual) {   // (epilogue-local: no accumulator registers live across the K loop)

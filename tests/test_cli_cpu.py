@@ -266,3 +266,25 @@ def test_main_dist_default_path_spawns_ranks_cpu(tmp_path):
     assert os.path.exists(tmp_path / "o" / "ckpt.pth"), out
     ck = torch.load(tmp_path / "o" / "ckpt.pth", weights_only=True)
     assert all(k.startswith("module.") for k in ck["net"])
+
+
+def test_data_parallel_rank_count_stays_off_gpu(monkeypatch):
+    """main.py counts ranks from --nproc / the visible-device list, else in a child process —
+    never by initialising HIP in the launcher parent."""
+    import importlib.util
+    import types
+
+    spec = importlib.util.spec_from_file_location("pca_main_cli", os.path.join(ROOT, "main.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    args = types.SimpleNamespace(nproc=0, cpu=False)
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2")
+    assert mod._data_parallel_ranks(args) == 3
+    assert mod._data_parallel_ranks(types.SimpleNamespace(nproc=5, cpu=False)) == 5
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    calls = []
+    monkeypatch.setattr(mod.torch.cuda, "device_count", lambda: calls.append(1) or 8)
+    assert mod._data_parallel_ranks(args) >= 1      # counted in a child (no GPU here: 1)
+    assert not calls, "device_count() ran in the launcher parent"

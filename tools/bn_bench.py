@@ -45,7 +45,10 @@ def main():
         g, b = torch.ones(ch, device="cuda"), torch.zeros(ch, device="cuda")
         aux = C.bn_finalize(C.bn_stats(y), float(M), g, b, rm, rv, None, 0.1, 1e-5, True, False)
         out, mask = C.bn_apply(y, aux, None, None, None, 1, True)
+        dst = torch.empty_like(y)
         cases = [
+            ("copy (stock)", lambda: dst.copy_(y), 2 * T),
+            ("copy_rows", lambda: C.copy_rows(y, dst), 2 * T),
             ("apply relu", lambda: C.bn_apply(y, aux, None, None, None, 1, True), 2 * T + T / 16),
             ("apply +res relu", lambda: C.bn_apply(y, aux, r, None, None, 1, True), 3 * T + T / 16),
             ("apply +bn2 relu", lambda: C.bn_apply(y, aux, None, r, aux, 1, True), 3 * T + T / 16),
