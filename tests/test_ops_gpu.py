@@ -576,10 +576,8 @@ def test_split_and_cat_shuffle2_match_torch(C):
 def test_noact_bn_fusion_matches_separate_reduce(stride, monkeypatch):
     """A BatchNorm without activation (MobileNetV2 block tail) whose backward sums are reduced by
     its consumer conv's dgrad epilogue under an all-ones mask (PCA_FUSE_BN_NOACT=1) vs the
-    separate reduce + finalize passes (0): input gradient, dgamma / dbeta and every other
-    parameter gradient agree."""
-    import copy
-
+    separate reduce + finalize passes (0): against the fp32 CPU reference, every gradient of the
+    fused run is as accurate as the unfused run's."""
     from pytorch_cifar_amd.models.mobilenetv2 import Block
     from pytorch_cifar_amd.nn import Sequential
     from pytorch_cifar_amd.ops import functional as OF
@@ -587,24 +585,28 @@ def test_noact_bn_fusion_matches_separate_reduce(stride, monkeypatch):
     torch.manual_seed(3)
     # block tails with identity shortcuts (stride 1) and without (stride 2), each consumed by the
     # next block's expand conv (the fused consumer dgrad)
-    first = Block(24, 32, 6, stride)
-    m0 = Sequential(first, Block(32, 32, 6, 1), Block(32, 32, 6, 1)).cuda().to(memory_format=torch.channels_last)
-    m1 = copy.deepcopy(m0)
-    x = torch.randn(16, 24, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    base = Sequential(Block(24, 32, 6, stride), Block(32, 32, 6, 1), Block(32, 32, 6, 1))
+    x = torch.randn(32, 24, 16, 16).bfloat16().float()
+    ref = copy.deepcopy(base)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    g = torch.randn(yr.shape).bfloat16().float()
+    yr.backward(g)
+    want = {n: p.grad for n, p in ref.named_parameters()}
     res = {}
-    for fuse, m in ((True, m0), (False, m1)):
+    for fuse in (True, False):
+        m = copy.deepcopy(base).cuda().to(memory_format=torch.channels_last)
         monkeypatch.setattr(OF, "_FUSE_BN_NOACT", fuse)
-        xi = x.clone().requires_grad_(True)
+        xi = x.cuda().bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_(True)
         with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
             y = m(xi)
-            g = torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(5))
-            y.backward(g.to(y.dtype).contiguous(memory_format=torch.channels_last))
+            y.backward(g.cuda().to(y.dtype).contiguous(memory_format=torch.channels_last))
             torch.cuda.synchronize()
         reduces = sum(1 for e in prof.events() if "bn_bwd_reduce" in e.name)
-        res[fuse] = (xi.grad.float(), {n: p.grad.float().clone() for n, p in m.named_parameters()},
-                     reduces)
+        errs = {n: rel(p.grad, want[n]) for n, p in m.named_parameters()}
+        res[fuse] = (rel(xi.grad, xr.grad), errs, reduces)
     assert res[True][2] < res[False][2], (res[True][2], res[False][2])   # the fusion engaged
-    assert rel(res[True][0], res[False][0]) < 2e-2
-    for n, g in res[False][1].items():
-        assert rel(res[True][1][n], g) < 3e-2, n
-    assert any(n.endswith("bn3.weight") for n in res[False][1])
+    assert res[True][0] <= 1.5 * res[False][0] + 1e-2, (res[True][0], res[False][0])
+    bad = [(n, round(e, 4), round(res[False][1][n], 4)) for n, e in res[True][1].items()
+           if e > 1.5 * res[False][1][n] + 2e-2]
+    assert not bad, bad

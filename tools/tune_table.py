@@ -17,6 +17,7 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 CONFIGS = [("ResNet18", 1024), ("ResNet18", 512), ("ResNet18", 256), ("ResNet18", 128),
            ("MobileNetV2", 1024), ("EfficientNetB0", 1024), ("EfficientNetB0", 128)]
 
