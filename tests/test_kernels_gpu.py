@@ -475,7 +475,9 @@ def test_pools_and_gap(C, Cc):
                                             (1152, 1, 5, 1, 2), (672, 1, 5, 2, 4), (2304, 1, 3, 1, 4),
                                             (20, 1, 5, 1, 6), (44, 1, 7, 1, 8), (88, 1, 7, 2, 8),
                                             (176, 1, 7, 1, 4), (30, 1, 7, 2, 9), (58, 1, 3, 1, 8),
-                                            (116, 1, 3, 2, 8), (58, 1, 5, 1, 6), (26, 1, 3, 1, 5)])
+                                            (116, 1, 3, 2, 8), (58, 1, 5, 1, 6), (26, 1, 3, 1, 5),
+                                            (96, 1, 3, 1, 32), (144, 1, 3, 1, 32), (200, 1, 3, 1, 12),
+                                            (144, 1, 3, 2, 32), (960, 1, 3, 1, 4)])
 def test_depthwise(C, Cin, mult, k, s, H):
     """Multiplier 1, k3/k5/k7, even C takes the rolling-window fast paths (8/4/2 channels per thread)
     (dwk_*, incl. > 256 channel groups split over grid.y in wgrad), the rest the generic
