@@ -24,9 +24,9 @@ class BasicBlock(tnn.Module):
                 Conv2d(in_planes, self.expansion * planes, kernel_size=1, stride=stride, bias=False),
                 BatchNorm2d(self.expansion * planes))
 
-    def forward(self, x):
-        out = self.bn1(self.conv1(x), act="relu")
-        return self.bn2(self.conv2(out), act="relu", **shortcut_kwargs(self.shortcut, x))
+    def forward(self, x, out=None):
+        y = self.bn1(self.conv1(x), act="relu")
+        return self.bn2(self.conv2(y), act="relu", out=out, **shortcut_kwargs(self.shortcut, x))
 
 
 class Root(tnn.Module):
@@ -36,13 +36,18 @@ class Root(tnn.Module):
                            padding=(kernel_size - 1) // 2, bias=False)
         self.bn = BatchNorm2d(out_channels)
 
-    def forward(self, xs):
-        return self.bn(self.conv(F.cat(list(xs), 1)), act="relu")
+    def forward(self, xs, out=None):
+        return self.forward_cat(F.cat(list(xs), 1), out)
+
+    def forward_cat(self, x, out=None):
+        return self.bn(self.conv(x), act="relu", out=out)
 
 
 class Tree(tnn.Module):
     def __init__(self, block, in_channels, out_channels, level=1, stride=1):
         super().__init__()
+        self.stride = stride
+        self.out_channels = out_channels
         self.root = Root(2 * out_channels, out_channels)
         if level == 1:
             self.left_tree = block(in_channels, out_channels, stride=stride)
@@ -51,10 +56,20 @@ class Tree(tnn.Module):
             self.left_tree = Tree(block, in_channels, out_channels, level=level - 1, stride=stride)
             self.right_tree = Tree(block, out_channels, out_channels, level=level - 1, stride=1)
 
-    def forward(self, x):
+    def forward(self, x, out=None):
+        C = self.out_channels
+        if F.ChannelSlab.usable(x, [C, C]):
+            # zero-copy Root concat: both children write their final BN output into their slice
+            # of one slab, which the root conv reads whole; the right child gets a dense copy of
+            # the left output (one C-wide pass instead of the 2C concat + split)
+            hw = ((x.shape[2] - 1) // self.stride + 1, (x.shape[3] - 1) // self.stride + 1)
+            slab = F.ChannelSlab(x, [C, C], hw)
+            out1 = self.left_tree(x, out=slab.dest(0))
+            out2 = self.right_tree(F.dense_copy(out1), out=slab.dest(1))
+            return self.root.forward_cat(slab.cat([out1, out2]), out=out)
         out1 = self.left_tree(x)
         out2 = self.right_tree(out1)
-        return self.root([out1, out2])
+        return self.root([out1, out2], out=out)
 
 
 def _stem(cin, cout):

@@ -16,6 +16,7 @@ from ..ops.functional import (  # noqa: F401
     cat_shuffle2,
     channel_shuffle,
     cross_entropy,
+    dense_copy,
     dpn_merge,
     drop_connect,
     dropout,

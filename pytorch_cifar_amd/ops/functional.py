@@ -2177,8 +2177,10 @@ class ChannelSlab:
     """Destination of a channel concatenation: ``dest(i)`` is producer i's slice (pass it as the
     ``out=`` of its final BatchNorm), ``cat(parts)`` returns the whole slab as the concat result."""
 
-    def __init__(self, like, widths):
+    def __init__(self, like, widths, hw=None):
         N, _, H, W = like.shape
+        if hw is not None:
+            H, W = hw          # the producers' output size (they may stride their input)
         self.widths = list(widths)
         self.offs = [0]
         for w in self.widths:
@@ -2200,6 +2202,28 @@ class ChannelSlab:
                     or pn.storage_offset() != self.buf.storage_offset() + o or pn.shape[-1] != w):
                 raise RuntimeError("ChannelSlab.cat: part was not produced into its slab slice")
         return to_nchw(_SlabCat.apply(self, *pns))
+
+
+class _CopyRows(torch.autograd.Function):
+    """Dense copy of a row-strided NHWC slab slice (one native pass; identity backward)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        _C().copy_rows(x, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+def dense_copy(x):
+    """A dense NHWC-stored copy of ``x`` (an NCHW-shaped view of a concat slab slice) for
+    consumers that need dense operands (the MFMA convs' A side, residual adds)."""
+    if _ref(x):
+        return x
+    return to_nchw(_CopyRows.apply(x.permute(0, 2, 3, 1)))
 
 
 class _SlabCat(torch.autograd.Function):

@@ -163,3 +163,42 @@ def test_densenet121_slab_trace(monkeypatch):
     names = {e.name for e in prof.events()}
     bad = [n for n in names if "cat_nhwc" in n or "split_nhwc" in n or "CatArray" in n]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("level,stride", [(1, 1), (2, 2)])
+def test_simpledla_tree_slab_bitwise(level, stride, monkeypatch, deterministic):
+    """SimpleDLA Tree with the zero-copy Root (children write their slab slices, the right child
+    reads a dense copy) vs the copying concat: bitwise equal outputs, gradients, running stats."""
+    from pytorch_cifar_amd.models.dla_simple import BasicBlock, Tree
+
+    torch.manual_seed(0)
+    m0 = Tree(BasicBlock, 32, 64, level=level, stride=stride).cuda().to(memory_format=torch.channels_last)
+    m1 = copy.deepcopy(m0)
+    x = torch.randn(8, 32, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ho = (16 - 1) // stride + 1
+    g = torch.randn(8, 64, ho, ho, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a = _step(m0, x, g, True, monkeypatch)
+    b = _step(m1, x, g, False, monkeypatch)
+    assert torch.equal(a[0], b[0]), "forward"
+    assert torch.equal(a[1], b[1]), "input gradient"
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), n
+    for n in a[3]:
+        assert torch.equal(a[3][n], b[3][n]), n
+
+
+def test_simpledla_step_has_no_concat_kernels(monkeypatch):
+    from pytorch_cifar_amd.models import SimpleDLA
+
+    torch.manual_seed(0)
+    m = SimpleDLA().cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(16, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(16, 10, device="cuda").to(torch.bfloat16)
+    monkeypatch.setenv("PCA_ZERO_COPY_CAT", "1")
+    m(x.clone().requires_grad_(True)).backward(gy)      # (warm: tuning, accumulators)
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        m(x.clone().requires_grad_(True)).backward(gy)
+        torch.cuda.synchronize()
+    names = {e.name for e in prof.events()}
+    bad = [n for n in names if "cat_nhwc" in n or "split_nhwc" in n or "CatArray" in n]
+    assert not bad, bad
