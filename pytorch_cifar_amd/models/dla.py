@@ -13,6 +13,8 @@ class Tree(tnn.Module):
     def __init__(self, block, in_channels, out_channels, level=1, stride=1):
         super().__init__()
         self.level = level
+        self.stride = stride
+        self.out_channels = out_channels
         if level == 1:
             self.root = Root(2 * out_channels, out_channels)
             self.left_node = block(in_channels, out_channels, stride=stride)
@@ -25,7 +27,11 @@ class Tree(tnn.Module):
             self.left_node = block(out_channels, out_channels, stride=1)
             self.right_node = block(out_channels, out_channels, stride=1)
 
-    def forward(self, x):
+    def forward(self, x, out=None):
+        C = self.out_channels
+        n = self.level + 2 if self.level > 1 else 2
+        if F.ChannelSlab.usable(x, [C] * n):
+            return self._forward_slab(x, C, n, out)
         xs = [self.prev_root(x)] if self.level > 1 else []
         for i in reversed(range(1, self.level)):
             x = getattr(self, "level_%d" % i)(x)
@@ -34,7 +40,25 @@ class Tree(tnn.Module):
         xs.append(x)
         x = self.right_node(x)
         xs.append(x)
-        return self.root(xs)
+        return self.root(xs, out=out)
+
+    def _forward_slab(self, x, C, n, out):
+        """Zero-copy Root concat: every child writes its final BN output into its slice of one
+        slab that the root conv reads whole; a child that also feeds the next one hands it a dense
+        copy (one C-wide pass instead of the n*C concat + split)."""
+        hw = ((x.shape[2] - 1) // self.stride + 1, (x.shape[3] - 1) // self.stride + 1)
+        slab = F.ChannelSlab(x, [C] * n, hw)
+        parts = []
+        if self.level > 1:
+            parts.append(self.prev_root(x, out=slab.dest(0)))
+        for i in reversed(range(1, self.level)):
+            y = getattr(self, "level_%d" % i)(x, out=slab.dest(len(parts)))
+            parts.append(y)
+            x = F.dense_copy(y)
+        y = self.left_node(x, out=slab.dest(len(parts)))
+        parts.append(y)
+        parts.append(self.right_node(F.dense_copy(y), out=slab.dest(len(parts))))
+        return self.root.forward_cat(slab.cat(parts), out=out)
 
 
 def _stem(cin, cout):

@@ -187,11 +187,35 @@ def test_simpledla_tree_slab_bitwise(level, stride, monkeypatch, deterministic):
         assert torch.equal(a[3][n], b[3][n]), n
 
 
-def test_simpledla_step_has_no_concat_kernels(monkeypatch):
-    from pytorch_cifar_amd.models import SimpleDLA
+@pytest.mark.parametrize("level,stride", [(1, 2), (2, 2), (3, 1)])
+def test_dla_tree_slab_bitwise(level, stride, monkeypatch, deterministic):
+    """DLA (paper-style) Tree with the zero-copy Root over level + 2 children vs the copying
+    concat: bitwise equal."""
+    from pytorch_cifar_amd.models.dla import BasicBlock, Tree
 
     torch.manual_seed(0)
-    m = SimpleDLA().cuda().to(memory_format=torch.channels_last)
+    cin = 32 if level < 3 else 64    # (level >= 3 chains level_i trees: reference needs cin == cout)
+    m0 = Tree(BasicBlock, cin, 64, level=level, stride=stride).cuda().to(memory_format=torch.channels_last)
+    m1 = copy.deepcopy(m0)
+    x = torch.randn(8, cin, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ho = (16 - 1) // stride + 1
+    g = torch.randn(8, 64, ho, ho, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a = _step(m0, x, g, True, monkeypatch)
+    b = _step(m1, x, g, False, monkeypatch)
+    assert torch.equal(a[0], b[0]), "forward"
+    assert torch.equal(a[1], b[1]), "input gradient"
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), n
+    for n in a[3]:
+        assert torch.equal(a[3][n], b[3][n]), n
+
+
+@pytest.mark.parametrize("name", ["SimpleDLA", "DLA"])
+def test_dla_step_has_no_concat_kernels(name, monkeypatch):
+    from pytorch_cifar_amd import models
+
+    torch.manual_seed(0)
+    m = models.build_model(name).cuda().to(memory_format=torch.channels_last)
     x = torch.randn(16, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     gy = torch.randn(16, 10, device="cuda").to(torch.bfloat16)
     monkeypatch.setenv("PCA_ZERO_COPY_CAT", "1")
