@@ -66,6 +66,10 @@ void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int,
 int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
 void conv_set_bn_dual(const bf16* y2, const float* aux2);
+void conv_set_addend_s2c(int on);
+bool conv_dgrad_s2c_ok(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                       int groups, int Ho, int Wo);
+void s2c_expand_launch(const bf16* in, bf16* out, int N, int Hc, int Wc, int C, hipStream_t st);
 void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
                        int Cin, int Cout, int KH, int KW, int stride, int pad, int groups, int Ho,
                        int Wo, hipStream_t st);
@@ -465,7 +469,8 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
                                     const optional<Tensor>& bn_acc = c10::nullopt,
                                     int acc_rows = 0,
                                     const optional<Tensor>& bn_y2 = c10::nullopt,
-                                    const optional<Tensor>& bn_aux2 = c10::nullopt) {
+                                    const optional<Tensor>& bn_aux2 = c10::nullopt,
+                                    bool addend_s2c = false) {
   check_bf16(dy, "dy");
   check_bf16(wt, "wt");
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
@@ -475,11 +480,20 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
   TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo,
               "dgrad geometry mismatch");
   const bf16* add = nullptr;
+  Tensor add_full;   // a compact stride-2 addend expanded, where the selected kernel needs it whole
   if (addend.has_value() && addend->defined()) {
     check_bf16(*addend, "addend");
-    TORCH_CHECK(addend->numel() == (int64_t)N * H * W * Cin && addend->is_contiguous(),
-                "addend must match dx (NHWC)");
-    add = ptr<bf16>(*addend);
+    if (addend_s2c) {
+      // [N][H/2][W/2][Cin]: the dX of a 1x1 stride-2 conv of the same input (even-even pixels)
+      TORCH_CHECK(stride == 2 && H % 2 == 0 && W % 2 == 0 && addend->is_contiguous() &&
+                      addend->numel() == (int64_t)N * (H / 2) * (W / 2) * Cin,
+                  "compact stride-2 addend must be [N][H/2][W/2][Cin]");
+      // (expanded lazily below: for tuning trials, or when the selected kernel needs it whole)
+    } else {
+      TORCH_CHECK(addend->numel() == (int64_t)N * H * W * Cin && addend->is_contiguous(),
+                  "addend must match dx (NHWC)");
+      add = ptr<bf16>(*addend);
+    }
   }
   const bool want_bn = bn_y.has_value() && bn_y->defined();
   if (want_bn) {
@@ -512,8 +526,18 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
       if (on) pca::conv_set_bn_dual(nullptr, nullptr);
     }
   } dual_scope(dual, dual ? ptr<bf16>(*bn_y2) : nullptr, dual ? ptr<float>(*bn_aux2) : nullptr);
+  auto expand_s2c = [&]() {
+    if (!add_full.defined()) {
+      add_full = at::empty({N, H, W, Cin}, dy.options());
+      pca::s2c_expand_launch(ptr<bf16>(*addend), ptr<bf16>(add_full), N, H / 2, W / 2, Cin,
+                             cur_stream());
+    }
+    return ptr<bf16>(add_full);
+  };
+  const bool s2c = addend_s2c && addend.has_value() && addend->defined();
   if (g_autotune && !stream_capturing(cur_stream()) &&
       pca::conv_needs_tune(1, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, false)) {
+    if (s2c) add = expand_s2c();   // (trials run with the whole addend)
     // trials run the call as issued: with the fused BN-backward reduce when it is requested
     // (its epilogue traffic decides between candidates that tie on the plain dgrad)
     autotune_conv(1, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, [&] {
@@ -551,6 +575,18 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
     part = at::empty({rows, 2, Cin}, dy.options().dtype(at::kFloat));
   }
   ShardScope shards(use_acc ? acc_rows : 0);
+  // the kernel the (tuned) selection runs adds a compact addend itself when it can
+  struct S2cScope {
+    bool on;
+    explicit S2cScope(bool o) : on(o) {
+      if (on) pca::conv_set_addend_s2c(1);
+    }
+    ~S2cScope() {
+      if (on) pca::conv_set_addend_s2c(0);
+    }
+  } s2c_scope(s2c && pca::conv_dgrad_s2c_ok(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho,
+                                            Wo));
+  if (s2c) add = s2c_scope.on ? ptr<bf16>(*addend) : expand_s2c();
   pca::conv_dgrad_launch(ptr<bf16>(dy), ptr<bf16>(wt), ptr<bf16>(dx), N, H, W, Cin, Cout, KH, KW,
                          stride, pad, groups, Ho, Wo, cur_stream(), add,
                          wsn > 0 ? ptr<float>(ws) : nullptr,
@@ -563,9 +599,9 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
 }
 
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, int pad,
-                  int groups, const optional<Tensor>& addend) {
+                  int groups, const optional<Tensor>& addend, bool addend_s2c) {
   return conv_dgrad_impl(dy, wt, H, W, stride, pad, groups, addend, c10::nullopt, c10::nullopt,
-                         c10::nullopt)[0];
+                         c10::nullopt, c10::nullopt, 0, c10::nullopt, c10::nullopt, addend_s2c)[0];
 }
 
 // dw: fp32 [Cout, KH, KW, Cin/G] (zeroed here)
@@ -1889,11 +1925,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("groups"), py::arg("want_stats"), py::arg("stat_acc") = py::none(),
         py::arg("acc_rows") = 0, py::arg("stat_shift") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"),
-        py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend") = py::none());
+        py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend") = py::none(),
+        py::arg("addend_s2c") = false);
   m.def("conv_dgrad_bn", &conv_dgrad_impl, py::arg("dy"), py::arg("wt"), py::arg("H"),
         py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend"),
         py::arg("bn_y"), py::arg("bn_mask"), py::arg("bn_aux"), py::arg("bn_acc") = py::none(),
         py::arg("acc_rows") = 0, py::arg("bn_y2") = py::none(), py::arg("bn_aux2") = py::none(),
+        py::arg("addend_s2c") = false,
         "dgrad + fused backward reduce of the producing BN+ReLU -> (dx, partial[rows][2][C]); "
         "with bn_y2 / bn_aux2 (dual BN, accumulator mode) the accumulator gets [R][3][C] sums");
   m.def("conv_wgrad", &conv_wgrad);

@@ -34,6 +34,7 @@ struct HxGeom {
   int tiles;        // N * H * W / BM
   uint32_t a_bytes, b_bytes;
   int shards;       // stats / bn_part: 0 = slab rows, >0 = sharded atomic accumulator
+  int add_s2c;      // stride-2 dgrad: compact [N][H/2][W/2][Cin] addend for class 0 only
   // dgrad: fused backward reduce of the BN(+ReLU) that produced this conv's input (bn_part != 0)
   const bf16* bn_y;
   const uint8_t* bn_mask;
@@ -200,6 +201,8 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
   // its output-tensor channel (depth-to-space: class ch / COUT, channel ch % COUT)
   const int co_lane = D2S ? ch_lane % g.COUT : ch_lane;
   const int cls_lane = D2S ? ch_lane / g.COUT : 0;
+  // (a compact stride-2 addend belongs to parity class 0: the even-even output pixels)
+  const bool add_on = addend != nullptr && (!D2S || !g.add_s2c || cls_lane == 0);
   if (bnf) {   // the block's BN mean / istd once into LDS (read per element in the epilogue)
     for (int i = tid; i < 2 * BN; i += NW * 64)
       auxs[i] = g.bn_aux[(i >= BN ? g.COUT : 0) + (nb0 + (i % BN)) % g.COUT];
@@ -281,9 +284,12 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
               const size_t o = out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
-              if (addend) {
-                pre_a[mi][0] = *reinterpret_cast<const uint4*>(addend + o);
-                pre_a[mi][1] = *reinterpret_cast<const uint4*>(addend + o + 8);
+              if (add_on) {
+                const size_t oa = (D2S && g.add_s2c)
+                                      ? ((size_t)t * BM + wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane
+                                      : o;
+                pre_a[mi][0] = *reinterpret_cast<const uint4*>(addend + oa);
+                pre_a[mi][1] = *reinterpret_cast<const uint4*>(addend + oa + 8);
               }
               if (bnf) {
                 if constexpr (kHxPrefetchY) {
@@ -366,7 +372,7 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
         }
       }
       if constexpr (DGRAD) {
-        if (addend) {   // dX = conv^T(dY) + addend in fp32, rounded to bf16 once
+        if (add_on) {   // dX = conv^T(dY) + addend in fp32, rounded to bf16 once
           float b2[16];
           unpack8(pre_a[mi][0], b2);
           unpack8(pre_a[mi][1], b2 + 8);
@@ -546,6 +552,9 @@ static int hx_dispatch(const bf16* a, const bf16* b, bf16* y, float* stats, cons
 // launch (or, with launch = false, only size: returns the BN-statistics slab rows).
 // dgrad: H is the produced (= dY) map size; mode 2 (stride-2 dgrad) takes H = the dY map size and
 // b = the 2x2 class weights from conv_hx_s2_weights (CO = 4 x Cin).
+static int g_hx_add_s2c = 0;
+void conv_hx_set_addend_s2c(int on) { g_hx_add_s2c = on; }
+
 int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf16* addend,
                    const float* bias, int N, int H, int CA, int CO, int mode, hipStream_t st,
                    const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
@@ -566,6 +575,7 @@ int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf
   g.bn_y2 = mode == 1 && bn_part ? bn_y2 : nullptr;   // (accumulator mode: rows of 3 sums)
   g.bn_aux2 = g.bn_y2 ? bn_aux2 : nullptr;
   g.kshift = mode == 0 && stats ? stat_shift() : nullptr;
+  g.add_s2c = mode == 2 ? g_hx_add_s2c : 0;
   if (mode == 0) return hx_dispatch<0>(a, b, y, stats, addend, bias, g, H, st, launch);
   if (mode == 1) return hx_dispatch<1>(a, b, y, stats, addend, bias, g, H, st, launch);
   return hx_dispatch<2>(a, b, y, stats, addend, bias, g, H, st, launch);

@@ -80,6 +80,10 @@ struct ConvGeom {
   const float* bn_aux2;
   int shards;           // BN partial sums (stats / bn_part): 0 = slab rows, >0 = sharded atomics
   const float* kshift;  // forward stats: per-channel shift K (common.h stat_shift), or nullptr
+  // parity dgrad (MODE 2): the addend is COMPACT — [N][H/2][W/2][Co], the dX of a 1x1 stride-2
+  // conv reading the same input (ResNet projection shortcut), nonzero only at the even-even
+  // pixels: parity class 0 adds it at its own row index, the other classes add nothing
+  int addend_s2c;
 };
 
 // dz = dX * relu'(y), accumulated as (sum dz, sum dz * xhat) for 8 channels
@@ -665,6 +669,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
     // flight while row it is combined and stored, so the tile's epilogue costs about one memory
     // round trip instead of EIT of them (the one-workgroup-per-CU 256x128 dgrad otherwise idles
     // its matrix cores for EIT latencies per tile). Two rows' operands live: 18 VGPRs.
+    // (a compact stride-2 addend exists for parity class 0 only)
+    const bool add_on = addend != nullptr && (!PARITY || !g.addend_s2c || cls == 0);
     struct EOp {
       size_t o;
       bool ok;
@@ -683,7 +689,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         pix = ((size_t)n * g.Ho + 2 * h + ph) * g.Wo + 2 * w + pw;
       }
       e.o = e.ok ? pix * g.Co + (size_t)grp * g.Cn + gc : 0;
-      if (addend) e.av = *reinterpret_cast<const uint4*>(addend + e.o);
+      if (add_on) {
+        const size_t oa = (PARITY && g.addend_s2c) ? (e.ok ? (size_t)gm * g.Co + (size_t)grp * g.Cn + gc : 0) : e.o;
+        e.av = *reinterpret_cast<const uint4*>(addend + oa);
+      }
       if (bnf) {
         e.yv = *reinterpret_cast<const uint4*>(g.bn_y + e.o);
         e.mk = g.bn_mask[e.o >> 3];
@@ -693,7 +702,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
     auto eproc = [&](int it, const EOp& e) {
       const int r = (tid + it * NT) / CG;
       uint4 v = *reinterpret_cast<const uint4*>(Cs + r * CST + c8 * 8);
-      if (addend) {
+      if (add_on) {
         float a[8], b[8];
         unpack8(v, a);
         unpack8(e.av, b);
@@ -748,9 +757,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         }
         o[u] = ok[u] ? pix * g.Co + (size_t)grp * g.Cn + gc : 0;
       }
-      if (addend) {
+      const bool add_on = addend != nullptr && (!PARITY || !g.addend_s2c || cls == 0);
+      if (add_on) {
 #pragma unroll
-        for (int u = 0; u < EU; ++u) av[u] = *reinterpret_cast<const uint4*>(addend + o[u]);
+        for (int u = 0; u < EU; ++u) {
+          const int gm = m0 + (tid + (it0 + u) * NT) / CG;
+          const size_t oa = (PARITY && g.addend_s2c) ? (ok[u] ? (size_t)gm * g.Co + (size_t)grp * g.Cn + gc : 0) : o[u];
+          av[u] = *reinterpret_cast<const uint4*>(addend + oa);
+        }
       }
       if (bnf) {
 #pragma unroll
@@ -767,7 +781,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       for (int u = 0; u < EU; ++u) {
         const int r = (tid + (it0 + u) * NT) / CG;
         uint4 v = *reinterpret_cast<const uint4*>(Cs + r * CST + c8 * 8);
-        if (addend) {
+        if (add_on) {
           // fused gradient accumulation (dgrad): dX = conv^T(dY) + the other branch's dX
           float a[8], b[8];
           unpack8(v, a);
@@ -1696,6 +1710,7 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   g.bn_aux2 = nullptr;
   g.shards = stat_shards();
   g.kshift = stat_shift();
+  g.addend_s2c = 0;
   return g;
 }
 
@@ -1859,6 +1874,7 @@ static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, co
     const int M = g.N * g.Ho * g.Wo;
     int rpb;
     const int gx = splitk_reduce_grid(M, g.Co, &rpb);
+    if (g.addend_s2c) addend = nullptr;   // (tuning trials only: bindings expand it for real calls)
     if (stats)
       hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
                          rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2,
@@ -1965,6 +1981,7 @@ int conv_hx_launch(const bf16* a, const bf16* b, bf16* y, float* stats, const bf
 bool conv_hx_s2_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                            int pad, int groups, int Ho, int Wo);
 bool conv_hx_dual();
+void conv_hx_set_addend_s2c(int on);
 void conv_hx_s2_weights(const bf16* wt, int Cin, int Cout, bf16* w2, hipStream_t st);
 // (for a dgrad geometry g: Hs/Ws/Cs = dY, Ho/Wo/Co = dX)
 static bool hx_ok(const ConvGeom& g, int mode) {
@@ -2042,8 +2059,10 @@ static void igemm_dispatch(const bf16* A, const bf16* B, bf16* Y, float* stats, 
       conv_hx_s2_weights(B, g.Co, g.Cs, w2, st);
       Bw = w2;
     }
+    conv_hx_set_addend_s2c(MODE == 2 ? g.addend_s2c : 0);
     conv_hx_launch(A, Bw, Y, stats, addend, bias, g.N, g.Hs, g.Cs, MODE == 2 ? 4 * g.Co : g.Co,
                    MODE, st, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, true, g.bn_y2, g.bn_aux2);
+    conv_hx_set_addend_s2c(0);
     return;
   }
   switch (igemm_select(g)) {
@@ -2117,6 +2136,22 @@ static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int K
 
 static bool dgrad_parity(int H, int W, int stride, int Ho, int Wo) {
   return stride == 2 && H % 2 == 0 && W % 2 == 0 && Ho == H / 2 && Wo == W / 2;
+}
+
+// compact stride-2 addend (ConvGeom::addend_s2c) of the next dgrad launches (bindings scope it)
+static int g_addend_s2c = 0;
+void conv_set_addend_s2c(int on) { g_addend_s2c = on; }
+
+// can the dgrad this geometry selects take a compact stride-2 addend? (parity class 0 adds it:
+// the halo stride-2 kernel and the unsplit parity igemm; c64 / split-K / generic gather cannot)
+bool conv_dgrad_s2c_ok(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                       int groups, int Ho, int Wo) {
+  if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return false;
+  const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+  if (g.mode != 2 || ph_cfg<2>(g) >= 0) return false;
+  if (use_hx<2>(g)) return true;
+  return igemm_ws_floats<2>(g) == 0;
 }
 
 int64_t conv_dgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
@@ -2294,6 +2329,7 @@ void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, i
   g.bn_mask = bn_mask;
   g.bn_aux = bn_aux;
   g.bn_part = bn_part;
+  g.addend_s2c = g.mode == 2 ? g_addend_s2c : 0;
   if (bn_part && g_dual_y2 && g.mode == 1 && ph_cfg<1>(g) < 0 && (!use_hx<1>(g) || conv_hx_dual())) {
     g.bn_y2 = g_dual_y2;
     g.bn_aux2 = g_dual_aux2;

@@ -439,6 +439,31 @@ void cat_nhwc_launch(const CatArgs& a, bf16* whole, int P, bool split, hipStream
 // ---- row copy between NHWC matrices with their own row strides (zero-copy concatenation: a
 // producer's output into its channel slice of a slab, a slab slice's gradient out to a dense
 // tensor): dst[p * ldd + c] = src[p * lds + c], c < C (C % 8 == 0), 16-byte vectors
+// out[n][2i+a][2j+b][c] = (a == b == 0) ? in[n][i][j][c] : 0 — a compact stride-2 dgrad
+// addend expanded for a kernel that cannot add it per parity class (16-byte vectors, C % 8 == 0)
+__global__ __launch_bounds__(256) void s2c_expand_kernel(const bf16* __restrict__ in,
+                                                         bf16* __restrict__ out, int Hc, int Wc,
+                                                         int C8, int64_t total) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C8);
+    int64_t q = i / C8;
+    const int x = (int)(q % (2 * Wc));
+    q /= 2 * Wc;
+    const int y = (int)(q % (2 * Hc));
+    const int64_t n = q / (2 * Hc);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (!(x & 1) && !(y & 1))
+      v = reinterpret_cast<const uint4*>(in)[((n * Hc + (y >> 1)) * Wc + (x >> 1)) * C8 + c];
+    reinterpret_cast<uint4*>(out)[i] = v;
+  }
+}
+
+void s2c_expand_launch(const bf16* in, bf16* out, int N, int Hc, int Wc, int C, hipStream_t st) {
+  const int64_t total = (int64_t)N * 4 * Hc * Wc * (C / 8);
+  hipLaunchKernelGGL(s2c_expand_kernel, dim3((unsigned)std::min<int64_t>(cdiv64(total, 256), 8192)),
+                     dim3(256), 0, st, in, out, Hc, Wc, C / 8, total);
+}
+
 __global__ __launch_bounds__(256) void copy_rows_kernel(const bf16* __restrict__ src, int lds,
                                                         bf16* __restrict__ dst, int ldd, int P,
                                                         int C) {

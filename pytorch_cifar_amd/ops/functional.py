@@ -112,11 +112,14 @@ _FUSE_GRAD = os.environ.get("PCA_FUSE_RESIDUAL_GRAD", "1") != "0"
 
 
 class GradSlot:
-    __slots__ = ("grad", "closed")
+    # s2c: the owner is a 3x3 / stride-2 / pad-1 conv, so a 1x1 / stride-2 sibling may hand over
+    # its dX in compact form (even-even pixels only; the owner's parity dgrad adds it in place)
+    __slots__ = ("grad", "closed", "s2c")
 
     def __init__(self):
         self.grad = None
         self.closed = False
+        self.s2c = False
 
     def offer(self, g) -> bool:
         if self.closed or self.grad is not None or g is None:
@@ -594,16 +597,17 @@ def _own_stats(bn, role, y_nhwc, stats):
 
 
 def _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add):
+    s2c = add is not None and getattr(add, "_pca_s2c", False)
     if src is None or src.act != 1 or src.mask is None or (src.y2 is not None and src.acc is None):
-        return C.conv_dgrad(dy, wt, H, W, stride, padding, groups, add)
+        return C.conv_dgrad(dy, wt, H, W, stride, padding, groups, add, s2c)
     acc = src.acc
     if acc is not None:
         acc.begin()
         dx, part = C.conv_dgrad_bn(dy, wt, H, W, stride, padding, groups, add, src.y, src.mask,
-                                   src.aux, acc.buf, acc.R, src.y2, src.aux2)
+                                   src.aux, acc.buf, acc.R, src.y2, src.aux2, s2c)
     else:
         dx, part = C.conv_dgrad_bn(dy, wt, H, W, stride, padding, groups, add, src.y, src.mask,
-                                   src.aux)
+                                   src.aux, addend_s2c=s2c)
     if part.numel():
         src.part, src.dx = part, dx   # the reference to dx keeps autograd from adding into it
     elif acc is not None:
@@ -620,6 +624,10 @@ class _ConvMFMA(torch.autograd.Function):
         C = _C()
         ctx.slot, ctx.owner = slot, owner
         ctx.bnsrc = bnsrc
+        if slot is not None and owner:
+            slot.s2c = (_S2C_ADDEND and stride == 2 and padding == 1 and groups == 1 and
+                        weight.shape[2] == 3 and weight.shape[3] == 3 and
+                        x.shape[1] % 2 == 0 and x.shape[2] % 2 == 0)
         w_phys = G.physical(weight)
         if not w_phys.is_contiguous():
             w_phys = w_phys.contiguous()
@@ -692,6 +700,18 @@ class _ConvMFMA(torch.autograd.Function):
                     dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add)
                 elif slot is None:
                     dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, None)
+                elif (slot.s2c and stride == 2 and padding == 0 and groups == 1 and
+                      wt.shape[1] == 1 and wt.shape[2] == 1 and H == 2 * dy.shape[1] and
+                      W == 2 * dy.shape[2]):
+                    # 1x1 stride-2 projection shortcut: its dX is nonzero only at the even-even
+                    # pixels — computed compact as a plain 1x1 dgrad (a GEMM, no parity classes
+                    # writing zeros) and added by the owner's parity dgrad in its class 0
+                    dxc = C.conv_dgrad(dy, wt, dy.shape[1], dy.shape[2], 1, 0, 1)
+                    dxc._pca_s2c = True
+                    if slot.offer(dxc):
+                        dx = None
+                    else:
+                        dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
                 else:
                     dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
                     if slot.offer(dx):
@@ -940,6 +960,9 @@ _GROUP_PAD = os.environ.get("PCA_GROUP_PAD", "1") != "0"
 # PCA_GROUP_DENSE: 1 (default) for widths that are not multiples of 8, "all" also for multiples
 # of 8 below 64, 0 off.
 _GROUP_DENSE = os.environ.get("PCA_GROUP_DENSE", "1")
+# PCA_S2C_ADDEND=0: projection-shortcut dX written whole (zeros at 3 of 4 pixels) and added as a
+# full addend, instead of the compact even-even form
+_S2C_ADDEND = os.environ.get("PCA_S2C_ADDEND", "1") != "0"
 
 
 def _group_dense_width(Cin, Cout, Cg, cout_g, groups):

@@ -839,3 +839,36 @@ def test_squeeze_excite_matches_fp32(N, H, C, R, act, bias):
         assert rel_err(db2 - db20, b2r.grad) < 1e-3
     else:
         assert db1 is None and db2 is None
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout", [(8, 32, 64, 128), (16, 16, 128, 256), (32, 8, 256, 512),
+                                          (2, 16, 128, 256)])
+@pytest.mark.parametrize("cfg", [-1, 3, 7, 30])
+def test_dgrad_compact_s2_addend(C, N, H, Cin, Cout, cfg):
+    """Stride-2 dgrad with the projection shortcut's dX handed over compact ([N][H/2][W/2][Cin],
+    even-even pixels): equal to the same kernel with the expanded addend, for the halo stride-2
+    kernel, the parity igemm (split-K configs fall back to the expanded form) and the tuned choice;
+    plus the fused BN-reduce form."""
+    torch.manual_seed(11)
+    Ho = H // 2
+    dy = (torch.randn(N, Ho, Ho, Cout, device="cuda") * 0.5).bfloat16()
+    w = torch.randn(Cout, 3, 3, Cin, device="cuda") * 0.05
+    _, wt = C.weight_prep(w, 1, True)
+    comp = torch.randn(N, Ho, Ho, Cin, device="cuda").bfloat16()
+    full = torch.zeros(N, H, H, Cin, device="cuda").bfloat16()
+    full[:, ::2, ::2, :] = comp
+    C.set_conv_tile(0, cfg)
+    try:
+        ref = C.conv_dgrad(dy, wt, H, H, 2, 1, 1, full)
+        got = C.conv_dgrad(dy, wt, H, H, 2, 1, 1, comp, True)
+        assert torch.equal(got, ref)
+        y = torch.randn(N, H, H, Cin, device="cuda").bfloat16()
+        mask = torch.randint(0, 256, (y.numel() // 8,), device="cuda", dtype=torch.uint8)
+        aux = torch.cat([torch.randn(Cin, device="cuda") * 0.1, torch.rand(Cin, device="cuda") + 0.5])
+        r1, p1 = C.conv_dgrad_bn(dy, wt, H, H, 2, 1, 1, full, y, mask, aux)
+        r2, p2 = C.conv_dgrad_bn(dy, wt, H, H, 2, 1, 1, comp, y, mask, aux, addend_s2c=True)
+        assert torch.equal(r1, r2)
+        if p1.numel():
+            assert torch.allclose(p1.sum(0), p2.sum(0), rtol=1e-4, atol=1e-3)
+    finally:
+        C.set_conv_tile(0, -1)
