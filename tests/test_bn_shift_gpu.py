@@ -74,3 +74,34 @@ def test_shifted_stats(case, acc_form, det):
     tol2 = (2 * d.abs() * ya).sum(0) / 256 + 1e-4 * (d * d).sum(0) + 1e-2
     assert ((sk[0].double() - d.sum(0)).abs() <= tol1).all()
     assert ((sk[1].double() - (d * d).sum(0)).abs() <= tol2).all()
+
+
+def test_one_conv_output_two_bns_slab_path(monkeypatch):
+    """on the slab path a conv's sums carry a snapshot of the shift K they
+    were taken against, so two BNs finalizing the same conv output one after the other (the second
+    reading sums whose live pilot the first finalize has already overwritten) both get the right
+    batch mean / running mean. Accumulators disabled; three steps so the pilot is non-zero."""
+    import torch.nn.functional as TF
+
+    from pytorch_cifar_amd.nn import BatchNorm2d, Conv2d
+    from pytorch_cifar_amd.ops import functional as OF
+
+    monkeypatch.setattr(OF, "acc_enabled", lambda *a, **k: False)
+    torch.manual_seed(4)
+    conv = Conv2d(32, 64, 3, padding=1, bias=False).cuda()
+    bn_a, bn_b = BatchNorm2d(64).cuda(), BatchNorm2d(64).cuda()
+    ref_rm = torch.zeros(64, device="cuda")
+    ref_rv = torch.ones(64, device="cuda")
+    for step in range(3):
+        x = (torch.randn(16, 32, 8, 8, device="cuda") + 3.0).bfloat16().contiguous(memory_format=torch.channels_last)
+        with torch.no_grad():
+            y = conv(x)
+            a = bn_a(y, act="relu")
+            b = bn_b(y)
+            yf = y.float()
+            ref = TF.batch_norm(yf, ref_rm, ref_rv, None, None, True, 0.1, 1e-5)
+        assert (b.float() - ref).abs().max() < 5e-2, step
+        assert (a.float() - ref.clamp_min(0)).abs().max() < 5e-2, step
+    for bn in (bn_a, bn_b):
+        assert torch.allclose(bn.running_mean, ref_rm, rtol=1e-3, atol=1e-3)
+        assert torch.allclose(bn.running_var, ref_rv, rtol=1e-2, atol=1e-3)
