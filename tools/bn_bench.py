@@ -50,6 +50,8 @@ def main():
             ("copy (stock)", lambda: dst.copy_(y), 2 * T),
             ("copy_rows", lambda: C.copy_rows(y, dst), 2 * T),
             ("apply relu", lambda: C.bn_apply(y, aux, None, None, None, 1, True), 2 * T + T / 16),
+            ("apply relu no mask", lambda: C.bn_apply(y, aux, None, None, None, 1, False), 2 * T),
+            ("apply none", lambda: C.bn_apply(y, aux, None, None, None, 0, False), 2 * T),
             ("apply +res relu", lambda: C.bn_apply(y, aux, r, None, None, 1, True), 3 * T + T / 16),
             ("apply +bn2 relu", lambda: C.bn_apply(y, aux, None, r, aux, 1, True), 3 * T + T / 16),
             ("bwd relu", lambda: C.bn_backward(r, None, mask, y, aux, g, None, None, None, 1, True,
