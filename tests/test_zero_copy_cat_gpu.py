@@ -165,14 +165,16 @@ def test_densenet121_slab_trace(monkeypatch):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("level,stride", [(1, 1), (2, 2)])
-def test_simpledla_tree_slab_bitwise(level, stride, monkeypatch, deterministic):
+def test_simpledla_tree_slab_bitwise(level, stride, train, monkeypatch, deterministic):
     """SimpleDLA Tree with the zero-copy Root (children write their slab slices, the right child
     reads a dense copy) vs the copying concat: bitwise equal outputs, gradients, running stats."""
     from pytorch_cifar_amd.models.dla_simple import BasicBlock, Tree
 
     torch.manual_seed(0)
     m0 = Tree(BasicBlock, 32, 64, level=level, stride=stride).cuda().to(memory_format=torch.channels_last)
+    m0.train(train)
     m1 = copy.deepcopy(m0)
     x = torch.randn(8, 32, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     ho = (16 - 1) // stride + 1
@@ -187,8 +189,9 @@ def test_simpledla_tree_slab_bitwise(level, stride, monkeypatch, deterministic):
         assert torch.equal(a[3][n], b[3][n]), n
 
 
+@pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("level,stride", [(1, 2), (2, 2), (3, 1)])
-def test_dla_tree_slab_bitwise(level, stride, monkeypatch, deterministic):
+def test_dla_tree_slab_bitwise(level, stride, train, monkeypatch, deterministic):
     """DLA (paper-style) Tree with the zero-copy Root over level + 2 children vs the copying
     concat: bitwise equal."""
     from pytorch_cifar_amd.models.dla import BasicBlock, Tree
@@ -196,6 +199,7 @@ def test_dla_tree_slab_bitwise(level, stride, monkeypatch, deterministic):
     torch.manual_seed(0)
     cin = 32 if level < 3 else 64    # (level >= 3 chains level_i trees: reference needs cin == cout)
     m0 = Tree(BasicBlock, cin, 64, level=level, stride=stride).cuda().to(memory_format=torch.channels_last)
+    m0.train(train)
     m1 = copy.deepcopy(m0)
     x = torch.randn(8, cin, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     ho = (16 - 1) // stride + 1
@@ -226,3 +230,19 @@ def test_dla_step_has_no_concat_kernels(name, monkeypatch):
     names = {e.name for e in prof.events()}
     bad = [n for n in names if "cat_nhwc" in n or "split_nhwc" in n or "CatArray" in n]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["DenseNet121", "GoogLeNet", "DLA", "SimpleDLA"])
+def test_zero_copy_inference_matches_copying(name, monkeypatch):
+    """Eval mode under no_grad (the test loop of main.py): zero-copy and copying concat agree."""
+    from pytorch_cifar_amd import models
+
+    torch.manual_seed(0)
+    m = models.build_model(name).cuda().to(memory_format=torch.channels_last).eval()
+    x = torch.randn(8, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for z in ("1", "0"):
+        monkeypatch.setenv("PCA_ZERO_COPY_CAT", z)
+        with torch.no_grad():
+            outs.append(m(x).float())
+    assert torch.equal(outs[0], outs[1])
