@@ -99,6 +99,14 @@ __device__ __forceinline__ void stat_out(float* base, int row, int shards, size_
 
 // Row strides of the BatchNorm kernels' tensors (batchnorm.hip set_bn_ld; 0 = dense [M][C]):
 // y input, out forward output, dout / dx backward input / output (dx_acc: add into dx)
+// f where bit `bit` of the ReLU mask m is set, else +0: the bit is sign-extended into an
+// all-ones / zero word and ANDed with f's bits (v_bfe_i32 + v_and: one op fewer than a compare +
+// select per element in the fused BN-backward reduces)
+__device__ __forceinline__ float relu_bit(float f, uint32_t m, int bit) {
+  const int keep = ((int)(m << (31 - bit))) >> 31;
+  return __int_as_float(__float_as_int(f) & keep);
+}
+
 struct BnLd {
   int y, out, dout, dx, dx_acc;
 };

@@ -217,9 +217,9 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
         const uint32_t m = pre_m[mi];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
+          const float dz = relu_bit(f[e], m, e);
           bs1[e] += dz;
-          bs2[e] += dz * (yy[e] - bmean[e]) * bistd[e];
+          bs2[e] = fmaf(dz, yy[e] - bmean[e], bs2[e]);   // (x istd at the flush)
         }
       }
     }
@@ -351,6 +351,10 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
   }
 
   // ---- per-block channel sums: lanes of one 16-lane group share channels q*16 + e ----
+  if constexpr (DGRAD) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bs2[e] *= bistd[e];   // sum dz*(y - mean) -> sum dz*xhat
+  }
   if (STATS || bnf) {
     float* s1 = STATS ? st_s : bs1;
     float* s2 = STATS ? st_q : bs2;

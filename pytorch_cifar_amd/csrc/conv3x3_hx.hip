@@ -391,10 +391,10 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
           const uint32_t m = pre_m[mi];
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
+            const float dz = relu_bit(f[e], m, e);
             s1[e] += dz;
             const int c = ch_lane - nb0 + e;
-            s2[e] += dz * (yy[e] - auxs[c]) * auxs[BN + c];   // (aux of channel c % COUT)
+            s2[e] = fmaf(dz, yy[e] - auxs[c], s2[e]);   // (x istd at the flush; aux of c % COUT)
           }
           if constexpr (DUAL) {   // (y2 read here: no prefetch registers for it)
             const size_t o = out_pix(t, wm * 64 + mi * 16 + (lane & 15)) * g.COUT + co_lane;
@@ -402,9 +402,9 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
             unpack8(*reinterpret_cast<const uint4*>(g.bn_y2 + o + 8), yy + 8);
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-              const float dz = ((m >> e) & 1u) ? f[e] : 0.f;
+              const float dz = relu_bit(f[e], m, e);
               const int c = ch_lane - nb0 + e;
-              s3[e] += dz * (yy[e] - auxs[2 * BN + c]) * auxs[3 * BN + c];
+              s3[e] = fmaf(dz, yy[e] - auxs[2 * BN + c], s3[e]);   // (x istd2 at the flush)
             }
           }
         }
@@ -416,6 +416,16 @@ void conv3x3_hx_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Bw,
   }
 
   // ---- per-block channel sums: the 16 lanes of a group share channels; WM waves per column ----
+  if constexpr (DGRAD) {
+    if (bnf) {   // sums of dz * (y - mean) -> dz * xhat (istd of channel c, istd2 for the dual)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int c = ch_lane - nb0 + e;
+        s2[e] *= auxs[BN + c];
+        if constexpr (DUAL) s3[e] *= auxs[3 * BN + c];
+      }
+    }
+  }
   if (STATS || bnf) {
     constexpr int NSR = DUAL ? 3 : 2;             // sums per channel
 #pragma unroll

@@ -101,31 +101,29 @@ __device__ __forceinline__ void bn_fuse_acc(const uint4& v, const bf16* y, uint8
   }
 }
 
-// the same with y already in registers (the batched store loop of the igemm epilogue)
+// the same with y already in registers (the batched store loop of the igemm epilogue); s2
+// collects sum dz * (y - mean) — the per-channel istd is applied once at the flush
 __device__ __forceinline__ void bn_fuse_acc_v(const uint4& v, const uint4& yv, uint8_t m,
-                                              const float* mean, const float* istd, float* s1,
-                                              float* s2) {
+                                              const float* mean, float* s1, float* s2) {
   float f[8], yy[8];
   unpack8(v, f);
   unpack8(yv, yy);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
+    const float dz = relu_bit(f[q], m, q);
     s1[q] += dz;
-    s2[q] += dz * (yy[q] - mean[q]) * istd[q];
+    s2[q] = fmaf(dz, yy[q] - mean[q], s2[q]);
   }
 }
 
+// dual-BN third sum, sum dz * (y2 - mean2) (x istd2 at the flush)
 __device__ __forceinline__ void bn_fuse_acc3_v(const uint4& v, const uint4& y2v, uint8_t m,
-                                               const float* m2, const float* i2, float* s3) {
+                                               const float* m2, float* s3) {
   float f[8], yy[8];
   unpack8(v, f);
   unpack8(y2v, yy);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
-    s3[q] += dz * (yy[q] - m2[q]) * i2[q];
-  }
+  for (int q = 0; q < 8; ++q) s3[q] = fmaf(relu_bit(f[q], m, q), yy[q] - m2[q], s3[q]);
 }
 
 // dual-BN third sum from mean2 / istd2 already in LDS or registers (m2, i2: this vector's 8
@@ -711,14 +709,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         v = pack8(a);
       }
       const uint8_t m = e.ok ? e.mk : 0;
-      if (bnf) bn_fuse_acc_v(v, e.yv, m, bmean, bistd, bs1, bs2);
+      if (bnf) bn_fuse_acc_v(v, e.yv, m, bmean, bs1, bs2);
       if (dual) {
         if constexpr (AUX2_LDS) {
           const float* aux2s = reinterpret_cast<const float*>(smem + AUX2_OFF) + c8 * 8;
-          bn_fuse_acc3_v(v, e.y2v, m, aux2s, aux2s + BN, bs3);
+          bn_fuse_acc3_v(v, e.y2v, m, aux2s, bs3);
         } else {
           const float* a2 = g.bn_aux2 + grp * g.Cn + gc;
-          bn_fuse_acc3_v(v, e.y2v, m, a2, a2 + g.Co, bs3);
+          bn_fuse_acc3_v(v, e.y2v, m, a2, bs3);
         }
       }
       if (e.ok) *reinterpret_cast<uint4*>(Y + e.o) = v;
@@ -791,14 +789,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
           v = pack8(a);
         }
         const uint8_t m = ok[u] ? mk[u] : 0;   // (masked-off rows add nothing to the sums)
-        if (bnf) bn_fuse_acc_v(v, yv[u], m, bmean, bistd, bs1, bs2);
+        if (bnf) bn_fuse_acc_v(v, yv[u], m, bmean, bs1, bs2);
         if (dual) {
           if constexpr (AUX2_LDS) {
             const float* aux2s = reinterpret_cast<const float*>(smem + AUX2_OFF) + c8 * 8;
-            bn_fuse_acc3_v(v, y2v[u], m, aux2s, aux2s + BN, bs3);
+            bn_fuse_acc3_v(v, y2v[u], m, aux2s, bs3);
           } else {   // (configs whose LDS would cost occupancy: from global, L1-cached)
             const float* a2 = g.bn_aux2 + grp * g.Cn + gc;
-            bn_fuse_acc3_v(v, y2v[u], m, a2, a2 + g.Co, bs3);
+            bn_fuse_acc3_v(v, y2v[u], m, a2, bs3);
           }
         }
         if (ok[u]) *reinterpret_cast<uint4*>(Y + o[u]) = v;
@@ -808,6 +806,17 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
     __syncthreads();   // the C tile aliases the ring the next tile's prologue refills
     if constexpr (DGRAD && !SPLITK) {
       if (dual) {   // (epilogue-local: no accumulator registers live across the K loop)
+        // sum dz * (y2 - mean2) -> dz * xhat2: istd2 of this thread's 8 channels
+        // (the LDS aux2 tail is overwritten by the flush's reduction only after this read)
+        if (gc < g.Cn) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float i2;
+            if constexpr (AUX2_LDS) i2 = reinterpret_cast<const float*>(smem + AUX2_OFF)[BN + c8 * 8 + q];
+            else i2 = g.bn_aux2[g.Co + grp * g.Cn + gc + q];
+            bs3[q] *= i2;
+          }
+        }
         bn_flush_block<NT, CG_, 1>(reinterpret_cast<float*>(smem), bs3, grp * g.Cn + n0,
                                    g.Cn - n0, g.Co, g.bn_part, (int)blockIdx.x, g.shards, 3, 2);
         __syncthreads();
@@ -818,11 +827,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
   if constexpr (DGRAD && !SPLITK) {
     if (bnf) {   // slab row per (M-walker, parity class); channels of this block's N tile
       const int row = PARITY ? (int)blockIdx.x * 4 + cls : (int)blockIdx.x;
+      float bmean[8], bistd[8];
+      load_bn_aux(bmean, bistd);   // (sum dz * (y - mean) -> sum dz * xhat)
       float v[16];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         v[q] = bs1[q];
-        v[8 + q] = bs2[q];
+        v[8 + q] = bs2[q] * bistd[q];
       }
       bn_flush_block<NT, CG_, 2>(reinterpret_cast<float*>(smem), v, grp * g.Cn + n0, g.Cn - n0,
                                  g.Co, g.bn_part, row, g.shards, g.bn_y2 ? 3 : 2, 0);
