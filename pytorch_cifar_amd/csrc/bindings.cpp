@@ -173,7 +173,7 @@ struct CatArgs {
   int k;
 };
 void cat_nhwc_launch(const CatArgs&, bf16*, int, bool, hipStream_t);
-void interleave2_launch(bf16*, bf16*, bf16*, int, int, bool, hipStream_t);
+void interleave2_launch(bf16*, bf16*, bf16*, int, int, bool, hipStream_t, bf16* = nullptr);
 void chan_remap_launch(const void*, void*, bool, bool, const int*, const int*, int, int, int, int,
                        hipStream_t);
 void dpn_merge_fwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, hipStream_t);
@@ -1651,6 +1651,31 @@ std::vector<Tensor> deinterleave2(const Tensor& y) {
   return {a, b};
 }
 
+// split(shuffle(cat[a, b], 2)) into its channel halves [lo, hi] (each [N,H,W,C]) in one pass:
+// the ShuffleNetV2 join feeding the next block's SplitBlock; and its backward from [dlo, dhi]
+static void check_halves(const Tensor& a, const Tensor& b, const char* what) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  TORCH_CHECK(a.sizes() == b.sizes() && a.dim() == 4 && a.size(3) % 2 == 0, what,
+              ": equal NHWC shapes with an even channel count");
+}
+std::vector<Tensor> interleave2_split(const Tensor& a, const Tensor& b) {
+  check_halves(a, b, "interleave2_split");
+  const int P = a.size(0) * a.size(1) * a.size(2), C = a.size(3);
+  auto lo = at::empty_like(a), hi = at::empty_like(a);
+  pca::interleave2_launch(ptr<bf16>(a), ptr<bf16>(b), ptr<bf16>(lo), P, C, false, cur_stream(),
+                          ptr<bf16>(hi));
+  return {lo, hi};
+}
+std::vector<Tensor> deinterleave2_split(const Tensor& lo, const Tensor& hi) {
+  check_halves(lo, hi, "deinterleave2_split");
+  const int P = lo.size(0) * lo.size(1) * lo.size(2), C = lo.size(3);
+  auto a = at::empty_like(lo), b = at::empty_like(lo);
+  pca::interleave2_launch(ptr<bf16>(a), ptr<bf16>(b), const_cast<bf16*>(ptr<bf16>(lo)), P, C, true,
+                          cur_stream(), const_cast<bf16*>(ptr<bf16>(hi)));
+  return {a, b};
+}
+
 // DPN dual-path merge: x [N,H,W,Cx], o [N,H,W,Co] NHWC bf16 -> relu(cat[x[:d]+o[:d], x[d:], o[d:]])
 Tensor dpn_merge_fwd(const Tensor& x, const Tensor& o, int d) {
   check_bf16(x, "x");
@@ -2046,6 +2071,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("chan_remap", &chan_remap, py::arg("x"), py::arg("cmap"), py::arg("rmap") = py::none(),
         py::arg("K") = 1, py::arg("acc") = py::none());
   m.def("deinterleave2", &deinterleave2);
+  m.def("interleave2_split", &interleave2_split);
+  m.def("deinterleave2_split", &deinterleave2_split);
   m.def("split_nhwc", &split_nhwc);
   m.def("dpn_merge_bwd", &dpn_merge_bwd);
   m.def("act_fwd", &act_fwd);

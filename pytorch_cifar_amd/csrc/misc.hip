@@ -490,15 +490,25 @@ __device__ __forceinline__ void il_words(uint32_t ua, uint32_t ub, uint32_t& lo,
   hi = (ua >> 16) | (ub & 0xffff0000u);
 }
 
-template <int V, bool INV>
+// SPLIT: y is held as its two channel halves, y = [N,H,W,C] channels [0, C) and y1 = [C, 2C)
+// (the next ShuffleNetV2 block's SplitBlock halves, shufflenetv2.py:22-29, so the split is never
+// a pass of its own); needs C % (2V) == 0 so that no 2V-channel group straddles the halves.
+template <int V, bool INV, bool SPLIT = false>
 __global__ __launch_bounds__(256) void interleave2_kernel(bf16* __restrict__ a, bf16* __restrict__ b,
-                                                          bf16* __restrict__ y, int P, int C) {
+                                                          bf16* __restrict__ y0, int P, int C,
+                                                          bf16* __restrict__ y1 = nullptr) {
   const int G = C / V;
   const int total = P * G;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int gi = i % G, p = i / G;
     const size_t ia = (size_t)p * C + gi * V;         // element index in a / b
-    const size_t iy = (size_t)p * 2 * C + gi * 2 * V; // element index in y
+    size_t iy = (size_t)p * 2 * C + gi * 2 * V;       // element index in y
+    bf16* y = y0;
+    if constexpr (SPLIT) {
+      const int k = gi * 2 * V;                       // channel in the joined [0, 2C)
+      iy = (size_t)p * C + (k < C ? k : k - C);
+      if (k >= C) y = y1;
+    }
     if constexpr (V == 4) {
       if constexpr (!INV) {
         const uint2 va = *reinterpret_cast<const uint2*>(a + ia);
@@ -540,13 +550,21 @@ __global__ __launch_bounds__(256) void interleave2_kernel(bf16* __restrict__ a, 
   }
 }
 
-void interleave2_launch(bf16* a, bf16* b, bf16* y, int P, int C, bool inverse, hipStream_t st) {
-  const int V = C % 4 == 0 ? 4 : C % 2 == 0 ? 2 : 1;
+// y1 != nullptr: the joined tensor as two halves (y = channels [0, C), y1 = [C, 2C))
+void interleave2_launch(bf16* a, bf16* b, bf16* y, int P, int C, bool inverse, hipStream_t st,
+                        bf16* y1) {
+  const int V = y1 ? (C % 8 == 0 ? 4 : C % 4 == 0 ? 2 : 1) : (C % 4 == 0 ? 4 : C % 2 == 0 ? 2 : 1);
   const dim3 grid(grid_cap((size_t)P * C / V)), block(256);
 #define PCA_IL(VV)                                                                                  \
   if (V == VV) {                                                                                    \
-    if (inverse) hipLaunchKernelGGL((interleave2_kernel<VV, true>), grid, block, 0, st, a, b, y, P, C); \
-    else hipLaunchKernelGGL((interleave2_kernel<VV, false>), grid, block, 0, st, a, b, y, P, C);        \
+    if (y1 && inverse)                                                                              \
+      hipLaunchKernelGGL((interleave2_kernel<VV, true, true>), grid, block, 0, st, a, b, y, P, C, y1); \
+    else if (y1)                                                                                    \
+      hipLaunchKernelGGL((interleave2_kernel<VV, false, true>), grid, block, 0, st, a, b, y, P, C, y1); \
+    else if (inverse)                                                                               \
+      hipLaunchKernelGGL((interleave2_kernel<VV, true>), grid, block, 0, st, a, b, y, P, C, nullptr); \
+    else                                                                                            \
+      hipLaunchKernelGGL((interleave2_kernel<VV, false>), grid, block, 0, st, a, b, y, P, C, nullptr); \
     return;                                                                                         \
   }
   PCA_IL(4) PCA_IL(2) PCA_IL(1)

@@ -2,7 +2,14 @@
 
 Channel split -> (1x1 + BN + ReLU -> depthwise 3x3 + BN -> 1x1 + BN + ReLU) -> concat -> shuffle;
 two-branch stride-2 DownBlock. Odd widths (58/116/232 for net_size 1) fall back to the generic
-direct-conv and scalar depthwise kernels where the MFMA tile needs multiples of 8."""
+direct-conv and scalar depthwise kernels where the MFMA tile needs multiples of 8.
+
+Inside a stage the blocks hand each other the two SplitBlock halves instead of the joined
+tensor: every join but the stage's last is F.cat_shuffle2_split (one interleave pass writing
+both halves), so no split / concat pass runs between blocks (K22). Calling a block on its own
+keeps the reference contract (joined tensor in, joined tensor out)."""
+import os
+
 import torch.nn as tnn
 
 from ..nn import BatchNorm2d, Conv2d, Linear, Sequential
@@ -43,8 +50,17 @@ class BasicBlock(tnn.Module):
 
     def forward(self, x):
         x1, x2 = self.split(x)
+        return self._join(x1, self._branch(x2))
+
+    def _branch(self, x2):
         out = self.bn2(F.bn_act_dwconv(self.bn1, self.conv1(x2), "relu", self.conv2))
-        out = self.bn3(self.conv3(out), act="relu")
+        return self.bn3(self.conv3(out), act="relu")
+
+    def forward_halves(self, x1, x2, split_out=True):
+        """forward() on the SplitBlock halves; split_out: return the halves of the result."""
+        out = self._branch(x2)
+        if split_out and self.shuffle.groups == 2:
+            return F.cat_shuffle2_split(x1, out)
         return self._join(x1, out)
 
     def _join(self, a, b):
@@ -70,13 +86,50 @@ class DownBlock(tnn.Module):
         self.bn5 = BatchNorm2d(mid)
         self.shuffle = ShuffleBlock()
 
-    def forward(self, x):
+    def _branches(self, x):
         left = self.bn2(self.conv2(self.bn1(self.conv1(x))), act="relu")
         right = self.bn4(F.bn_act_dwconv(self.bn3, self.conv3(x), "relu", self.conv4))
-        right = self.bn5(self.conv5(right), act="relu")
+        return left, self.bn5(self.conv5(right), act="relu")
+
+    def forward(self, x):
+        left, right = self._branches(x)
         if self.shuffle.groups == 2 and left.shape == right.shape:
             return F.cat_shuffle2(left, right)
         return self.shuffle(F.cat([left, right], 1))
+
+    def forward_halves(self, x):
+        """forward() returned as the next block's SplitBlock halves."""
+        left, right = self._branches(x)
+        return F.cat_shuffle2_split(left, right)
+
+
+class _Stage(Sequential):
+    """_make_layer's Sequential (same state_dict keys) running its blocks on SplitBlock halves
+    (module docstring); falls back to block-by-block calls when a block carries hooks or a
+    split other than the reference's 0.5 / groups 2 / equal-width join."""
+
+    def _halves_ok(self):
+        if os.environ.get("PCA_ZERO_COPY_CAT", "1") == "0":
+            return False
+        blocks = list(self)
+        if len(blocks) < 2 or not isinstance(blocks[0], DownBlock):
+            return False
+        for b in blocks:
+            if b._forward_hooks or b._forward_pre_hooks or b.shuffle.groups != 2:
+                return False
+            if isinstance(b, BasicBlock) and b.split.ratio != 0.5:
+                return False
+        mid = blocks[0].conv2.out_channels
+        return all(b.conv1.in_channels == mid for b in blocks[1:])
+
+    def forward(self, x):
+        if not self._halves_ok():
+            return super().forward(x)
+        blocks = list(self)
+        h = blocks[0].forward_halves(x)
+        for i, b in enumerate(blocks[1:], 1):
+            h = b.forward_halves(*h, split_out=i < len(blocks) - 1)
+        return h
 
 
 class ShuffleNetV2(tnn.Module):
@@ -99,7 +152,7 @@ class ShuffleNetV2(tnn.Module):
         for _ in range(num_blocks):
             layers.append(BasicBlock(out_channels))
             self.in_channels = out_channels
-        return Sequential(*layers)
+        return _Stage(*layers)
 
     def forward(self, x):
         out = self.bn1(self.conv1(x), act="relu")

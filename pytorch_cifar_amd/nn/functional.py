@@ -14,6 +14,7 @@ from ..ops.functional import (  # noqa: F401
     bn_act_dwconv,
     cat,
     cat_shuffle2,
+    cat_shuffle2_split,
     channel_shuffle,
     cross_entropy,
     dense_copy,

@@ -2169,6 +2169,35 @@ def cat_shuffle2(a, b):
     return to_nchw(_Interleave2.apply(to_nhwc(a), to_nhwc(b)))
 
 
+class _Interleave2Split(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        lo, hi = _C().interleave2_split(a, b)
+        return lo, hi
+
+    @staticmethod
+    def backward(ctx, dlo, dhi):
+        ref = dlo if dlo is not None else dhi
+        dlo = dlo.contiguous() if dlo is not None else torch.zeros_like(ref)
+        dhi = dhi.contiguous() if dhi is not None else torch.zeros_like(ref)
+        da, db = _C().deinterleave2_split(dlo, dhi)
+        return da, db
+
+
+def cat_shuffle2_split(a, b):
+    """The two channel halves of channel_shuffle(cat([a, b], 1), 2) — a ShuffleNetV2 join followed
+    by the next block's SplitBlock (shufflenetv2.py:22-29, 49) — as ONE native interleave pass
+    writing both halves (backward: one pass reading both half-gradients): no concatenated
+    tensor is formed, and the split / concat passes of the two-step form disappear."""
+    if (_ref(a) or a.shape != b.shape or a.dtype != COMPUTE_DTYPE or b.dtype != COMPUTE_DTYPE
+            or a.dim() != 4 or a.shape[1] % 2):
+        y = cat_shuffle2(a, b)
+        c = y.shape[1] // 2
+        return y[:, :c], y[:, c:]
+    lo, hi = _Interleave2Split.apply(to_nhwc(a), to_nhwc(b))
+    return to_nchw(lo), to_nchw(hi)
+
+
 # ------------------------------------------------------------- zero-copy concatenation
 # SURVEY K22: a concatenation is a preallocated NHWC slab whose channel slices the producers
 # write directly (their BatchNorm+activation kernel takes the slice as a row-strided output:

@@ -246,3 +246,56 @@ def test_zero_copy_inference_matches_copying(name, monkeypatch):
         with torch.no_grad():
             outs.append(m(x).float())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("net_size", [0.5, 1])
+@pytest.mark.parametrize("train", [True, False])
+def test_shufflenetv2_halves_bitwise(net_size, train, monkeypatch, deterministic):
+    """ShuffleNetV2 stages handing blocks the SplitBlock halves (one interleave pass per join,
+    writing both halves) vs the block-by-block join + split: bitwise equal outputs, input and
+    parameter gradients, running statistics; and no split / concat kernel in the step."""
+    from pytorch_cifar_amd.models import ShuffleNetV2
+
+    torch.manual_seed(0)
+    m0 = ShuffleNetV2(net_size).cuda().to(memory_format=torch.channels_last)
+    m0.train(train)
+    m1 = copy.deepcopy(m0)
+    x = torch.randn(8, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(8, 10, device="cuda").to(torch.bfloat16)
+    a = _step(m0, x, g, True, monkeypatch)
+    b = _step(m1, x, g, False, monkeypatch)
+    assert torch.equal(a[0], b[0]), "forward"
+    assert torch.equal(a[1], b[1]), "input gradient"
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), n
+    for n in a[3]:
+        assert torch.equal(a[3][n], b[3][n]), n
+    monkeypatch.setenv("PCA_ZERO_COPY_CAT", "1")
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        m0(x.clone().requires_grad_(True)).backward(g)
+        torch.cuda.synchronize()
+    names = {e.name for e in prof.events()}
+    bad = [n for n in names if "cat_nhwc" in n or "split_nhwc" in n or "CatArray" in n]
+    assert not bad, bad
+
+
+def test_interleave2_split_matches_reference():
+    """cat_shuffle2_split == the halves of channel_shuffle(cat([a, b]), 2), forward and backward,
+    for vector widths 4 / 2 / 1 (C % 8, C % 4, C % 2)."""
+    from pytorch_cifar_amd.nn import functional as F
+
+    for c in (24, 12, 58, 6):
+        a = torch.randn(4, c, 5, 3, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        b = torch.randn_like(a).contiguous(memory_format=torch.channels_last)
+        a.requires_grad_(True)
+        b.requires_grad_(True)
+        lo, hi = F.cat_shuffle2_split(a, b)
+        y = torch.stack([a.detach(), b.detach()], 2).reshape(4, 2 * c, 5, 3)
+        assert torch.equal(lo.float(), y[:, :c].float()), c
+        assert torch.equal(hi.float(), y[:, c:].float()), c
+        dlo = torch.randn_like(lo)
+        dhi = torch.randn_like(hi)
+        (lo.float() * dlo.float()).sum().add((hi.float() * dhi.float()).sum()).backward()
+        dy = torch.cat([dlo, dhi], 1).reshape(4, c, 2, 5, 3)
+        assert torch.equal(a.grad.float(), dy[:, :, 0].float()), c
+        assert torch.equal(b.grad.float(), dy[:, :, 1].float()), c
