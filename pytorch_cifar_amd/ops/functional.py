@@ -280,7 +280,11 @@ class WeightPrepPlan:
         return None
 
     def register(self, w, groups, w_phys):
-        if isinstance(groups, tuple):
+        if isinstance(groups, tuple) and groups[0] == "gpad":
+            # per-group zero-padded operands (odd-width grouped / narrow convs): w_phys is the
+            # padded fp32 weight [G*op][KH][KW][cp], converted now (first sight)
+            wb, wt = _C().weight_prep(w_phys, groups[1], True)
+        elif isinstance(groups, tuple):
             # ("pad", Cp): forward-only bf16 copy with channels zero-padded to Cp (stem convs)
             co, cg, kh, kw = w.shape
             wb = torch.empty((co, kh, kw, groups[1]), dtype=COMPUTE_DTYPE, device=w.device)
@@ -305,6 +309,13 @@ class WeightPrepPlan:
             wp = G.physical(e.w)
             Cout, KH, KW, Cg = wp.shape
             n = wp.numel()
+            if isinstance(e.groups, tuple) and e.groups[0] == "gpad":
+                _, g, cout_g, op, cg, cp = e.groups
+                desc.append([wp.data_ptr(), e.wb.data_ptr(), e.wt.data_ptr(), g, op, KH * KW, cp,
+                             (cout_g << 32) | cg])
+                tiles = g * KH * KW * ((op + 63) // 64) * ((cp + 63) // 64)
+                chunks += [[t, k, 0, 5] for k in range(tiles)]
+                continue
             if isinstance(e.groups, tuple):
                 cp = e.groups[1]
                 rows = Cout * KH * KW
@@ -620,8 +631,11 @@ class _ConvMFMA(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, groups, want_stats, cin_pad, slot=None,
-                owner=False, bnsrc=None, acc=None, pilot=None):
+                owner=False, bnsrc=None, acc=None, pilot=None, padded=None):
+        # padded = (wb, wt, remap): operands of the per-group zero-padded form of ``weight``
+        # (_conv_group_padded, from the plan); the weight gradient is gathered back by ``remap``
         C = _C()
+        ctx.padded = padded[2] if padded is not None else None
         ctx.slot, ctx.owner = slot, owner
         ctx.bnsrc = bnsrc
         if slot is not None and owner:
@@ -646,6 +660,8 @@ class _ConvMFMA(torch.autograd.Function):
             if wb is None:
                 w_phys = F.pad(w_phys, (0, cin_pad - w_phys.shape[-1]))
                 wb, wt = C.weight_prep(w_phys, groups, need_dx)
+        elif padded is not None:
+            wb, wt = padded[0], padded[1]
         else:
             wb, wt = _prepped_weight(weight, groups, w_phys, need_dx)
         if not want_stats:
@@ -678,7 +694,7 @@ class _ConvMFMA(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return (None,) * 13
+            return (None,) * 14
         C = _C()
         x, wt = ctx.saved_tensors
         stride, padding, groups, cin_pad, H, W = ctx.geom
@@ -727,6 +743,17 @@ class _ConvMFMA(torch.autograd.Function):
             if sbuf is not None and C.stem_wgrad(x, dy, stride, padding, sbuf):
                 G.fire(weight)
                 weight = None
+        if weight is not None and weight.requires_grad and ctx.padded is not None:
+            # padded-form dW [G*op][KH][KW][cp], its real entries gathered into the arena
+            dw = C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, None)
+            buf = G.grad_buffer(weight)
+            phys = G.physical(weight).shape
+            if buf is not None and tuple(buf.shape) == tuple(phys):
+                ctx.padded.apply(dw, inverse=True, acc=buf)
+                G.fire(weight)
+            else:
+                G.accumulate(weight, ctx.padded.apply(dw, inverse=True).view(phys))
+            weight = None
         if weight is not None and weight.requires_grad:
             buf = None if (cin_pad or not weight.is_leaf) else G.grad_buffer(weight)
             side = wgrad_stream(x.device) if buf is not None else None
@@ -762,7 +789,7 @@ class _ConvMFMA(torch.autograd.Function):
                     G.accumulate(bias, db)
                 else:
                     db_ret = db
-        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None, None, None
+        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _ConvDirect(torch.autograd.Function):
@@ -1052,17 +1079,32 @@ def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
     N, H, W, _ = xn.shape
     if cp != Cg:
         xn = _RemapFn.apply(xn, _group_pad_remap(groups, Cg, cp), (N, H, W, groups * cp), None)
-    # weight [Cout, Cg, KH, KW] -> [G*op, cp, KH, KW], channels_last (the MFMA B layout)
+    # weight [Cout, Cg, KH, KW] -> [G*op, cp, KH, KW], channels_last (the MFMA B layout): with a
+    # plan, the padded bf16 operands are written by its batched launch (or the fused optimizer
+    # step) straight from the master — no per-step fp32 remap + convert
+    padded = None
     if cp != Cg or op != cout_g:
         wr = _weight_pad_remap(groups, cout_g, op, Cg, cp, KH * KW)
-        wp = to_nchw(_remap_param(weight, wr, (groups * op, KH, KW, cp)))
+        plan = _PLAN["cur"]
+        if (plan is not None and weight.is_leaf and weight.dtype == torch.float32
+                and weight.permute(0, 2, 3, 1).is_contiguous()):
+            key = ("gpad", groups, cout_g, op, Cg, cp)
+            e = plan.lookup(weight, key)
+            if e is None:
+                e = plan.register(weight, key, wr.apply(G.physical(weight).detach())
+                                  .view(groups * op, KH, KW, cp))
+            padded = (e.wb, e.wt, wr)
+            wp = weight
+        else:
+            wp = to_nchw(_remap_param(weight, wr, (groups * op, KH, KW, cp)))
     else:
         wp = weight
     bp = None
     if bias is not None:
         bp = bias if op == cout_g else _remap_param(bias, _group_pad_remap(groups, cout_g, op),
                                                     (groups * op,))
-    y, stats = _ConvMFMA.apply(xn, wp, bp, stride, padding, groups, want_stats, 0)
+    y, stats = _ConvMFMA.apply(xn, wp, bp, stride, padding, groups, want_stats, 0, None, False,
+                               None, None, None, padded)
     if op != cout_g:
         Ho, Wo = y.shape[1], y.shape[2]
         unpad = _group_unpad_remap(groups, cout_g, op)

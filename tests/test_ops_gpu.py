@@ -610,3 +610,45 @@ def test_noact_bn_fusion_matches_separate_reduce(stride, monkeypatch):
     bad = [(n, round(e, 4), round(res[False][1][n], 4)) for n, e in res[True][1].items()
            if e > 1.5 * res[False][1][n] + 2e-2]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["ShuffleNetV2_1", "ShuffleNetG2", "PNASNetA"])
+def test_group_padded_plan_operands_match_remap(name):
+    """Odd-width convs under a WeightPrepPlan get their zero-padded bf16 operands from the plan's
+    batched launch (weight_prep pass 5, straight from the fp32 master) instead of a per-step fp32
+    remap + convert: outputs and every gradient bitwise equal to the remap path."""
+    import copy
+
+    import pytorch_cifar_amd as pca
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.ops.functional import enable_batched_weight_prep
+
+    pca.set_deterministic(True)
+    try:
+        torch.manual_seed(0)
+        a = models.MODEL_REGISTRY[name]().cuda().to(memory_format=torch.channels_last)
+        b = copy.deepcopy(a)
+        enable_batched_weight_prep(b)
+        x = torch.randn(8, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        g = torch.randn(8, 10, device="cuda").to(torch.bfloat16)
+        outs = []
+        # three calls each, compared call by call (a call's BN statistics are shifted by the
+        # previous call's batch mean, so call i of one model matches call i of the other);
+        # b: the registration step, then the plan's batched refreshes
+        for m in (a, a, a, b, b, b):
+            m.zero_grad(set_to_none=True)
+            y = m(x.clone().requires_grad_(True))
+            y.backward(g)
+            torch.cuda.synchronize()
+            outs.append((y.detach().float(), {n: p.grad.clone() for n, p in m.named_parameters()
+                                              if p.grad is not None}))
+        plan = b.__dict__["_pca_wplan"]
+        assert any(isinstance(e.groups, tuple) and e.groups[0] == "gpad" for e in plan.entries)
+        for i in range(3):
+            o, r = outs[3 + i], outs[i]
+            assert torch.equal(o[0], r[0]), ("forward", i)
+            assert o[1].keys() == r[1].keys()
+            for n in o[1]:
+                assert torch.equal(o[1][n], r[1][n]), (n, i)
+    finally:
+        pca.set_deterministic(False)
