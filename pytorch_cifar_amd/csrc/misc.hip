@@ -1390,7 +1390,11 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, int G, int Cn, i
 //   pass 5: pass 4 for a per-group zero-padded operand (odd-width grouped / narrow convs): the
 //           operands are [G*Cn][T][Cr] with Cn, Cr the padded widths, the master [G*mCn][T][mCr]
 //           with desc numel slot = mCn << 32 | mCr; padded positions read nothing (each master
-//           element is still read, and in the fused optimizer updated, exactly once).
+//           element is still read, and in the fused optimizer updated, exactly once);
+//   pass 6: pass 4 for a block-diagonal super-group operand (narrow groups run as one group of
+//           S = P x Cg channels): operand [G'*Cn][T][S], master [G'*Cn][T][Cg] with numel slot =
+//           cout_g << 32 | Cg; output row r belongs to original group r / cout_g, whose Cg
+//           channels sit at [lg*Cg, (lg+1)*Cg) of the S, lg = (r / cout_g) % P (zeros elsewhere).
 // All index math is 32-bit and per block / per 8 elements (64-bit div/mod per element made the
 // first version of this kernel 10x slower than its bandwidth).
 // UPD: the fused optimizer form — every master element is read exactly once by the chunk plan,
@@ -1452,8 +1456,8 @@ __device__ __forceinline__ void prep_chunk(const int64_t* __restrict__ desc,
   }
   bf16* wt = reinterpret_cast<bf16*>(d[2]);
   bf16* wbt = ch[3] >= 4 ? reinterpret_cast<bf16*>(d[1]) : nullptr;   // pass 4/5: + forward copy
-  const int mCn = ch[3] == 5 ? (int)(d[7] >> 32) : Cn;               // master widths
-  const int mCr = ch[3] == 5 ? (int)(d[7] & 0xffffffff) : Cr;
+  const int mCn = ch[3] >= 5 ? (int)(d[7] >> 32) : Cn;               // master widths
+  const int mCr = ch[3] >= 5 ? (int)(d[7] & 0xffffffff) : Cr;
   const int nco = (Cn + 63) >> 6, nci = (Cr + 63) >> 6;
   int q = (int)ch[1];
   const int ci_t = q % nci;
@@ -1466,7 +1470,13 @@ __device__ __forceinline__ void prep_chunk(const int64_t* __restrict__ desc,
   for (int k = tid; k < 64 * 64; k += 256) {
     const int r = k >> 6, c = k & 63;               // r: co, c: ci (contiguous in w)
     const int co = co0 + r, ci = ci0 + c;
-    tile[r][c] = (co < mCn && ci < mCr) ? ld(((g * mCn + co) * T + tap) * mCr + ci) : 0.f;
+    if (ch[3] == 6) {   // block diagonal: mCn = cout_g, mCr = Cg
+      const int row = g * Cn + co, lg = (row / mCn) % (Cr / mCr), c_lo = lg * mCr;
+      tile[r][c] = (co < Cn && ci >= c_lo && ci < c_lo + mCr)
+                       ? ld((row * T + tap) * mCr + ci - c_lo) : 0.f;
+    } else {
+      tile[r][c] = (co < mCn && ci < mCr) ? ld(((g * mCn + co) * T + tap) * mCr + ci) : 0.f;
+    }
   }
   __syncthreads();
   if (wbt) {   // forward copy of the tile: 8 consecutive ci per thread, 16-byte stores

@@ -280,7 +280,7 @@ class WeightPrepPlan:
         return None
 
     def register(self, w, groups, w_phys):
-        if isinstance(groups, tuple) and groups[0] == "gpad":
+        if isinstance(groups, tuple) and groups[0] in ("gpad", "gdense"):
             # per-group zero-padded operands (odd-width grouped / narrow convs): w_phys is the
             # padded fp32 weight [G*op][KH][KW][cp], converted now (first sight)
             wb, wt = _C().weight_prep(w_phys, groups[1], True)
@@ -315,6 +315,14 @@ class WeightPrepPlan:
                              (cout_g << 32) | cg])
                 tiles = g * KH * KW * ((op + 63) // 64) * ((cp + 63) // 64)
                 chunks += [[t, k, 0, 5] for k in range(tiles)]
+                continue
+            if isinstance(e.groups, tuple) and e.groups[0] == "gdense":
+                _, g, cout_g, cg, S = e.groups
+                cn = Cout // g
+                desc.append([wp.data_ptr(), e.wb.data_ptr(), e.wt.data_ptr(), g, cn, KH * KW, S,
+                             (cout_g << 32) | cg])
+                tiles = g * KH * KW * ((cn + 63) // 64) * ((S + 63) // 64)
+                chunks += [[t, k, 0, 6] for k in range(tiles)]
                 continue
             if isinstance(e.groups, tuple):
                 cp = e.groups[1]
@@ -748,8 +756,11 @@ class _ConvMFMA(torch.autograd.Function):
             dw = C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, None)
             buf = G.grad_buffer(weight)
             phys = G.physical(weight).shape
+            flat = ctx.padded.flat
+            if flat:
+                dw = dw.reshape(-1)
             if buf is not None and tuple(buf.shape) == tuple(phys):
-                ctx.padded.apply(dw, inverse=True, acc=buf)
+                ctx.padded.apply(dw, inverse=True, acc=buf.view(-1) if flat else buf)
                 G.fire(weight)
             else:
                 G.accumulate(weight, ctx.padded.apply(dw, inverse=True).view(phys))
@@ -1034,11 +1045,25 @@ def _conv_group_dense(x, weight, bias, stride, padding, groups, S, want_stats, a
     Cout, Cg, KH, KW = weight.shape
     Cin = x.shape[1]
     remap = _group_dense_remap(Cout, Cout // groups, Cg, S, KH * KW)
-    wp = to_nchw(_remap_param(weight, remap, (Cout, KH, KW, S)))
+    plan = _PLAN["cur"]
+    padded = None
+    if (plan is not None and weight.is_leaf and weight.dtype == torch.float32
+            and weight.permute(0, 2, 3, 1).is_contiguous()):
+        # block-diagonal bf16 operands written by the plan's batched launch / the fused
+        # optimizer (weight_prep pass 6) from the master: no per-step expansion + convert
+        key = ("gdense", Cin // S, Cout // groups, Cg, S)
+        e = plan.lookup(weight, key)
+        if e is None:
+            e = plan.register(weight, key, remap.apply(G.physical(weight).detach().reshape(-1))
+                              .view(Cout, KH, KW, S))
+        padded = (e.wb, e.wt, remap)
+        wp = weight
+    else:
+        wp = to_nchw(_remap_param(weight, remap, (Cout, KH, KW, S)))
     slot, owner = _slot_for_conv(x)
     bnsrc = getattr(x, "_pca_bnsrc", None) if x.requires_grad else None
     y, stats = _ConvMFMA.apply(to_nhwc(x), wp, bias, stride, padding, Cin // S, want_stats, 0,
-                               slot, owner, bnsrc, acc if want_stats else None, pilot)
+                               slot, owner, bnsrc, acc if want_stats else None, pilot, padded)
     if want_stats and acc is not None:
         return to_nchw(y), acc
     return to_nchw(y), (stats if want_stats else None)

@@ -96,12 +96,14 @@ def test_fused_sgd_operands_are_current():
     assert checked > 10
 
 
-def test_fused_sgd_prep_padded_operands(deterministic):
-    """The fused optimizer step also writes the zero-padded operands of odd-width convs (pass 5):
-    bitwise equal to the unfused pipeline."""
-    net_u, ar_u, l_u, _ = _run("ShuffleNetV2_1", False, False)
-    net_f, ar_f, l_f, plan = _run("ShuffleNetV2_1", True, False)
-    assert any(isinstance(e.groups, tuple) and e.groups[0] == "gpad" for e in plan.entries)
+@pytest.mark.parametrize("name,kind", [("ShuffleNetV2_1", "gpad"), ("DPN26", "gdense")])
+def test_fused_sgd_prep_padded_operands(deterministic, name, kind):
+    """The fused optimizer step also writes the zero-padded operands of odd-width convs (pass 5)
+    and the block-diagonal ones of narrow-group convs (pass 6): bitwise equal to the unfused
+    pipeline."""
+    net_u, ar_u, l_u, _ = _run(name, False, False)
+    net_f, ar_f, l_f, plan = _run(name, True, False)
+    assert any(isinstance(e.groups, tuple) and e.groups[0] == kind for e in plan.entries)
     assert l_f == l_u, (l_f, l_u)
     assert torch.equal(ar_f.param_flat, ar_u.param_flat)
     assert torch.equal(ar_f.mom_flat, ar_u.mom_flat)

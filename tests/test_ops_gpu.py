@@ -612,11 +612,14 @@ def test_noact_bn_fusion_matches_separate_reduce(stride, monkeypatch):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("name", ["ShuffleNetV2_1", "ShuffleNetG2", "PNASNetA"])
-def test_group_padded_plan_operands_match_remap(name):
-    """Odd-width convs under a WeightPrepPlan get their zero-padded bf16 operands from the plan's
-    batched launch (weight_prep pass 5, straight from the fp32 master) instead of a per-step fp32
-    remap + convert: outputs and every gradient bitwise equal to the remap path."""
+@pytest.mark.parametrize("name,kind", [("ShuffleNetV2_1", "gpad"), ("ShuffleNetG2", "gpad"),
+                                       ("PNASNetA", "gpad"), ("DPN26", "gdense"),
+                                       ("ResNeXt29_32x4d", "gdense")])
+def test_group_padded_plan_operands_match_remap(name, kind):
+    """Odd-width convs (gpad) and narrow-group super-group convs (gdense) under a WeightPrepPlan
+    get their zero-padded / block-diagonal bf16 operands from the plan's batched launch
+    (weight_prep pass 5 / 6, straight from the fp32 master) instead of a per-step fp32 remap +
+    convert: outputs and every gradient bitwise equal to the remap path."""
     import copy
 
     import pytorch_cifar_amd as pca
@@ -643,7 +646,7 @@ def test_group_padded_plan_operands_match_remap(name):
             outs.append((y.detach().float(), {n: p.grad.clone() for n, p in m.named_parameters()
                                               if p.grad is not None}))
         plan = b.__dict__["_pca_wplan"]
-        assert any(isinstance(e.groups, tuple) and e.groups[0] == "gpad" for e in plan.entries)
+        assert any(isinstance(e.groups, tuple) and e.groups[0] == kind for e in plan.entries)
         for i in range(3):
             o, r = outs[3 + i], outs[i]
             assert torch.equal(o[0], r[0]), ("forward", i)
