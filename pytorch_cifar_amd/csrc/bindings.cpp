@@ -175,7 +175,7 @@ struct CatArgs {
 void cat_nhwc_launch(const CatArgs&, bf16*, int, bool, hipStream_t);
 void interleave2_launch(bf16*, bf16*, bf16*, int, int, bool, hipStream_t, bf16* = nullptr);
 void chan_remap_launch(const void*, void*, bool, bool, const int*, const int*, int, int, int, int,
-                       hipStream_t);
+                       hipStream_t, bool = false);
 void dpn_merge_fwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, hipStream_t);
 void dpn_merge_bwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, bf16*, hipStream_t);
 void se_scale_bwd_launch(const bf16*, const bf16*, const float*, int, int, int, bf16*, float*,
@@ -1599,10 +1599,11 @@ std::vector<Tensor> split_nhwc(const Tensor& whole, const std::vector<int64_t>& 
 // (Cin = last dim), out [Q, J] with Q = rmap.numel() * K (outer row map) or rows; `acc` (fp32)
 // is added into instead of allocating the output.
 Tensor chan_remap(const Tensor& x, const Tensor& cmap, const optional<Tensor>& rmap, int64_t K,
-                  const optional<Tensor>& acc) {
+                  const optional<Tensor>& acc, bool clear_src) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "chan_remap: contiguous GPU input");
   const bool fp32 = x.scalar_type() == at::kFloat;
   TORCH_CHECK(fp32 || x.scalar_type() == at::kBFloat16, "chan_remap: bf16 or fp32");
+  TORCH_CHECK(!clear_src || fp32, "chan_remap: clear_src is for fp32 gradient buffers");
   TORCH_CHECK(cmap.scalar_type() == at::kInt && cmap.is_cuda() && cmap.dim() == 1, "chan_remap: int32 cmap");
   const int64_t Cin = x.size(-1);
   const int64_t rows = Cin ? x.numel() / Cin : 0;
@@ -1625,7 +1626,8 @@ Tensor chan_remap(const Tensor& x, const Tensor& cmap, const optional<Tensor>& r
   }
   if (Q > 0)
     pca::chan_remap_launch(x.data_ptr(), out.data_ptr(), fp32, acc.has_value() && acc->defined(),
-                           ptr<int>(cmap), rm, (int)Q, (int)(rm ? K : 1), (int)Cin, (int)J, cur_stream());
+                           ptr<int>(cmap), rm, (int)Q, (int)(rm ? K : 1), (int)Cin, (int)J, cur_stream(),
+                           clear_src);
   return out;
 }
 
@@ -2069,7 +2071,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cat_nhwc", &cat_nhwc);
   m.def("interleave2", &interleave2);
   m.def("chan_remap", &chan_remap, py::arg("x"), py::arg("cmap"), py::arg("rmap") = py::none(),
-        py::arg("K") = 1, py::arg("acc") = py::none());
+        py::arg("K") = 1, py::arg("acc") = py::none(), py::arg("clear_src") = false);
   m.def("deinterleave2", &deinterleave2);
   m.def("interleave2_split", &interleave2_split);
   m.def("deinterleave2_split", &deinterleave2_split);

@@ -2126,8 +2126,10 @@ void weight_prep_launch(const float* w, int G, int Cn, int T, int Cr, bf16* wb, 
 // remap with the inverse maps. ACC adds into `out` (fp32 parameter gradients in the arena).
 // The channel map is staged in LDS once per block; each thread writes V consecutive output
 // channels with one vector store (the gathered reads hit the same input row, L1/L2-resident).
-template <typename T, int V, bool ACC>
-__global__ __launch_bounds__(256) void chan_remap_kernel(const T* __restrict__ in, T* __restrict__ out,
+// CLR zeroes every input element it reads (an injective map reads each at most once): a
+// persistent padded weight-gradient buffer is handed back clean for the next accumulation.
+template <typename T, int V, bool ACC, bool CLR = false>
+__global__ __launch_bounds__(256) void chan_remap_kernel(T* __restrict__ in, T* __restrict__ out,
                                                          const int* __restrict__ cmap,
                                                          const int* __restrict__ rmap, int Q, int K,
                                                          int Cin, int J, int map_in_lds) {
@@ -2150,12 +2152,15 @@ __global__ __launch_bounds__(256) void chan_remap_kernel(const T* __restrict__ i
       const int s = rmap[r];
       srow = s < 0 ? -1 : (int64_t)s * K + (q - r * K);
     }
-    const T* row = in + srow * Cin;
+    T* row = in + srow * Cin;
     Vec o;
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       const int c = mp[gi * V + u];
       o.v[u] = (srow >= 0 && c >= 0) ? row[c] : T(0.f);
+      if constexpr (CLR) {
+        if (srow >= 0 && c >= 0) row[c] = T(0.f);
+      }
     }
     Vec* dst = reinterpret_cast<Vec*>(out + (int64_t)q * J + gi * V);
     if constexpr (ACC) {
@@ -2235,10 +2240,10 @@ static bool chan_remap_rows(const T* in, T* out, const int* cmap, int Q, int Cin
   return false;
 }
 
-template <typename T, bool ACC>
-static void chan_remap_dispatch(const T* in, T* out, const int* cmap, const int* rmap, int Q, int K,
+template <typename T, bool ACC, bool CLR = false>
+static void chan_remap_dispatch(T* in, T* out, const int* cmap, const int* rmap, int Q, int K,
                                 int Cin, int J, hipStream_t st) {
-  if constexpr (!ACC) {
+  if constexpr (!ACC && !CLR) {
     if (!rmap && chan_remap_rows<T>(in, out, cmap, Q, Cin, J, st)) return;
   }
   constexpr int VMAX = 16 / sizeof(T);
@@ -2249,7 +2254,7 @@ static void chan_remap_dispatch(const T* in, T* out, const int* cmap, const int*
   const dim3 grid(grid_cap((size_t)Q * (J / V))), block(256);
 #define PCA_REMAP(VV)                                                                           \
   if (V == VV) {                                                                                \
-    hipLaunchKernelGGL((chan_remap_kernel<T, VV, ACC>), grid, block, lds, st, in, out, cmap, rmap, \
+    hipLaunchKernelGGL((chan_remap_kernel<T, VV, ACC, CLR>), grid, block, lds, st, in, out, cmap, rmap, \
                        Q, K, Cin, J, lds_ok);                                                   \
     return;                                                                                     \
   }
@@ -2259,14 +2264,22 @@ static void chan_remap_dispatch(const T* in, T* out, const int* cmap, const int*
 }
 
 void chan_remap_launch(const void* in, void* out, bool fp32, bool accumulate, const int* cmap,
-                       const int* rmap, int Q, int K, int Cin, int J, hipStream_t st) {
+                       const int* rmap, int Q, int K, int Cin, int J, hipStream_t st,
+                       bool clear_src) {
+  // (the kernels take a mutable source for the clearing form; the others only read it)
   if (fp32) {
-    if (accumulate)
-      chan_remap_dispatch<float, true>((const float*)in, (float*)out, cmap, rmap, Q, K, Cin, J, st);
+    float* i = const_cast<float*>(static_cast<const float*>(in));
+    if (accumulate && clear_src)
+      chan_remap_dispatch<float, true, true>(i, (float*)out, cmap, rmap, Q, K, Cin, J, st);
+    else if (accumulate)
+      chan_remap_dispatch<float, true>(i, (float*)out, cmap, rmap, Q, K, Cin, J, st);
+    else if (clear_src)
+      chan_remap_dispatch<float, false, true>(i, (float*)out, cmap, rmap, Q, K, Cin, J, st);
     else
-      chan_remap_dispatch<float, false>((const float*)in, (float*)out, cmap, rmap, Q, K, Cin, J, st);
+      chan_remap_dispatch<float, false>(i, (float*)out, cmap, rmap, Q, K, Cin, J, st);
   } else {
-    chan_remap_dispatch<bf16, false>((const bf16*)in, (bf16*)out, cmap, rmap, Q, K, Cin, J, st);
+    chan_remap_dispatch<bf16, false>(const_cast<bf16*>(static_cast<const bf16*>(in)), (bf16*)out,
+                                     cmap, rmap, Q, K, Cin, J, st);
   }
 }
 

@@ -227,10 +227,11 @@ _PREP_CHUNK = int(os.environ.get("PCA_PREP_CHUNK", "4096"))   # fp32 elements pe
 
 
 class _PrepEntry:
-    __slots__ = ("w", "groups", "wb", "wt")
+    __slots__ = ("w", "groups", "wb", "wt", "dwbuf")
 
     def __init__(self, w, groups, wb, wt):
         self.w, self.groups, self.wb, self.wt = w, groups, wb, wt
+        self.dwbuf = None     # zero-padded convs: persistent padded weight-gradient accumulator
 
 
 class WeightPrepPlan:
@@ -643,7 +644,7 @@ class _ConvMFMA(torch.autograd.Function):
         # padded = (wb, wt, remap): operands of the per-group zero-padded form of ``weight``
         # (_conv_group_padded, from the plan); the weight gradient is gathered back by ``remap``
         C = _C()
-        ctx.padded = padded[2] if padded is not None else None
+        ctx.padded = padded[2:] if padded is not None else None
         ctx.slot, ctx.owner = slot, owner
         ctx.bnsrc = bnsrc
         if slot is not None and owner:
@@ -753,17 +754,19 @@ class _ConvMFMA(torch.autograd.Function):
                 weight = None
         if weight is not None and weight.requires_grad and ctx.padded is not None:
             # padded-form dW [G*op][KH][KW][cp], its real entries gathered into the arena
-            dw = C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, None)
+            remap, dwbuf = ctx.padded
+            dw = C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, dwbuf)
+            clear = dwbuf is not None
             buf = G.grad_buffer(weight)
             phys = G.physical(weight).shape
-            flat = ctx.padded.flat
+            flat = remap.flat
             if flat:
                 dw = dw.reshape(-1)
             if buf is not None and tuple(buf.shape) == tuple(phys):
-                ctx.padded.apply(dw, inverse=True, acc=buf.view(-1) if flat else buf)
+                remap.apply(dw, inverse=True, acc=buf.view(-1) if flat else buf, clear_src=clear)
                 G.fire(weight)
             else:
-                G.accumulate(weight, ctx.padded.apply(dw, inverse=True).view(phys))
+                G.accumulate(weight, remap.apply(dw, inverse=True, clear_src=clear).view(phys))
             weight = None
         if weight is not None and weight.requires_grad:
             buf = None if (cin_pad or not weight.is_leaf) else G.grad_buffer(weight)
@@ -1056,7 +1059,7 @@ def _conv_group_dense(x, weight, bias, stride, padding, groups, S, want_stats, a
         if e is None:
             e = plan.register(weight, key, remap.apply(G.physical(weight).detach().reshape(-1))
                               .view(Cout, KH, KW, S))
-        padded = (e.wb, e.wt, remap)
+        padded = (e.wb, e.wt, remap, None)
         wp = weight
     else:
         wp = to_nchw(_remap_param(weight, remap, (Cout, KH, KW, S)))
@@ -1118,7 +1121,13 @@ def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
             if e is None:
                 e = plan.register(weight, key, wr.apply(G.physical(weight).detach())
                                   .view(groups * op, KH, KW, cp))
-            padded = (e.wb, e.wt, wr)
+            if e.dwbuf is None:
+                # the padded dW accumulates here and the adjoint remap that gathers its real
+                # entries zeroes them (its padding entries stay exact zeros: the padded input
+                # channels and output-gradient channels are zero) — no fill launch per step
+                e.dwbuf = torch.zeros((groups * op, KH, KW, cp), dtype=torch.float32,
+                                      device=weight.device)
+            padded = (e.wb, e.wt, wr, e.dwbuf)
             wp = weight
         else:
             wp = to_nchw(_remap_param(weight, wr, (groups * op, KH, KW, cp)))
@@ -2117,12 +2126,13 @@ class Remap:
             self._dev[device] = d
         return d
 
-    def apply(self, x, inverse=False, acc=None):
-        """Remap the contiguous ``x`` (last dim = channels) -> flat [Q, J] (or add into ``acc``)."""
+    def apply(self, x, inverse=False, acc=None, clear_src=False):
+        """Remap the contiguous ``x`` (last dim = channels) -> flat [Q, J] (or add into ``acc``);
+        ``clear_src`` zeroes the elements of ``x`` it read (fp32)."""
         cm, rm, icm, irm = self.maps(x.device)
         if inverse:
             cm, rm = icm, irm
-        return _C().chan_remap(x, cm, rm, self.K, acc)
+        return _C().chan_remap(x, cm, rm, self.K, acc, clear_src)
 
 
 class _RemapFn(torch.autograd.Function):

@@ -647,6 +647,9 @@ def test_group_padded_plan_operands_match_remap(name, kind):
                                               if p.grad is not None}))
         plan = b.__dict__["_pca_wplan"]
         assert any(isinstance(e.groups, tuple) and e.groups[0] == kind for e in plan.entries)
+        for e in plan.entries:     # persistent padded dW buffers are handed back all-zero
+            if getattr(e, "dwbuf", None) is not None:
+                assert not e.dwbuf.any(), e.groups
         for i in range(3):
             o, r = outs[3 + i], outs[i]
             assert torch.equal(o[0], r[0]), ("forward", i)
