@@ -199,7 +199,9 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     const float* __restrict__ stat, int R, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     int64_t* __restrict__ nbt, float momentum, float eps, int training, int update_running,
-    float* __restrict__ aux, const float* kin, float* pilot_out, float* zero, int zero_n) {
+    float* __restrict__ aux, const float* kin, float* pilot_out, float* zero, int zero_n, int ld) {
+  // (stat rows [R][2][ld], ld >= C: a zero-padded conv's statistics are read in place, its
+  // padding channels skipped)
   __shared__ float red[16][64][2];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -212,8 +214,8 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
   if (training && c < C) {
 #pragma unroll 4
     for (int r = rl; r < R; r += 16) {
-      s += stat[(size_t)r * 2 * C + c];
-      q += stat[(size_t)r * 2 * C + C + c];
+      s += stat[(size_t)r * 2 * ld + c];
+      q += stat[(size_t)r * 2 * ld + ld + c];
     }
   }
   red[rl][cl][0] = s;
@@ -955,10 +957,10 @@ void bn_finalize_launch(const float* stat, int R, int C, double count, const flo
                         const float* beta, float* rmean, float* rvar, int64_t* nbt,
                         float momentum, float eps, int training, int update_running, float* aux,
                         hipStream_t st, const float* kin, float* pilot_out, float* zero,
-                        int zero_n) {
+                        int zero_n, int ld) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C, count,
                      gamma, beta, rmean, rvar, nbt, momentum, eps, training, update_running, aux,
-                     kin, pilot_out, zero, zero_n);
+                     kin, pilot_out, zero, zero_n, ld > 0 ? ld : C);
 }
 
 void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const bf16* res,

@@ -83,7 +83,7 @@ void bias_grad_fold_launch(const float*, int, int, int, float*, hipStream_t);
 void bn_finalize_launch(const float*, int, int, double, const float*, const float*, float*, float*,
                         int64_t*, float, float, int, int, float*, hipStream_t,
                         const float* kin = nullptr, float* pilot_out = nullptr,
-                        float* zero = nullptr, int zero_n = 0);
+                        float* zero = nullptr, int zero_n = 0, int ld = 0);
 void bn_apply_launch(const bf16*, const float*, int, size_t, const bf16*, const bf16*,
                      const float*, int, bf16*, uint8_t*, hipStream_t);
 void bn_bwd_reduce_launch(const bf16*, const bf16*, const uint8_t*, const bf16*, const float*,
@@ -775,16 +775,24 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
   const float* stat = nullptr;
   int R = 0;
   Tensor folded;
+  int ld = C;
   if (training) {
     TORCH_CHECK(partial.has_value(), "training BN needs statistics");
     const Tensor& p = *partial;
-    check_f32(p, "partial");
+    TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat, "partial must be fp32 on the GPU");
     TORCH_CHECK(p.size(-1) == C, "stat channel mismatch");
+    if (!p.is_contiguous()) {
+      // the channel prefix of zero-padded statistics [R][2][ld] (a padded conv's slab rows)
+      TORCH_CHECK(p.dim() == 3 && p.size(1) == 2 && p.stride(2) == 1 && p.stride(1) >= C &&
+                      p.stride(0) == 2 * p.stride(1),
+                  "partial: contiguous, or the channel prefix of [R][2][ld] rows");
+      ld = (int)p.stride(1);
+    }
     R = p.size(0);
-    stat = ptr<float>(p);
+    stat = p.data_ptr<float>();
     if (R > 1024) {  // finalize folds up to 1024 partial rows in one pass
-      folded = at::empty({64, 2, C}, p.options());
-      R = pca::colsum_launch(stat, R, 2 * C, ptr<float>(folded), cur_stream());
+      folded = at::empty({64, 2, ld}, p.options());
+      R = pca::colsum_launch(stat, R, 2 * ld, ptr<float>(folded), cur_stream());
       stat = ptr<float>(folded);
     }
   }
@@ -801,7 +809,7 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
                           (float)eps, training ? 1 : 0, update_running ? 1 : 0, ptr<float>(aux),
                           cur_stream(), training ? optr<float>(kin) : nullptr,
                           training ? optr<float>(pilot_out) : nullptr, optr<float>(zero),
-                          (zero.has_value() && zero->defined()) ? (int)zero->numel() : 0);
+                          (zero.has_value() && zero->defined()) ? (int)zero->numel() : 0, ld);
   return aux;
 }
 

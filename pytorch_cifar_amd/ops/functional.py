@@ -1145,7 +1145,11 @@ def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
         y = _RemapFn.apply(y, unpad, (N, Ho, Wo, Cout), None)
         if want_stats and stats is not None and stats.numel():
             R = stats.shape[0]
-            stats = unpad.apply(stats.contiguous()).view(R, 2, Cout)
+            if groups == 1:
+                # the real channels are a prefix: the BN finalize reads the padded rows in place
+                stats = stats.view(R, 2, op)[:, :, :Cout]
+            else:
+                stats = unpad.apply(stats.contiguous()).view(R, 2, Cout)
     return to_nchw(y), (stats if want_stats and stats is not None and stats.numel() else None)
 
 
