@@ -173,7 +173,8 @@ struct CatArgs {
   int k;
 };
 void cat_nhwc_launch(const CatArgs&, bf16*, int, bool, hipStream_t);
-void interleave2_launch(bf16*, bf16*, bf16*, int, int, bool, hipStream_t, bf16* = nullptr);
+void interleave2_launch(bf16*, bf16*, bf16*, int, int, bool, hipStream_t, bf16* = nullptr,
+                        int ldh = 0);
 void chan_remap_launch(const void*, void*, bool, bool, const int*, const int*, int, int, int, int,
                        hipStream_t, bool = false);
 void dpn_merge_fwd_launch(const bf16*, const bf16*, int, int, int, int, bf16*, hipStream_t);
@@ -1669,20 +1670,33 @@ static void check_halves(const Tensor& a, const Tensor& b, const char* what) {
   TORCH_CHECK(a.sizes() == b.sizes() && a.dim() == 4 && a.size(3) % 2 == 0, what,
               ": equal NHWC shapes with an even channel count");
 }
-std::vector<Tensor> interleave2_split(const Tensor& a, const Tensor& b) {
+// pad_hi > C: hi is returned as the channel prefix of a [N,H,W,pad_hi] buffer whose padding
+// channels the kernel zeroes (a zero-padded conv input read in place)
+std::vector<Tensor> interleave2_split(const Tensor& a, const Tensor& b, int64_t pad_hi) {
   check_halves(a, b, "interleave2_split");
   const int P = a.size(0) * a.size(1) * a.size(2), C = a.size(3);
-  auto lo = at::empty_like(a), hi = at::empty_like(a);
+  const int ldh = pad_hi > C ? (int)pad_hi : C;
+  TORCH_CHECK(ldh == C || ldh % 8 == 0, "interleave2_split: padded width must be a multiple of 8");
+  auto lo = at::empty_like(a);
+  auto hib = at::empty({a.size(0), a.size(1), a.size(2), ldh}, a.options());
   pca::interleave2_launch(ptr<bf16>(a), ptr<bf16>(b), ptr<bf16>(lo), P, C, false, cur_stream(),
-                          ptr<bf16>(hi));
-  return {lo, hi};
+                          ptr<bf16>(hib), ldh);
+  return {lo, ldh == C ? hib : hib.narrow(3, 0, C)};
 }
 std::vector<Tensor> deinterleave2_split(const Tensor& lo, const Tensor& hi) {
-  check_halves(lo, hi, "deinterleave2_split");
+  check_bf16(lo, "lo");
+  TORCH_CHECK(hi.is_cuda() && hi.scalar_type() == at::kBFloat16, "hi: bf16 GPU tensor");
+  TORCH_CHECK(lo.is_contiguous() && lo.dim() == 4 && lo.size(3) % 2 == 0 && hi.sizes() == lo.sizes(),
+              "deinterleave2_split: equal NHWC shapes with an even channel count");
   const int P = lo.size(0) * lo.size(1) * lo.size(2), C = lo.size(3);
+  // hi: dense, or the channel prefix of wider rows (a padded conv input's gradient)
+  const int64_t ldh = hi.stride(2);
+  TORCH_CHECK(hi.stride(3) == 1 && ldh >= C && hi.stride(1) == hi.size(2) * ldh &&
+                  hi.stride(0) == hi.size(1) * hi.stride(1),
+              "deinterleave2_split: hi must be dense or row-strided NHWC");
   auto a = at::empty_like(lo), b = at::empty_like(lo);
   pca::interleave2_launch(ptr<bf16>(a), ptr<bf16>(b), const_cast<bf16*>(ptr<bf16>(lo)), P, C, true,
-                          cur_stream(), const_cast<bf16*>(ptr<bf16>(hi)));
+                          cur_stream(), ptr<bf16>(hi), (int)ldh);
   return {a, b};
 }
 
@@ -2081,7 +2095,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("chan_remap", &chan_remap, py::arg("x"), py::arg("cmap"), py::arg("rmap") = py::none(),
         py::arg("K") = 1, py::arg("acc") = py::none(), py::arg("clear_src") = false);
   m.def("deinterleave2", &deinterleave2);
-  m.def("interleave2_split", &interleave2_split);
+  m.def("interleave2_split", &interleave2_split, py::arg("a"), py::arg("b"), py::arg("pad_hi") = 0);
   m.def("deinterleave2_split", &deinterleave2_split);
   m.def("split_nhwc", &split_nhwc);
   m.def("dpn_merge_bwd", &dpn_merge_bwd);

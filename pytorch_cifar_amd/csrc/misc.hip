@@ -493,10 +493,14 @@ __device__ __forceinline__ void il_words(uint32_t ua, uint32_t ub, uint32_t& lo,
 // SPLIT: y is held as its two channel halves, y = [N,H,W,C] channels [0, C) and y1 = [C, 2C)
 // (the next ShuffleNetV2 block's SplitBlock halves, shufflenetv2.py:22-29, so the split is never
 // a pass of its own); needs C % (2V) == 0 so that no 2V-channel group straddles the halves.
+// ldh: row stride of the y1 half (>= C): the next block's branch input held zero-padded to a
+// multiple of 8 channels (the forward writes the padding zeros), so its odd-width 1x1 conv reads
+// it in place instead of a pad pass (shufflenetv2.py:41 conv1 on the 58-channel half).
 template <int V, bool INV, bool SPLIT = false>
 __global__ __launch_bounds__(256) void interleave2_kernel(bf16* __restrict__ a, bf16* __restrict__ b,
                                                           bf16* __restrict__ y0, int P, int C,
-                                                          bf16* __restrict__ y1 = nullptr) {
+                                                          bf16* __restrict__ y1 = nullptr,
+                                                          int ldh = 0) {
   const int G = C / V;
   const int total = P * G;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
@@ -506,8 +510,12 @@ __global__ __launch_bounds__(256) void interleave2_kernel(bf16* __restrict__ a, 
     bf16* y = y0;
     if constexpr (SPLIT) {
       const int k = gi * 2 * V;                       // channel in the joined [0, 2C)
-      iy = (size_t)p * C + (k < C ? k : k - C);
+      iy = k < C ? (size_t)p * C + k : (size_t)p * ldh + (k - C);
       if (k >= C) y = y1;
+      if constexpr (!INV) {
+        if (gi == G - 1)                              // (the row's last group: its padding)
+          for (int c = C; c < ldh; ++c) y1[(size_t)p * ldh + c] = bf16(0.f);
+      }
     }
     if constexpr (V == 4) {
       if constexpr (!INV) {
@@ -550,21 +558,23 @@ __global__ __launch_bounds__(256) void interleave2_kernel(bf16* __restrict__ a, 
   }
 }
 
-// y1 != nullptr: the joined tensor as two halves (y = channels [0, C), y1 = [C, 2C))
+// y1 != nullptr: the joined tensor as two halves (y = channels [0, C), y1 = [C, 2C) with row
+// stride ldh >= C, 0 = C)
 void interleave2_launch(bf16* a, bf16* b, bf16* y, int P, int C, bool inverse, hipStream_t st,
-                        bf16* y1) {
+                        bf16* y1, int ldh) {
+  if (ldh <= 0) ldh = C;
   const int V = y1 ? (C % 8 == 0 ? 4 : C % 4 == 0 ? 2 : 1) : (C % 4 == 0 ? 4 : C % 2 == 0 ? 2 : 1);
   const dim3 grid(grid_cap((size_t)P * C / V)), block(256);
 #define PCA_IL(VV)                                                                                  \
   if (V == VV) {                                                                                    \
     if (y1 && inverse)                                                                              \
-      hipLaunchKernelGGL((interleave2_kernel<VV, true, true>), grid, block, 0, st, a, b, y, P, C, y1); \
+      hipLaunchKernelGGL((interleave2_kernel<VV, true, true>), grid, block, 0, st, a, b, y, P, C, y1, ldh); \
     else if (y1)                                                                                    \
-      hipLaunchKernelGGL((interleave2_kernel<VV, false, true>), grid, block, 0, st, a, b, y, P, C, y1); \
+      hipLaunchKernelGGL((interleave2_kernel<VV, false, true>), grid, block, 0, st, a, b, y, P, C, y1, ldh); \
     else if (inverse)                                                                               \
-      hipLaunchKernelGGL((interleave2_kernel<VV, true>), grid, block, 0, st, a, b, y, P, C, nullptr); \
+      hipLaunchKernelGGL((interleave2_kernel<VV, true>), grid, block, 0, st, a, b, y, P, C, nullptr, 0); \
     else                                                                                            \
-      hipLaunchKernelGGL((interleave2_kernel<VV, false>), grid, block, 0, st, a, b, y, P, C, nullptr); \
+      hipLaunchKernelGGL((interleave2_kernel<VV, false>), grid, block, 0, st, a, b, y, P, C, nullptr, 0); \
     return;                                                                                         \
   }
   PCA_IL(4) PCA_IL(2) PCA_IL(1)

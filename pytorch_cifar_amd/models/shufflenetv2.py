@@ -6,14 +6,22 @@ direct-conv and scalar depthwise kernels where the MFMA tile needs multiples of 
 
 Inside a stage the blocks hand each other the two SplitBlock halves instead of the joined
 tensor: every join but the stage's last is F.cat_shuffle2_split (one interleave pass writing
-both halves), so no split / concat pass runs between blocks (K22). Calling a block on its own
-keeps the reference contract (joined tensor in, joined tensor out)."""
+both halves), so no split / concat pass runs between blocks (K22). At odd widths the second
+half is written zero-padded to a multiple of 8 channels, the layout the next block's 1x1 conv
+reads in place. Calling a block on its own keeps the reference contract (joined tensor in,
+joined tensor out)."""
 import os
 
 import torch.nn as tnn
 
 from ..nn import BatchNorm2d, Conv2d, Linear, Sequential
 from ..nn import functional as F
+
+
+def _pad8(c):
+    """Width the next block's branch input is held at (zero-padded to a multiple of 8 when its
+    odd-width 1x1 conv would otherwise pad it in a pass of its own), 0 = dense."""
+    return (c + 7) // 8 * 8 if c % 8 else 0
 
 
 class ShuffleBlock(tnn.Module):
@@ -60,7 +68,7 @@ class BasicBlock(tnn.Module):
         """forward() on the SplitBlock halves; split_out: return the halves of the result."""
         out = self._branch(x2)
         if split_out and self.shuffle.groups == 2:
-            return F.cat_shuffle2_split(x1, out)
+            return F.cat_shuffle2_split(x1, out, _pad8(out.shape[1]))
         return self._join(x1, out)
 
     def _join(self, a, b):
@@ -100,7 +108,7 @@ class DownBlock(tnn.Module):
     def forward_halves(self, x):
         """forward() returned as the next block's SplitBlock halves."""
         left, right = self._branches(x)
-        return F.cat_shuffle2_split(left, right)
+        return F.cat_shuffle2_split(left, right, _pad8(left.shape[1]))
 
 
 class _Stage(Sequential):

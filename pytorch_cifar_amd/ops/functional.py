@@ -1103,10 +1103,17 @@ def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
     Cout, Cg, KH, KW = weight.shape
     cout_g = Cout // groups
     cp, op = _round8(Cg), _round8(cout_g)
-    xn = to_nhwc(x)
-    N, H, W, _ = xn.shape
-    if cp != Cg:
-        xn = _RemapFn.apply(xn, _group_pad_remap(groups, Cg, cp), (N, H, W, groups * cp), None)
+    if groups == 1 and cp != Cg and getattr(x, "_pca_zpad", 0) == cp:
+        # the producer left x as the prefix of a zero-padded buffer of this width: read in place
+        xv = x.permute(0, 2, 3, 1)
+        N, H, W, _ = xv.shape
+        assert xv.stride() == (H * W * cp, W * cp, cp, 1), "zero-padded input layout"
+        xn = _ZeroPadView.apply(xv, cp)
+    else:
+        xn = to_nhwc(x)
+        N, H, W, _ = xn.shape
+        if cp != Cg:
+            xn = _RemapFn.apply(xn, _group_pad_remap(groups, Cg, cp), (N, H, W, groups * cp), None)
     # weight [Cout, Cg, KH, KW] -> [G*op, cp, KH, KW], channels_last (the MFMA B layout): with a
     # plan, the padded bf16 operands are written by its batched launch (or the fused optimizer
     # step) straight from the master — no per-step fp32 remap + convert
@@ -2252,31 +2259,57 @@ def cat_shuffle2(a, b):
 
 class _Interleave2Split(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b):
-        lo, hi = _C().interleave2_split(a, b)
+    def forward(ctx, a, b, pad_hi):
+        lo, hi = _C().interleave2_split(a, b, pad_hi)
         return lo, hi
 
     @staticmethod
     def backward(ctx, dlo, dhi):
         ref = dlo if dlo is not None else dhi
         dlo = dlo.contiguous() if dlo is not None else torch.zeros_like(ref)
-        dhi = dhi.contiguous() if dhi is not None else torch.zeros_like(ref)
+        if dhi is None:
+            dhi = torch.zeros_like(ref)
+        elif _rows_view(dhi) is not dhi:
+            dhi = dhi.contiguous()   # (a row-strided NHWC view, e.g. a padded conv's dX, is read in place)
         da, db = _C().deinterleave2_split(dlo, dhi)
-        return da, db
+        return da, db, None
 
 
-def cat_shuffle2_split(a, b):
+def cat_shuffle2_split(a, b, pad_hi=0):
     """The two channel halves of channel_shuffle(cat([a, b], 1), 2) — a ShuffleNetV2 join followed
     by the next block's SplitBlock (shufflenetv2.py:22-29, 49) — as ONE native interleave pass
     writing both halves (backward: one pass reading both half-gradients): no concatenated
-    tensor is formed, and the split / concat passes of the two-step form disappear."""
+    tensor is formed, and the split / concat passes of the two-step form disappear.
+    ``pad_hi`` (a multiple of 8 above the half width): the second half — the next block's
+    branch input — is the channel prefix of a zero-padded buffer of that width, which its
+    odd-width 1x1 conv then reads in place (``_pca_zpad``) instead of a pad pass."""
     if (_ref(a) or a.shape != b.shape or a.dtype != COMPUTE_DTYPE or b.dtype != COMPUTE_DTYPE
             or a.dim() != 4 or a.shape[1] % 2):
         y = cat_shuffle2(a, b)
         c = y.shape[1] // 2
         return y[:, :c], y[:, c:]
-    lo, hi = _Interleave2Split.apply(to_nhwc(a), to_nhwc(b))
-    return to_nchw(lo), to_nchw(hi)
+    C = a.shape[1]
+    pad = pad_hi if (pad_hi > C and pad_hi % 8 == 0 and _GROUP_PAD) else 0
+    lo, hi = _Interleave2Split.apply(to_nhwc(a), to_nhwc(b), pad)
+    hi = to_nchw(hi)
+    if pad:
+        hi._pca_zpad = pad
+    return to_nchw(lo), hi
+
+
+class _ZeroPadView(torch.autograd.Function):
+    """The whole zero-padded buffer [N,H,W,cp] behind a channel-prefix view (its padding channels
+    written as zeros by their producer); backward: the gradient's channel prefix, a view."""
+
+    @staticmethod
+    def forward(ctx, xn, cp):
+        N, H, W, C = xn.shape
+        ctx.C = C
+        return xn.as_strided((N, H, W, cp), (H * W * cp, W * cp, cp, 1))
+
+    @staticmethod
+    def backward(ctx, dxp):
+        return dxp[..., : ctx.C], None
 
 
 # ------------------------------------------------------------- zero-copy concatenation

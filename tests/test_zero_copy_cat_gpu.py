@@ -284,12 +284,16 @@ def test_interleave2_split_matches_reference():
     for vector widths 4 / 2 / 1 (C % 8, C % 4, C % 2)."""
     from pytorch_cifar_amd.nn import functional as F
 
-    for c in (24, 12, 58, 6):
+    for c, pad in ((24, 0), (12, 0), (58, 0), (6, 0), (58, 64), (6, 8), (12, 16)):
         a = torch.randn(4, c, 5, 3, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         b = torch.randn_like(a).contiguous(memory_format=torch.channels_last)
         a.requires_grad_(True)
         b.requires_grad_(True)
-        lo, hi = F.cat_shuffle2_split(a, b)
+        lo, hi = F.cat_shuffle2_split(a, b, pad)
+        if pad:   # hi: channel prefix of a zero-padded [N,H,W,pad] buffer
+            assert getattr(hi, "_pca_zpad", 0) == pad
+            full = hi.permute(0, 2, 3, 1).as_strided((4, 5, 3, pad), (15 * pad, 3 * pad, pad, 1))
+            assert not full[..., c:].any(), "padding channels must be zero"
         y = torch.stack([a.detach(), b.detach()], 2).reshape(4, 2 * c, 5, 3)
         assert torch.equal(lo.float(), y[:, :c].float()), c
         assert torch.equal(hi.float(), y[:, c:].float()), c

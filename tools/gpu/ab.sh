@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B runner (one script for every comparison of the rounds' notes).
 #
-#   bash tools/gpu/ab.sh [-t "<pytest args>"] [-r REPS] [-b "BATCHES"] [-m "Model batch"]... ARM ARM...
+#   bash tools/gpu/ab.sh [-t '<pytest args, e.g. tests/x.py -k "a or b">'] [-r REPS] [-b "BATCHES"] [-m "Model batch"]... ARM ARM...
 #
 # An ARM is a source tree holding bench.py + a built pytorch_cifar_amd/, optionally followed by
 # "|" and environment settings:  "."  "ab/base"  ".|PCA_GROUP_DENSE=0"  ".|PCA_S2C_ADDEND=0".
@@ -27,7 +27,8 @@ shift $((OPTIND - 1))
 [ $# -ge 2 ] || { echo "need at least two arms"; exit 2; }
 ARMS=("$@")
 if [ -n "$TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread $TESTS \
+  # (eval: quotes inside the -t string group a -k expression)
+  eval "timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread $TESTS" \
     > gpurun_out/ab_tests.log 2>&1 || { tail -40 gpurun_out/ab_tests.log; exit 1; }
   tail -1 gpurun_out/ab_tests.log
 fi
