@@ -261,13 +261,15 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
                                                        const bf16* __restrict__ y2,
                                                        const float* __restrict__ aux2, int act,
                                                        bf16* __restrict__ out,
-                                                       uint8_t* __restrict__ mask) {
+                                                       uint8_t* __restrict__ mask, int ldy) {
+  // (ldy > C: y is the channel prefix of wider rows — a zero-padded conv's output read in place)
   const size_t nvec = total / VEC;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 256) {
     const size_t e = i * VEC;
     const int c0 = (int)(e % C);
+    const size_t ey = ldy == C ? e : (e / C) * ldy + c0;
     float f[VEC];
-    load_vec<VEC>(y + e, f);
+    load_vec<VEC>(y + ey, f);
 #pragma unroll
     for (int v = 0; v < VEC; ++v) f[v] = f[v] * aux[2 * C + c0 + v] + aux[3 * C + c0 + v];
     if (res) {
@@ -544,17 +546,24 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16* __restrict__ y, const float* __restrict__ aux, const float* __restrict__ coef,
     int act, int C, size_t total,
     bf16* __restrict__ dy, bf16* __restrict__ dres, const bf16* __restrict__ y2,
-    bf16* __restrict__ dy2) {
+    bf16* __restrict__ dy2, int ldy, int ldx) {
+  // ldy / ldx > C: y read from, and dy written into, the channel prefix of wider rows; dy's
+  // padding channels are written as zeros (the gradient of a zero-padded conv's output, handed
+  // to that conv without a pad pass)
   const size_t nvec = total / VEC;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 256) {
     const size_t e = i * VEC;
     const int c0 = (int)(e % C);
+    const size_t row = e / C;
+    const size_t ey = ldy == C ? e : row * ldy + c0, ex = ldx == C ? e : row * ldx + c0;
     float dz[VEC], yy[VEC], o[VEC];
-    compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz, e, e);
-    load_vec<VEC>(y + e, yy);
+    compute_dz<VEC>(dout, out, mask, y, aux, C, c0, e, act, dz, e, ey);
+    load_vec<VEC>(y + ey, yy);
 #pragma unroll
     for (int v = 0; v < VEC; ++v) o[v] = coef[c0 + v] * dz[v] + coef[C + c0 + v] * yy[v] + coef[2 * C + c0 + v];
-    store_vec<VEC>(dy + e, o);
+    store_vec<VEC>(dy + ex, o);
+    if (ldx > C && c0 + VEC == C)
+      for (int c = C; c < ldx; ++c) dy[row * ldx + c] = bf16(0.f);
     if (dres) store_vec<VEC>(dres + e, dz);
     if (dy2) {
       load_vec<VEC>(y2 + e, yy);
@@ -986,19 +995,21 @@ void bn_apply_launch(const bf16* y, const float* aux, int C, size_t total, const
 #undef PCA_APPLY
     return;
   }
-  if (!bn_ld_dense()) {
+  // (the vector kernels take a row-strided input y only: a zero-padded conv's output prefix)
+  if (g_bn_ld.out || g_bn_ld.dout || g_bn_ld.dx || g_bn_ld.dx_acc || (g_bn_ld.y && (res || y2))) {
     fprintf(stderr, "pca: strided BatchNorm apply needs the row-tiled kernel (C %% 8 == 0)\n");
     abort();
   }
+  const int ldy = ld_or(g_bn_ld.y, C);
   switch (bn_vec(C)) {
     case 8:
       hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, y, aux, C,
-                         total, res, y2, aux2, act, out, mask);
+                         total, res, y2, aux2, act, out, mask, ldy);
       break;
 #define PCA_APPLY_V(V)                                                                             \
   case V:                                                                                          \
     hipLaunchKernelGGL(bn_apply_kernel<V>, dim3(grid_for(total / V)), dim3(256), 0, st, y, aux, C, \
-                       total, res, y2, aux2, act, out, (uint8_t*)nullptr);                         \
+                       total, res, y2, aux2, act, out, (uint8_t*)nullptr, ldy);                    \
     break;
     PCA_APPLY_V(4) PCA_APPLY_V(2) PCA_APPLY_V(1)
 #undef PCA_APPLY_V
@@ -1074,20 +1085,24 @@ void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask,
 #undef PCA_BWD
     return;
   }
-  if (!bn_ld_dense()) {
+  // (the vector kernels take a row-strided y and dy only — a zero-padded conv's output prefix
+  // and its gradient, whose padding they zero)
+  if (g_bn_ld.out || g_bn_ld.dout || g_bn_ld.dx_acc ||
+      ((g_bn_ld.y || g_bn_ld.dx) && (dres || y2 || dy2))) {
     fprintf(stderr, "pca: strided BatchNorm backward needs the row-tiled kernel (C %% 8 == 0)\n");
     abort();
   }
+  const int ldy = ld_or(g_bn_ld.y, C), ldx = ld_or(g_bn_ld.dx, C);
   switch (bn_vec(C)) {
     case 8:
       hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(grid_for(total / 8)), dim3(256), 0, st, dout,
-                         out, mask, y, aux, coef, act, C, total, dy, dres, y2, dy2);
+                         out, mask, y, aux, coef, act, C, total, dy, dres, y2, dy2, ldy, ldx);
       break;
 #define PCA_BWD_V(V)                                                                              \
   case V:                                                                                         \
     hipLaunchKernelGGL(bn_bwd_apply_kernel<V>, dim3(grid_for(total / V)), dim3(256), 0, st, dout, \
                        out, (const uint8_t*)nullptr, y, aux, coef, act, C, total, dy, dres, y2,   \
-                       dy2);                                                                      \
+                       dy2, ldy, ldx);                                                            \
     break;
     PCA_BWD_V(4) PCA_BWD_V(2) PCA_BWD_V(1)
 #undef PCA_BWD_V

@@ -257,6 +257,18 @@ int rows_ld(const Tensor& t, const char* name) {
   return (int)t.stride(2);
 }
 
+// rows_ld without the C % 8 condition: a BatchNorm input that is the channel prefix of a
+// zero-padded conv output (rows of a multiple of 8), read by the vector kernels with a row stride
+int rows_ld_bn(const Tensor& t, const char* name) {
+  const int C = t.size(-1);
+  if (t.is_contiguous() || C % 8 == 0) return rows_ld(t, name);
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, name, " must be bf16 on the GPU");
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.stride(2) > C && t.stride(2) % 8 == 0 &&
+                  t.stride(1) == t.size(2) * t.stride(2) && t.stride(0) == t.size(1) * t.stride(1),
+              name, " must be contiguous NHWC or the channel prefix of rows padded to a multiple of 8");
+  return (int)t.stride(2);
+}
+
 // dst <- src for NHWC [N,H,W,C] tensors of the same shape, either of them row-strided (a channel
 // slice of a concat slab), C % 8 == 0
 void copy_rows(const Tensor& src, const Tensor& dst) {
@@ -815,10 +827,26 @@ Tensor bn_finalize(const optional<Tensor>& partial, double count, const optional
 }
 
 // out: optional destination (a row-strided channel slice of a concat slab), else a new tensor
+// (a strided odd-width y goes to the vector kernels only without residual / second BN; with
+// them it is made dense first)
+static bool bn_odd_strided(const Tensor& y) { return !y.is_contiguous() && y.size(-1) % 8 != 0; }
+
+std::vector<Tensor> bn_apply_impl(const Tensor& y, const Tensor& aux, const optional<Tensor>& res,
+                                  const optional<Tensor>& y2, const optional<Tensor>& aux2, int act,
+                                  bool want_mask, const optional<Tensor>& out_opt);
 std::vector<Tensor> bn_apply(const Tensor& y, const Tensor& aux, const optional<Tensor>& res,
                              const optional<Tensor>& y2, const optional<Tensor>& aux2, int act,
                              bool want_mask, const optional<Tensor>& out_opt) {
-  const int ldy = rows_ld(y, "y");
+  const bool extra = (res.has_value() && res->defined()) || (y2.has_value() && y2->defined()) ||
+                     (out_opt.has_value() && out_opt->defined());
+  if (bn_odd_strided(y) && extra) return bn_apply_impl(y.contiguous(), aux, res, y2, aux2, act, want_mask, out_opt);
+  return bn_apply_impl(y, aux, res, y2, aux2, act, want_mask, out_opt);
+}
+
+std::vector<Tensor> bn_apply_impl(const Tensor& y, const Tensor& aux, const optional<Tensor>& res,
+                                  const optional<Tensor>& y2, const optional<Tensor>& aux2, int act,
+                                  bool want_mask, const optional<Tensor>& out_opt) {
+  const int ldy = rows_ld_bn(y, "y");
   const int C = y.size(-1);
   TORCH_CHECK(aux.size(1) == C, "aux channel mismatch");
   if (res.has_value() && res->defined()) {
@@ -940,7 +968,41 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
 }
 
 // Full BN backward: returns {dy, dres, dy2, dgamma, dbeta, dgamma2, dbeta2}
+std::vector<Tensor> bn_backward_impl(const Tensor& dout, const optional<Tensor>& out,
+                                     const optional<Tensor>& mask, const Tensor& y,
+                                     const Tensor& aux, const optional<Tensor>& gamma,
+                                     const optional<Tensor>& y2, const optional<Tensor>& aux2,
+                                     const optional<Tensor>& gamma2, int act, bool training,
+                                     bool need_dres, const optional<Tensor>& dgamma_acc,
+                                     const optional<Tensor>& dbeta_acc,
+                                     const optional<Tensor>& dgamma2_acc,
+                                     const optional<Tensor>& dbeta2_acc,
+                                     const optional<Tensor>& partial_in,
+                                     const optional<Tensor>& acc_in, int acc_rows, bool acc_filled,
+                                     const optional<Tensor>& zero1, const optional<Tensor>& zero2,
+                                     const optional<Tensor>& dx_out, bool dx_acc);
 std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
+                                const optional<Tensor>& mask, const Tensor& y,
+                                const Tensor& aux, const optional<Tensor>& gamma,
+                                const optional<Tensor>& y2, const optional<Tensor>& aux2,
+                                const optional<Tensor>& gamma2, int act, bool training,
+                                bool need_dres, const optional<Tensor>& dgamma_acc,
+                                const optional<Tensor>& dbeta_acc,
+                                const optional<Tensor>& dgamma2_acc,
+                                const optional<Tensor>& dbeta2_acc,
+                                const optional<Tensor>& partial_in,
+                                const optional<Tensor>& acc_in, int acc_rows, bool acc_filled,
+                                const optional<Tensor>& zero1, const optional<Tensor>& zero2,
+                                const optional<Tensor>& dx_out, bool dx_acc) {
+  const bool extra = need_dres || (y2.has_value() && y2->defined()) ||
+                     (dx_out.has_value() && dx_out->defined());
+  const Tensor yd = bn_odd_strided(y) && extra ? y.contiguous() : y;
+  return bn_backward_impl(dout, out, mask, yd, aux, gamma, y2, aux2, gamma2, act, training,
+                          need_dres, dgamma_acc, dbeta_acc, dgamma2_acc, dbeta2_acc, partial_in,
+                          acc_in, acc_rows, acc_filled, zero1, zero2, dx_out, dx_acc);
+}
+
+std::vector<Tensor> bn_backward_impl(const Tensor& dout, const optional<Tensor>& out,
                                 const optional<Tensor>& mask, const Tensor& y,
                                 const Tensor& aux, const optional<Tensor>& gamma,
                                 const optional<Tensor>& y2, const optional<Tensor>& aux2,
@@ -956,7 +1018,7 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
   // dout / y may be row-strided channel slices of concat slabs; dx_out (optional) receives dy
   // (added into it with dx_acc), else dy is a new tensor
   const int ldd = rows_ld(dout, "dout");
-  const int ldy = rows_ld(y, "y");
+  const int ldy = rows_ld_bn(y, "y");
   const int C = y.size(-1);
   TORCH_CHECK(dout.sizes() == y.sizes(), "dout shape mismatch");
   int ldx = C;
@@ -966,8 +1028,17 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
     TORCH_CHECK(dx_out->sizes() == y.sizes(), "dx_out shape mismatch");
   }
   TORCH_CHECK(has_dx || !dx_acc, "dx_acc needs dx_out");
+  // y the prefix of zero-padded rows (C % 8 != 0): dy comes back in the same padded layout, its
+  // padding zeroed by the kernel — the padded conv's dY, with no pad pass
+  const bool pad_dy = !has_dx && ldy != C && C % 8 != 0;
+  if (pad_dy) ldx = ldy;
   BnLdScope lds(C, ldy, C, ldd, ldx, dx_acc);
-  auto new_dy = [&]() { return has_dx ? *dx_out : at::empty(y.sizes(), y.options()); };
+  auto new_dy = [&]() {
+    if (has_dx) return *dx_out;
+    if (pad_dy)
+      return at::empty({y.size(0), y.size(1), y.size(2), (int64_t)ldy}, y.options()).narrow(3, 0, C);
+    return at::empty(y.sizes(), y.options());
+  };
   const int M = y.numel() / C;
   const bool dual = y2.has_value() && y2->defined();
   const int NS = dual ? 3 : 2;

@@ -989,6 +989,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
 # through them. Even where the padded group leaves most of a 64-wide MFMA tile empty (DPN's
 # 3-channel groups) this beats the scalar direct kernels by 10-30x (tools/zoo_bench.py).
 _GROUP_PAD = os.environ.get("PCA_GROUP_PAD", "1") != "0"
+# zero-padded convs (groups == 1) hand their output to the consumer as a row-strided prefix view
+_PAD_VIEW = os.environ.get("PCA_PAD_VIEW", "1") != "0"
 
 
 # Narrow groups as block-diagonal super-groups: P = S / Cg neighbouring groups become one group of
@@ -1146,6 +1148,15 @@ def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
                                                     (groups * op,))
     y, stats = _ConvMFMA.apply(xn, wp, bp, stride, padding, groups, want_stats, 0, None, False,
                                None, None, None, padded)
+    if op != cout_g and groups == 1 and _PAD_VIEW:
+        # the real channels are a prefix: consumers read them in place (BatchNorm: row-strided
+        # vector kernels, its dY handed back already padded)
+        slot = _PadSlot()
+        yv = to_nchw(_UnpadView.apply(y, Cout, slot))
+        yv._pca_padslot = slot
+        if want_stats and stats is not None and stats.numel():
+            stats = stats.view(stats.shape[0], 2, op)[:, :, :Cout]
+        return yv, (stats if want_stats and stats is not None and stats.numel() else None)
     if op != cout_g:
         Ho, Wo = y.shape[1], y.shape[2]
         unpad = _group_unpad_remap(groups, cout_g, op)
@@ -1191,7 +1202,7 @@ def add_bias(y_nhwc, bias):
 # -------------------------------------------------------------------------- batch norm
 class _BNCfg:
     __slots__ = ("bn", "bn2", "act", "training", "count", "src", "bacc", "faccs", "pilot", "pilot2",
-                 "dest", "dslot")
+                 "dest", "dslot", "padslot")
 
     def __init__(self, bn, bn2, act, training, count):
         self.bn, self.bn2, self.act, self.training, self.count = bn, bn2, act, training, count
@@ -1201,6 +1212,7 @@ class _BNCfg:
         self.src = None
         self.bacc = None      # the BN's backward StatAcc (sharded sums of dz, dz*xhat[, dz*xhat2])
         self.faccs = ()       # forward StatAccs this BN consumed (cleared by its backward kernel)
+        self.padslot = None   # zero-padded conv output read in place: its dY goes back padded
 
 
 def _bn_aux(C, bn, y, stats, training, count, pilot=None, kin=None, zero=None):
@@ -1221,7 +1233,8 @@ def _bn_aux(C, bn, y, stats, training, count, pilot=None, kin=None, zero=None):
     update = training and bn.running_mean is not None
     if use_batch and stats is None:
         # no producer delivered sums: one centred pass (sums of y - y[0]; robust variance)
-        stats, kin = C.bn_stats_centered(y)
+        stats, kin = C.bn_stats_centered(y if y.is_contiguous() or y.shape[-1] % 8 == 0
+                                         else y.contiguous())
     elif use_batch and kin is None:
         kin = getattr(stats, "_pca_kin", None)
     momentum = bn.momentum if bn.momentum is not None else 0.1
@@ -1380,6 +1393,14 @@ class _BatchNormAct(torch.autograd.Function):
             ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2, part,
             acc.buf if acc is not None else None, acc.R if acc is not None else 0, filled,
             zeros[0], zeros[1], dgx, dgx is not None)
+        ps = cfg.padslot
+        if ps is not None and dy is not None and not dy.is_contiguous() and dy.dim() == 4:
+            # dY written into zero-padded rows (the binding's pad_dy): the producer conv takes
+            # the whole padded tensor
+            n, h, w, _ = dy.shape
+            ld = dy.stride(2)
+            ps.base = dy.as_strided((n, h, w, ld), (h * w * ld, w * ld, ld, 1))
+            ps.dy = dy
         ret = {}
 
         def deliver(p, buf, val, slot):
@@ -1429,6 +1450,8 @@ def _bn_input(x):
         r = _rows_view(v)
         if r is v:
             return v
+    if not v.is_contiguous() and getattr(x, "_pca_padslot", None) is not None:
+        return v           # (a zero-padded conv's output prefix: the BN kernels take its rows)
     return to_nhwc(x)
 
 
@@ -1468,6 +1491,7 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None,
     if out is not None:
         cfg.dest = out
     cfg.dslot = getattr(x, "_pca_dense_slot", None)
+    cfg.padslot = getattr(x, "_pca_padslot", None) if not y.is_contiguous() else None
     if cfg.dslot is not None and torch.is_grad_enabled():
         cfg.dslot.claimed = True
     if training and bn.running_mean is not None:
@@ -2310,6 +2334,38 @@ class _ZeroPadView(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dxp):
         return dxp[..., : ctx.C], None
+
+
+class _PadSlot:
+    """Hand-off between a zero-padded conv's output prefix (_UnpadView) and the BatchNorm that
+    reads it in place: the BN backward deposits its dY, written into zero-padded rows, here."""
+    __slots__ = ("base", "dy")
+
+    def __init__(self):
+        self.base = self.dy = None
+
+
+class _UnpadView(torch.autograd.Function):
+    """The real channels of a zero-padded conv output [N,H,W,op] as a row-strided view (no slice
+    pass). Backward: the padded gradient the consuming BatchNorm left in the slot (same tensor:
+    no pad pass), else the gradient padded with zeros here."""
+
+    @staticmethod
+    def forward(ctx, yp, C, slot):
+        ctx.C, ctx.slot, ctx.op = C, slot, yp.shape[-1]
+        return yp[..., :C]
+
+    @staticmethod
+    def backward(ctx, dy):
+        slot = ctx.slot
+        base, dyv = slot.base, slot.dy
+        slot.base = slot.dy = None
+        if base is not None and dyv is not None and dy.data_ptr() == dyv.data_ptr() and \
+                dy.shape == dyv.shape and dy.stride() == dyv.stride():
+            return base, None, None
+        out = dy.new_zeros(dy.shape[:-1] + (ctx.op,))
+        out[..., : ctx.C] = dy
+        return out, None, None
 
 
 # ------------------------------------------------------------- zero-copy concatenation

@@ -658,3 +658,43 @@ def test_group_padded_plan_operands_match_remap(name, kind):
                 assert torch.equal(o[1][n], r[1][n]), (n, i)
     finally:
         pca.set_deterministic(False)
+
+
+@pytest.mark.parametrize("name", ["ShuffleNetV2_1", "PNASNetA"])
+def test_padded_conv_output_read_in_place(name, monkeypatch):
+    """Zero-padded convs (groups == 1) hand their output to the BatchNorm as a row-strided prefix
+    view, and the BN's dY comes back already padded (PCA_PAD_VIEW): forward, every gradient and
+    the running statistics bitwise equal to the slice / pad passes."""
+    import copy
+
+    import pytorch_cifar_amd as pca
+    from pytorch_cifar_amd import models
+    from pytorch_cifar_amd.ops import functional as OF
+
+    pca.set_deterministic(True)
+    try:
+        torch.manual_seed(0)
+        a = models.MODEL_REGISTRY[name]().cuda().to(memory_format=torch.channels_last)
+        b = copy.deepcopy(a)
+        x = torch.randn(8, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        g = torch.randn(8, 10, device="cuda").to(torch.bfloat16)
+        res = []
+        for m, view in ((a, False), (b, True)):
+            monkeypatch.setattr(OF, "_PAD_VIEW", view)
+            outs = []
+            for _ in range(2):
+                m.zero_grad(set_to_none=True)
+                y = m(x.clone().requires_grad_(True))
+                y.backward(g)
+                torch.cuda.synchronize()
+                outs.append((y.detach().float(), {n: p.grad.clone() for n, p in m.named_parameters()
+                                                  if p.grad is not None}))
+            res.append((outs, {n: t.clone() for n, t in m.named_buffers()}))
+        for i in range(2):
+            assert torch.equal(res[0][0][i][0], res[1][0][i][0]), ("forward", i)
+            for n in res[0][0][i][1]:
+                assert torch.equal(res[0][0][i][1][n], res[1][0][i][1][n]), (n, i)
+        for n in res[0][1]:
+            assert torch.equal(res[0][1][n], res[1][1][n]), n
+    finally:
+        pca.set_deterministic(False)
