@@ -41,11 +41,13 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--timeout", type=int, default=150)
+    ap.add_argument("--native-only", action="store_true", help="skip the stock comparator runs")
     ap.add_argument("models", nargs="*")
     args = ap.parse_args()
     for m in args.models or FAMILIES:
         nat, e1 = run(m, args.batch, args.steps, args.warmup, args.timeout, False)
-        ref, e2 = run(m, args.batch, args.steps, args.warmup, args.timeout, True)
+        ref, e2 = (None, None) if args.native_only else run(m, args.batch, args.steps, args.warmup,
+                                                             args.timeout, True)
         out = {"model": m, "batch": args.batch,
                "native_img_s": nat["value"] if nat else None,
                "native_ms": nat["ms_per_step"] if nat else None,
