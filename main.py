@@ -88,10 +88,17 @@ def _data_parallel_ranks(args):
     for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
         if v is not None:
+            # an empty list hides every GPU: one process (it runs on the CPU)
             return max(1, len([d for d in v.split(",") if d.strip()]))
     import subprocess
-    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
-                       capture_output=True, text=True)
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=180)
+    except subprocess.TimeoutExpired:
+        sys.exit("main.py: counting GPUs timed out (HIP runtime hung?); pass --nproc N")
+    if r.returncode != 0:
+        sys.exit(f"main.py: counting GPUs failed (rc {r.returncode}): {r.stderr.strip()[-300:]}; "
+                 "pass --nproc N")
     try:
         return max(1, int(r.stdout.strip().splitlines()[-1]))
     except (ValueError, IndexError):

@@ -13,6 +13,7 @@ caused it (named in the message) instead of at some later sync point — the HIP
 from __future__ import annotations
 
 import os
+import sys
 
 _lib = None
 _err: Exception | None = None
@@ -126,8 +127,9 @@ def _tune_cache(mod):
         from .engine.tuning import load_table
 
         load_table(mod)
-    except Exception:
-        pass
+    except Exception as e:    # a bad table must not stop the library loading: say why, tune afresh
+        print(f"pytorch_cifar_amd: shipped tune table failed to load ({type(e).__name__}: {e})",
+              file=sys.stderr)
     path = os.environ.get("PCA_TUNE_CACHE")
     if not path or not hasattr(mod, "tune_import"):
         return

@@ -928,6 +928,11 @@ static int grid_for(size_t nvec) {
 
 static int bn_vec(int C) { return C % 8 == 0 ? 8 : C % 4 == 0 ? 4 : C % 2 == 0 ? 2 : 1; }
 
+// Widest C the row-tiled kernels take (0 when PCA_BN_ROWS=0). Row-strided BN operands (concat
+// slab slices and suffixes, zero-padded conv prefixes) need these kernels: callers that would hand
+// such operands to a wider BN keep dense tensors instead (ops/functional.py ChannelSlab/DenseSlab).
+int bn_rows_max_c() { return rows_enabled() ? 2048 : 0; }
+
 int bn_row_blocks(int M, int C) {
   const int vec = bn_vec(C);
   RowPar rp = make_rowpar(C, vec);

@@ -47,7 +47,8 @@ void wgrad_clear_tuned();
 std::vector<std::vector<int>> tune_export();
 void c64_set_prof(int64_t* p);
 int c64_grid_size(int N, int H);
-void copy_rows_launch(const bf16* src, int lds, bf16* dst, int ldd, int P, int C, hipStream_t st);
+void copy_rows_launch(const bf16* src, int lds, bf16* dst, int ldd, int P, int C, hipStream_t st,
+                      const bf16* add = nullptr, int lda = 0);
 // batchnorm.hip: row strides of the next BN launches' tensors (0 = dense; common.h BnLd)
 struct BnLd {
   int y, out, dout, dx, dx_acc;
@@ -77,6 +78,10 @@ int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int
                              int pad, int groups, int Ho, int Wo);
 // batchnorm.hip
 int bn_row_blocks(int M, int C);
+int bn_rows_max_c();
+void wgrad_defer_scope(bool on);
+int wgrad_deferred_count();
+void wgrad_flush_launch(hipStream_t st);
 void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t, float* krow = nullptr);
 int colsum_launch(const float*, int, int, float*, hipStream_t);
 void bias_grad_fold_launch(const float*, int, int, int, float*, hipStream_t);
@@ -277,6 +282,17 @@ void copy_rows(const Tensor& src, const Tensor& dst) {
   const int C = src.size(3);
   TORCH_CHECK(C % 8 == 0, "copy_rows needs C % 8 == 0");
   pca::copy_rows_launch(ptr<bf16>(src), ls, ptr<bf16>(dst), ld, (int)(src.numel() / C), C, cur_stream());
+}
+
+// dst <- src + add (NHWC rows; every operand dense or row-strided)
+void add_rows(const Tensor& src, const Tensor& add, const Tensor& dst) {
+  const int ls = rows_ld(src, "src"), la = rows_ld(add, "add"), ld = rows_ld(dst, "dst");
+  TORCH_CHECK(src.sizes() == dst.sizes() && add.sizes() == dst.sizes() && src.dim() == 4,
+              "add_rows: shape mismatch");
+  const int C = src.size(3);
+  TORCH_CHECK(C % 8 == 0, "add_rows needs C % 8 == 0");
+  pca::copy_rows_launch(ptr<bf16>(src), ls, ptr<bf16>(dst), ld, (int)(src.numel() / C), C,
+                        cur_stream(), ptr<bf16>(add), la);
 }
 
 // RAII: the row strides (0 = dense) the BatchNorm launches in scope read / write with
@@ -618,8 +634,13 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int H, int W, int stride, 
 }
 
 // dw: fp32 [Cout, KH, KW, Cin/G] (zeroed here)
+// slab workspaces of deferred reductions: alive until wgrad_flush launched their reduce
+static std::vector<Tensor> g_deferred_ws;
+
+// defer: a split-K slab reduction is recorded (one batched launch at wgrad_flush) instead of
+// launched; only for `out` = the gradient buffer the caller flushes before anyone reads it
 Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride, int pad,
-                  int groups, const optional<Tensor>& out) {
+                  int groups, const optional<Tensor>& out, bool defer) {
   check_bf16(x, "x");
   check_bf16(dy, "dy");
   const int N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
@@ -671,9 +692,24 @@ Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride,
   const int64_t wsn = pca::conv_wgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   Tensor ws;
   if (wsn > 0) ws = at::empty({wsn}, x.options().dtype(at::kFloat));
+  defer = defer && wsn > 0 && out.has_value() && out->defined();
+  const int pend = pca::wgrad_deferred_count();
+  if (defer) pca::wgrad_defer_scope(true);
   pca::conv_wgrad_launch(ptr<bf16>(x), ptr<bf16>(dy), ptr<float>(dw), wsn > 0 ? ptr<float>(ws) : nullptr,
                          N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, cur_stream());
+  if (defer) {
+    pca::wgrad_defer_scope(false);
+    if (pca::wgrad_deferred_count() > pend) g_deferred_ws.push_back(ws);
+  }
   return dw;
+}
+
+// every deferred slab reduction in one launch (per 20) on the current stream; returns how many
+int wgrad_flush() {
+  const int n = pca::wgrad_deferred_count();
+  if (n) pca::wgrad_flush_launch(cur_stream());
+  g_deferred_ws.clear();   // (stream-ordered: later reuse of the slabs runs after the reduce)
+  return n;
 }
 
 // w fp32 [Cout, KH, KW, Cin/G] contiguous -> (bf16 same layout, bf16 [Cin, KH, KW, Cout/G])
@@ -2054,7 +2090,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("addend_s2c") = false,
         "dgrad + fused backward reduce of the producing BN+ReLU -> (dx, partial[rows][2][C]); "
         "with bn_y2 / bn_aux2 (dual BN, accumulator mode) the accumulator gets [R][3][C] sums");
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("KH"), py::arg("KW"),
+        py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("out"),
+        py::arg("defer") = false);
+  m.def("wgrad_flush", &wgrad_flush,
+        "launch every deferred weight-gradient slab reduction (one batched kernel); returns count");
+  m.def("wgrad_deferred", &pca::wgrad_deferred_count, "pending deferred slab reductions");
   m.def("conv_autotune", [](bool on) { g_autotune = on; }, "enable/disable conv tile autotuning");
   m.def("conv_autotune_enabled", []() { return g_autotune; });
   m.def("c64_set_prof", [](const optional<Tensor>& t) {
@@ -2096,6 +2137,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_acc_max_elems", &acc_max_elems,
         "largest tensor whose BN sums a separate pass adds into an accumulator");
   m.def("bn_stats_acc", &bn_stats_acc, "BN sums of a bare tensor into a sharded accumulator");
+  m.def("bn_rows_max_c", &pca::bn_rows_max_c,
+        "widest C of the row-tiled BN kernels (0: disabled); row-strided BN operands need them");
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("accum") = py::none());
   m.def("bn_finalize", &bn_finalize, py::arg("partial"), py::arg("count"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("momentum"),
@@ -2121,6 +2164,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "training BN(+act/+res/+BN2) with the finalize folded in from sharded accumulators");
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("copy_rows", &copy_rows, "dst <- src for NHWC tensors, either a row-strided channel slice");
+  m.def("add_rows", &add_rows, "dst <- src + add for NHWC tensors (each dense or row-strided)");
   m.def("nhwc_to_nchw", &nhwc_to_nchw);
   m.def("augment", &augment);
   m.def("augment_packed", &augment_packed);

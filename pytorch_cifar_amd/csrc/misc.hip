@@ -14,6 +14,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include <type_traits>
 
@@ -464,20 +465,40 @@ void s2c_expand_launch(const bf16* in, bf16* out, int N, int Hc, int Wc, int C, 
                      dim3(256), 0, st, in, out, Hc, Wc, C / 8, total);
 }
 
+// dst <- src [+ add] over NHWC rows of C channels, each operand with its own row stride (a concat
+// slab slice or a dense tensor). With `add` it is the gradient junction of a slab slice that also
+// fed a dense copy (DLA / SimpleDLA trees): the two gradients summed in fp32, rounded once — the
+// arithmetic of the autograd bf16 add it replaces.
+template <bool ADD>
 __global__ __launch_bounds__(256) void copy_rows_kernel(const bf16* __restrict__ src, int lds,
                                                         bf16* __restrict__ dst, int ldd, int P,
-                                                        int C) {
+                                                        int C, const bf16* __restrict__ add,
+                                                        int lda) {
   const int G = C / 8;
   const size_t total = (size_t)P * G;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
     const size_t p = i / G, c = (i - p * G) * 8;
-    *reinterpret_cast<uint4*>(dst + p * ldd + c) = *reinterpret_cast<const uint4*>(src + p * lds + c);
+    uint4 v = *reinterpret_cast<const uint4*>(src + p * lds + c);
+    if constexpr (ADD) {
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(*reinterpret_cast<const uint4*>(add + p * lda + c), b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += b[k];
+      v = pack8(a);
+    }
+    *reinterpret_cast<uint4*>(dst + p * ldd + c) = v;
   }
 }
 
-void copy_rows_launch(const bf16* src, int lds, bf16* dst, int ldd, int P, int C, hipStream_t st) {
-  hipLaunchKernelGGL(copy_rows_kernel, dim3(grid_cap((size_t)P * C / 8)), dim3(256), 0, st, src,
-                     lds, dst, ldd, P, C);
+void copy_rows_launch(const bf16* src, int lds, bf16* dst, int ldd, int P, int C, hipStream_t st,
+                      const bf16* add, int lda) {
+  if (add)
+    hipLaunchKernelGGL(copy_rows_kernel<true>, dim3(grid_cap((size_t)P * C / 8)), dim3(256), 0, st,
+                       src, lds, dst, ldd, P, C, add, lda);
+  else
+    hipLaunchKernelGGL(copy_rows_kernel<false>, dim3(grid_cap((size_t)P * C / 8)), dim3(256), 0, st,
+                       src, lds, dst, ldd, P, C, nullptr, 0);
 }
 
 // ---- ShuffleNetV2 join: shuffle(cat[a, b], groups=2) with equal widths C is the channel
@@ -1936,13 +1957,34 @@ static PoolGeom pg(int N, int H, int W, int C, int Ho, int Wo, int k, int s, int
   PoolGeom g{N, H, W, C, Ho, Wo, k, s, p};
   return g;
 }
+// pool.hip fast paths (PCA_POOL_FAST=0: the generic kernels below for every geometry)
+bool avgpool_ks_launch(bool bwd, const bf16* in, int N, int H, int W, int C, int k, int s, int p,
+                       bf16* out, hipStream_t st);
+void maxpool3s1_fwd_launch(const bf16* x, int N, int H, int W, int C, bf16* y, uint8_t* arg,
+                           hipStream_t st);
+void maxpool3s1_bwd_launch(const bf16* dy, const uint8_t* arg, int N, int H, int W, int C, bf16* dx,
+                           hipStream_t st);
+static bool pool_fast() {
+  static const bool on = [] {
+    const char* e = getenv("PCA_POOL_FAST");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static bool maxpool3s1_ok(int N, int H, int W, int C, int k, int s, int p) {
+  return pool_fast() && k == 3 && s == 1 && p == 1 && C % 8 == 0 &&
+         (size_t)N * H * W * C < (size_t)INT32_MAX;
+}
+
 void avgpool_fwd_launch(const bf16* x, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                         int p, bf16* y, hipStream_t st) {
+  if (pool_fast() && avgpool_ks_launch(false, x, N, H, W, C, k, s, p, y, st)) return;
   hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_cap((size_t)N * Ho * Wo * C)), dim3(256), 0, st,
                      x, pg(N, H, W, C, Ho, Wo, k, s, p), y);
 }
 void avgpool_bwd_launch(const bf16* dy, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                         int p, bf16* dx, hipStream_t st) {
+  if (pool_fast() && avgpool_ks_launch(true, dy, N, H, W, C, k, s, p, dx, st)) return;
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_cap((size_t)N * H * W * C)), dim3(256), 0, st, dy,
                      pg(N, H, W, C, Ho, Wo, k, s, p), dx);
 }
@@ -1951,6 +1993,10 @@ static bool pool8_ok(int N, int H, int W, int C) {
 }
 void maxpool_fwd_launch(const bf16* x, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                         int p, bf16* y, uint8_t* arg, hipStream_t st) {
+  if (maxpool3s1_ok(N, H, W, C, k, s, p)) {
+    maxpool3s1_fwd_launch(x, N, H, W, C, y, arg, st);
+    return;
+  }
   if (k * k <= 256 && pool8_ok(N, H, W, C) && pool8_ok(N, Ho, Wo, C)) {
     hipLaunchKernelGGL(maxpool_fwd8_kernel, dim3(grid_cap((size_t)N * Ho * Wo * C / 8)), dim3(256), 0,
                        st, x, pg(N, H, W, C, Ho, Wo, k, s, p), y, arg);
@@ -1961,6 +2007,10 @@ void maxpool_fwd_launch(const bf16* x, int N, int H, int W, int C, int Ho, int W
 }
 void maxpool_bwd_launch(const bf16* dy, const uint8_t* arg, int N, int H, int W, int C, int Ho,
                         int Wo, int k, int s, int p, bf16* dx, hipStream_t st) {
+  if (maxpool3s1_ok(N, H, W, C, k, s, p)) {
+    maxpool3s1_bwd_launch(dy, arg, N, H, W, C, dx, st);
+    return;
+  }
   if (k * k <= 256 && pool8_ok(N, H, W, C) && pool8_ok(N, Ho, Wo, C)) {
     hipLaunchKernelGGL(maxpool_bwd8_kernel, dim3(grid_cap((size_t)N * H * W * C / 8)), dim3(256), 0,
                        st, dy, arg, pg(N, H, W, C, Ho, Wo, k, s, p), dx);

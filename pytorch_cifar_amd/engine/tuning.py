@@ -53,9 +53,40 @@ def load_table(lib, path: str = TABLE_PATH) -> int:
     except (OSError, ValueError):
         return 0
     if tab.get("version") != lib.tune_version():
+        _skip(f"candidate-set version {tab.get('version')} != {lib.tune_version()}")
         return 0   # candidate set changed since the table was measured: tune afresh
+    why = device_mismatch(tab)
+    if why:
+        _skip(why)
+        return 0
     _loaded["rows"] = int(lib.tune_import(tab.get("rows", [])))
     return _loaded["rows"]
+
+
+def _skip(why: str) -> None:
+    import sys
+
+    print(f"pytorch_cifar_amd: shipped tune table not used ({why}); autotuning every geometry",
+          file=sys.stderr)
+
+
+def device_mismatch(tab: dict) -> str:
+    """Why the table does not describe the current device ('' = it does). The selections are
+    timings of one part: another architecture or CU count must re-tune. Checked only once the
+    process already holds a GPU context (the table is imported when the extension loads, and
+    asking for device properties earlier would initialise HIP in launcher parents)."""
+    import torch
+
+    if not (torch.cuda.is_available() and torch.cuda.is_initialized()):
+        return ""
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    arch = str(getattr(props, "gcnArchName", "") or "").split(":")[0]
+    if tab.get("arch") and arch and arch != tab["arch"]:
+        return f"table arch {tab['arch']}, device {arch}"
+    cus = tab.get("cus")
+    if cus and props.multi_processor_count != cus:
+        return f"table measured on {cus} CUs, device has {props.multi_processor_count}"
+    return ""
 
 
 def sync_selection(ctx, lib=None, export=None, import_=None, clear=None) -> str:

@@ -49,8 +49,10 @@ class Transition(tnn.Module):
         self.conv = Conv2d(in_planes, out_planes, kernel_size=1, bias=False)
 
     def forward(self, x):
-        out = self.conv(self.bn(x, act="relu"), want_stats=False)
-        return F.avg_pool2d(out, 2)
+        # avg_pool2d(conv1x1(z), 2) == conv1x1(avg_pool2d(z, 2)) exactly (a bias-free 1x1 conv is
+        # a per-pixel linear map, densenet.py:31-32): pooling first runs the conv on a quarter of
+        # the pixels (4x fewer FLOPs and conv bytes)
+        return self.conv(F.avg_pool2d(self.bn(x, act="relu"), 2), want_stats=False)
 
 
 class DenseNet(tnn.Module):

@@ -55,5 +55,5 @@ class GoogLeNet(tnn.Module):
             out = m(out)
         out = self.maxpool(out)
         out = self.b5(self.a5(out))
-        out = self.avgpool(out)
-        return self.linear(out.reshape(out.size(0), -1))
+        # avgpool(8) over the 8x8 map + Linear (googlenet.py:95-98) as the fused head kernel
+        return F.pool_linear(out, self.avgpool.kernel_size, self.linear)

@@ -95,8 +95,11 @@ class DownBlock(tnn.Module):
         self.shuffle = ShuffleBlock()
 
     def _branches(self, x):
-        left = self.bn2(self.conv2(self.bn1(self.conv1(x))), act="relu")
+        # the right branch first: its 1x1 conv3 becomes the owner of x's gradient slot, so the
+        # left branch's depthwise dgrad (whose backward then runs first) hands its dX to conv3's
+        # dgrad epilogue instead of an autograd add (same values either order)
         right = self.bn4(F.bn_act_dwconv(self.bn3, self.conv3(x), "relu", self.conv4))
+        left = self.bn2(self.conv2(self.bn1(self.conv1(x))), act="relu")
         return left, self.bn5(self.conv5(right), act="relu")
 
     def forward(self, x):

@@ -7,6 +7,7 @@ Sequential runs each BatchNorm2d+ReLU pair as one pass and the conv epilogue fee
 import torch.nn as tnn
 
 from ..nn import AvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU, Sequential
+from ..nn import functional as F
 
 cfg = {
     "VGG11": [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
@@ -37,5 +38,5 @@ class VGG(tnn.Module):
 
     def forward(self, x):
         out = self.features(x)
-        out = out.reshape(out.size(0), -1)
-        return self.classifier(out)
+        # flatten of the 1x1 map + Linear (vgg.py:21-23) as the fused head kernel
+        return F.pool_linear(out, 1, self.classifier)

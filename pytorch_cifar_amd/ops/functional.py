@@ -11,6 +11,7 @@ except pure data movement (cat/slice/shuffle views) which has no arithmetic.
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 
@@ -214,6 +215,38 @@ def join_wgrad_streams():
     """Make the current stream wait for all outstanding side-stream weight gradients."""
     if _side:
         _join_side_streams()
+
+
+# Deferred weight-gradient reductions. A split-K wgrad that writes slab rows records its reduce
+# instead of launching it (csrc/conv_halo.hip wgrad_flush_launch); every pending one then runs in
+# ONE batched launch when the gradients are next needed: at the end of the backward pass (an
+# autograd-engine callback queued by the first deferred wgrad), or earlier by a DDP bucket about
+# to be all-reduced (parallel/ddp.py). Bitwise the per-conv reduce kernels' result (same order).
+# ResNet-18 bs128: 12 reduce launches (117 us) -> 1.
+# Measured SLOWER and therefore opt-in (PCA_WGRAD_DEFER=1), same box, 2 reps: ResNet-18 bs128
+# 1.867 -> 1.886-1.890 ms, bs1024 6.479-6.483 -> 6.513-6.544 ms. The per-conv reduce reads its slab
+# right after the wgrad wrote it (L2-resident); deferred, every slab is re-read from MALL / HBM at
+# the end of the pass, which costs more than the ~11 launches it saves (ResNet-152 bs128: 779 us
+# for the 3 batched launches).
+_WGRAD_DEFER = os.environ.get("PCA_WGRAD_DEFER", "0") == "1"
+_defer_queued = {"on": False}
+
+
+def flush_wgrads():
+    """Launch every deferred weight-gradient reduction on the current stream (no-op if none)."""
+    _defer_queued["on"] = False
+    if _native._lib is not None:
+        _C().wgrad_flush()
+
+
+def _after_deferred_wgrad():
+    if _defer_queued["on"]:
+        return
+    try:
+        torch.autograd.Variable._execution_engine.queue_callback(flush_wgrads)
+        _defer_queued["on"] = True
+    except RuntimeError:      # not inside a backward pass: nobody would flush later
+        flush_wgrads()
 
 
 # ------------------------------------------------------------------ batched weight prep
@@ -738,7 +771,18 @@ class _ConvMFMA(torch.autograd.Function):
                     else:
                         dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
                 else:
-                    dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
+                    # another consumer's gradient already waiting in the slot (GoogLeNet's
+                    # Inception input feeds three 1x1 convs and a max-pool): this dgrad adds it in
+                    # its epilogue and hands the sum on, so the owner finally stores the total —
+                    # no autograd add between the branches
+                    pend = slot.grad
+                    if (pend is None or getattr(pend, "_pca_s2c", False) or pend.dim() != 4
+                            or tuple(pend.shape) != (dy.shape[0], H, W, wt.shape[0])
+                            or not pend.is_contiguous() or pend.dtype != dy.dtype):
+                        pend = None
+                    else:
+                        slot.grad = None
+                    dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups, pend)
                     if slot.offer(dx):
                         dx = None                # delivered through the owner's epilogue
 
@@ -780,7 +824,9 @@ class _ConvMFMA(torch.autograd.Function):
                 _schedule_join()
                 G.fire(weight)
             elif buf is not None:
-                C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, buf)
+                C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, buf, defer=_WGRAD_DEFER)
+                if _WGRAD_DEFER and C.wgrad_deferred():
+                    _after_deferred_wgrad()
                 G.fire(weight)
             else:
                 dw = C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, None)
@@ -858,8 +904,9 @@ class _ConvDepthwise(torch.autograd.Function):
     (mobilenetv2.py:33-36, efficientnet.py:96-103)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, padding, acc=None, bnsrc=None, out=None):
+    def forward(ctx, x, weight, stride, padding, acc=None, bnsrc=None, out=None, slot=None):
         C = _C()
+        ctx.slot = slot
         Co, _, KH, KW = weight.shape
         wT = _dw_weight(weight)
         if acc is not None:
@@ -898,6 +945,10 @@ class _ConvDepthwise(torch.autograd.Function):
                     src.acc.state = "clean"
             else:
                 dx = C.dw_dgrad(dy, wT, H, W, Cx, KH, KW, stride, padding)
+                if ctx.slot is not None and ctx.slot.offer(dx):
+                    # (ShuffleNetV2 DownBlock, shufflenetv2.py:84-90: x feeds this depthwise conv
+                    # and a 1x1 conv — the 1x1's dgrad epilogue adds this gradient)
+                    dx = None
         w = ctx.weight
         dw_ret = None
         if w.requires_grad:
@@ -913,7 +964,7 @@ class _ConvDepthwise(torch.autograd.Function):
                     G.accumulate(w, dw.view(w.shape[0], KH, KW, 1))
                 else:
                     dw_ret = dw.view(w.shape)
-        return dx, dw_ret, None, None, None, None, None
+        return dx, dw_ret, None, None, None, None, None, None
 
 
 # PCA_DW_BN_FUSE=1: depthwise k3 convs carry the BatchNorm sums of their neighbours in their
@@ -950,7 +1001,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
         fuse = _DW_BN_FUSE and bias is None
         bnsrc = getattr(x, "_pca_bnsrc", None) if (x.requires_grad and fuse) else None
         y = _ConvDepthwise.apply(to_nhwc(x), weight, stride, padding,
-                                 acc if (want_stats and fuse) else None, bnsrc, got)
+                                 acc if (want_stats and fuse) else None, bnsrc, got,
+                                 _slot_for_residual(x))
         if bias is not None:
             y = add_bias(y, bias)
         return to_nchw(y), (got[0] if got else None)
@@ -1146,7 +1198,10 @@ def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
     if bias is not None:
         bp = bias if op == cout_g else _remap_param(bias, _group_pad_remap(groups, cout_g, op),
                                                     (groups * op,))
-    y, stats = _ConvMFMA.apply(xn, wp, bp, stride, padding, groups, want_stats, 0, None, False,
+    # an unpadded input (only the output width is odd) is x itself: the conv takes part in x's
+    # gradient slot like any MFMA conv (ShuffleNetV2 DownBlock conv3, shufflenetv2.py:84-90)
+    slot, owner = _slot_for_conv(x) if (groups == 1 and cp == Cg) else (None, False)
+    y, stats = _ConvMFMA.apply(xn, wp, bp, stride, padding, groups, want_stats, 0, slot, owner,
                                None, None, None, padded)
     if op != cout_g and groups == 1 and _PAD_VIEW:
         # the real channels are a prefix: consumers read them in place (BatchNorm: row-strided
@@ -1706,25 +1761,30 @@ def add_act(a, b, act=None):
 
 class _DPNMerge(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, o, d):
+    def forward(ctx, x, o, d, slot=None):
         y = _C().dpn_merge_fwd(x, o, d)
         ctx.save_for_backward(y)
         ctx.geom = (x.shape[-1], o.shape[-1], d)
+        ctx.slot = slot
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
         dx, do = _C().dpn_merge_bwd(dy.contiguous(), y, *ctx.geom)
-        return dx, do, None
+        if ctx.slot is not None and ctx.slot.offer(dx):
+            dx = None        # the block input's conv1 dgrad adds it in its epilogue
+        return dx, do, None, None
 
 
 def dpn_merge(x, out, d):
     """DPN dual-path join relu(cat[x[:, :d] + out[:, :d], x[:, d:], out[:, d:]]) (dpn.py:29-31)
-    as one native pass each way (no channel-slice copies / separate add, ReLU and concat)."""
+    as one native pass each way (no channel-slice copies / separate add, ReLU and concat).
+    With an identity shortcut ``x`` is the block input, also read by conv1: its gradient from
+    the join is handed to conv1's dgrad epilogue (GradSlot) instead of an autograd add."""
     if _ref(x) or d % 8 or x.shape[1] % 8 or out.shape[1] % 8:
         return torch.cat([add_act(x[:, :d], out[:, :d], "relu"), relu(x[:, d:]), relu(out[:, d:])], 1)
-    return to_nchw(_DPNMerge.apply(to_nhwc(x), to_nhwc(out), d))
+    return to_nchw(_DPNMerge.apply(to_nhwc(x), to_nhwc(out), d, _slot_for_residual(x)))
 
 
 # ---------------------------------------------------------------------------- pooling
@@ -1880,9 +1940,10 @@ class _AvgPool(torch.autograd.Function):
 
 class _MaxPool(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p):
+    def forward(ctx, x, k, s, p, slot=None):
         y, arg = _C().maxpool_fwd(x, k, s, p)
         ctx.cfg = (x.shape[1], x.shape[2], k, s, p)
+        ctx.slot = slot
         ctx.save_for_backward(arg)
         ctx.mark_non_differentiable(arg)
         return y
@@ -1891,7 +1952,12 @@ class _MaxPool(torch.autograd.Function):
     def backward(ctx, dy):
         (arg,) = ctx.saved_tensors
         H, W, k, s, p = ctx.cfg
-        return _C().maxpool_bwd(dy.contiguous(), arg, H, W, k, s, p), None, None, None
+        dx = _C().maxpool_bwd(dy.contiguous(), arg, H, W, k, s, p)
+        if ctx.slot is not None and ctx.slot.offer(dx):
+            # (GoogLeNet's Inception pool branch, googlenet.py:41-45: its input gradient joins the
+            # sibling convs' dgrad epilogues instead of an autograd add)
+            dx = None
+        return dx, None, None, None, None
 
 
 def _pair1(v):
@@ -1908,10 +1974,10 @@ def avg_pool2d(x, kernel_size, stride=None, padding=0):
     if _ref(x):
         return F.avg_pool2d(x, k, s, p)
     H, W = x.shape[2], x.shape[3]
+    if k == 1 and s == 1 and p == 0:
+        return x           # (vgg.py:33's AvgPool2d(1, 1): identity, no pass — also on a 1x1 map)
     if p == 0 and k == H and k == W:
         return global_avg_pool(x)
-    if k == 1 and s == 1 and p == 0:
-        return x
     return to_nchw(_AvgPool.apply(to_nhwc(x), k, s, p))
 
 
@@ -1921,7 +1987,7 @@ def max_pool2d(x, kernel_size, stride=None, padding=0):
     p = _pair1(padding)
     if _ref(x):
         return F.max_pool2d(x, k, s, p)
-    return to_nchw(_MaxPool.apply(to_nhwc(x), k, s, p))
+    return to_nchw(_MaxPool.apply(to_nhwc(x), k, s, p, _slot_for_residual(x)))
 
 
 def adaptive_avg_pool2d(x, output_size):
@@ -2281,6 +2347,13 @@ def cat_shuffle2(a, b):
     return to_nchw(_Interleave2.apply(to_nhwc(a), to_nhwc(b)))
 
 
+def _nhwc_rows(t):
+    """Dense NHWC rows, possibly wider than C (row stride >= C, dense outer strides): the layout
+    the row-strided native kernels accept, at any channel count."""
+    return (t.dim() == 4 and t.stride(3) == 1 and t.stride(2) >= t.shape[3]
+            and t.stride(1) == t.shape[2] * t.stride(2) and t.stride(0) == t.shape[1] * t.stride(1))
+
+
 class _Interleave2Split(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, b, pad_hi):
@@ -2293,8 +2366,10 @@ class _Interleave2Split(torch.autograd.Function):
         dlo = dlo.contiguous() if dlo is not None else torch.zeros_like(ref)
         if dhi is None:
             dhi = torch.zeros_like(ref)
-        elif _rows_view(dhi) is not dhi:
-            dhi = dhi.contiguous()   # (a row-strided NHWC view, e.g. a padded conv's dX, is read in place)
+        elif not _nhwc_rows(dhi):
+            dhi = dhi.contiguous()
+        # (a row-strided NHWC view — at the odd half widths 58 / 116 the prefix of the padded
+        # conv's dX — is read in place: the kernel takes any row stride >= C)
         da, db = _C().deinterleave2_split(dlo, dhi)
         return da, db, None
 
@@ -2386,6 +2461,14 @@ def _rows_view(t):
     return t.contiguous()
 
 
+@functools.lru_cache(maxsize=None)
+def _bn_rows_max_c():
+    """Widest channel count the native row-tiled BatchNorm kernels take (0 with PCA_BN_ROWS=0):
+    the only BN kernels that read / write row-strided (slab) operands."""
+    lib = _C()
+    return int(lib.bn_rows_max_c()) if hasattr(lib, "bn_rows_max_c") else 0
+
+
 def _slab_alias(buf, c0, c1):
     """A fresh tensor over channels [c0, c1) of the NHWC slab ``buf`` — not an autograd view of
     it: slices are written by native kernels (no in-place op autograd could see), and each slice
@@ -2412,7 +2495,10 @@ class ChannelSlab:
 
     @staticmethod
     def usable(x, widths):
+        # (the BatchNorms reading / writing the slices row-strided need the row-tiled kernels:
+        # slab width within their reach, and PCA_BN_ROWS not disabled)
         return (not _ref(x) and x.dim() == 4 and all(w % 8 == 0 for w in widths)
+                and sum(widths) <= _bn_rows_max_c()
                 and os.environ.get("PCA_ZERO_COPY_CAT", "1") != "0")
 
     def dest(self, i):
@@ -2424,21 +2510,43 @@ class ChannelSlab:
             if (pn.untyped_storage().data_ptr() != self.buf.untyped_storage().data_ptr()
                     or pn.storage_offset() != self.buf.storage_offset() + o or pn.shape[-1] != w):
                 raise RuntimeError("ChannelSlab.cat: part was not produced into its slab slice")
+        self.junctions = [getattr(p, "_pca_junction", None) for p in parts]
         return to_nchw(_SlabCat.apply(self, *pns))
 
 
+class _Junction(GradSlot):
+    """Gradient junction of a slab slice that also fed a dense copy (DLA / SimpleDLA Root: the left
+    child's output is read by the root conv through the slab and by the right child through
+    ``dense_copy``). The slab's backward (it runs first: the root is later in the forward) leaves
+    the slice's gradient here instead of returning it; the copy's backward adds its own gradient
+    in one native pass (``add_rows``) and returns the sum — no autograd add."""
+    __slots__ = ()
+
+
 class _CopyRows(torch.autograd.Function):
-    """Dense copy of a row-strided NHWC slab slice (one native pass; identity backward)."""
+    """Dense copy of a row-strided NHWC slab slice (one native pass; identity backward, or the
+    junction sum when the slab left the slice's gradient in ``junction``)."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, junction=None):
         out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
         _C().copy_rows(x, out)
+        ctx.junction = junction
         return out
 
     @staticmethod
     def backward(ctx, g):
-        return g
+        j = ctx.junction
+        if j is not None:
+            other = j.take()
+            if other is not None and g is not None and g.dtype == other.dtype:
+                gv = g if _nhwc_rows(g) else g.contiguous()
+                out = torch.empty(g.shape, dtype=g.dtype, device=g.device)
+                _C().add_rows(other, gv, out)
+                return out, None
+            if other is not None:
+                g = other if g is None else g + other
+        return g, None
 
 
 def dense_copy(x):
@@ -2446,20 +2554,35 @@ def dense_copy(x):
     consumers that need dense operands (the MFMA convs' A side, residual adds)."""
     if _ref(x):
         return x
-    return to_nchw(_CopyRows.apply(x.permute(0, 2, 3, 1)))
+    j = None
+    if torch.is_grad_enabled() and x.requires_grad and x.shape[1] % 8 == 0:
+        j = _Junction()
+        x._pca_junction = j
+    return to_nchw(_CopyRows.apply(x.permute(0, 2, 3, 1), j))
 
 
 class _SlabCat(torch.autograd.Function):
     @staticmethod
     def forward(ctx, slab, *parts):
         ctx.offs = slab.offs
+        ctx.junctions = getattr(slab, "junctions", None) or [None] * len(parts)
         return _slab_alias(slab.buf, 0, slab.offs[-1])
 
     @staticmethod
     def backward(ctx, dy):
-        # dy: NHWC-shaped gradient of the slab; producer i gets its channel range as a view
+        # dy: NHWC-shaped gradient of the slab; producer i gets its channel range as a view —
+        # or, when part i also fed a dense copy, the view waits in that junction for the copy's
+        # gradient (summed there in one native pass)
         o = ctx.offs
-        return (None,) + tuple(dy[..., o[i]:o[i + 1]] for i in range(len(o) - 1))
+        out = []
+        for i in range(len(o) - 1):
+            v = dy[..., o[i]:o[i + 1]]
+            j = ctx.junctions[i]
+            if (j is not None and v.dtype == COMPUTE_DTYPE and _nhwc_rows(v)
+                    and v.shape[-1] % 8 == 0 and j.offer(v)):
+                v = None
+            out.append(v)
+        return (None,) + tuple(out)
 
 
 class DenseSlab:
@@ -2481,8 +2604,12 @@ class DenseSlab:
 
     @staticmethod
     def usable(x0, growth, layers):
+        # every suffix BatchNorm reads up to the whole slab row-strided: the final width must be
+        # within the row-tiled kernels' reach (DenseNet161's dense3 / dense4 reach 2112 / 2208
+        # channels and keep the copying concat)
         return (not _ref(x0) and x0.dim() == 4 and x0.dtype == COMPUTE_DTYPE and growth % 8 == 0
-                and x0.shape[1] % 8 == 0 and os.environ.get("PCA_ZERO_COPY_CAT", "1") != "0")
+                and x0.shape[1] % 8 == 0 and x0.shape[1] + growth * layers <= _bn_rows_max_c()
+                and os.environ.get("PCA_ZERO_COPY_CAT", "1") != "0")
 
     @staticmethod
     def _suffix(t_nhwc, slot):

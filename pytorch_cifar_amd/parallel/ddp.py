@@ -249,6 +249,10 @@ class DistributedDataParallel(nn.Module):
         b.launched = True
         if not self._collectives:
             return
+        # deferred weight-gradient slab reductions (ops/functional.py) complete this bucket's
+        # gradients: one batched launch on the compute stream, before the fork orders the
+        # collective after it
+        F.flush_wgrads()
         self._fork()
         with self._stream_ctx():
             if b.low is not None:

@@ -872,3 +872,35 @@ def test_dgrad_compact_s2_addend(C, N, H, Cin, Cout, cfg):
             assert torch.allclose(p1.sum(0), p2.sum(0), rtol=1e-4, atol=1e-3)
     finally:
         C.set_conv_tile(0, -1)
+
+
+@pytest.mark.parametrize("HW,Cc", [(32, 192), (16, 64), (8, 832), (4, 24)])
+def test_maxpool3s1_rolling_ties(C, HW, Cc):
+    """The rolling 3x3 / stride-1 / pad-1 max pool (csrc/pool.hip, GoogLeNet's Inception pool
+    branch) on data full of ties: forward values exact, the gradient lands on the first maximum
+    of each window in (kh, kw) order — where torch's fp32 max_pool2d puts it — and sums match."""
+    torch.manual_seed(7)
+    x = torch.randint(-3, 4, (3, Cc, HW, HW), device="cuda").float().requires_grad_(True)
+    ref = F.max_pool2d(x, 3, 1, 1)
+    dy = torch.randint(-4, 5, ref.shape, device="cuda").float()
+    (g,) = torch.autograd.grad(ref, x, dy)
+    xn = nhwc(x.detach()).bfloat16()
+    y, arg = C.maxpool_fwd(xn, 3, 1, 1)
+    assert torch.equal(nchw(y).float(), ref.detach())
+    dx = C.maxpool_bwd(nhwc(dy).bfloat16(), arg, HW, HW, 3, 1, 1)
+    assert torch.equal(nchw(dx).float(), g)     # small integers: every sum is exact in bf16
+
+
+@pytest.mark.parametrize("k,HW,Cc", [(2, 32, 64), (2, 16, 456), (4, 8, 24), (8, 8, 1024)])
+def test_avgpool_window_eq_stride(C, k, HW, Cc):
+    """Vectorized k == s average pool (csrc/pool.hip: DenseNet transitions, pooled heads)."""
+    torch.manual_seed(8)
+    x = bf(torch.randn(4, Cc, HW, HW, device="cuda")).requires_grad_(True)
+    ref = F.avg_pool2d(x.float(), k, k, 0)
+    dy = bf(torch.randn_like(ref))
+    (g,) = torch.autograd.grad(ref, x, dy)
+    xn = nhwc(x.detach()).bfloat16()
+    y = C.avgpool_fwd(xn, k, k, 0)
+    assert rel_err(nchw(y), ref) < 4e-3
+    dx = C.avgpool_bwd(nhwc(dy).bfloat16(), HW, HW, k, k, 0)
+    assert rel_err(nchw(dx), g) < 4e-3

@@ -40,7 +40,7 @@ def _run(model, x, y, device, stock=False):
     return out.float()
 
 
-def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True, warm=0,
+def compare_model(ctor, batch=32, factor=3.0, slack=0.01, check_buffers=True, warm=0,
                   return_models=False):
     torch.manual_seed(0)
     ref = ctor()
@@ -65,8 +65,8 @@ def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True, wa
     e_n, e_s = rel(out_n, out_r), rel(out_s, out_r)
     assert e_n <= factor * e_s + slack, f"logits: native {e_n:.4f} vs stock-bf16 {e_s:.4f}"
     gr, gn, gs = _grads(ref), _grads(native), _grads(stock)
-    # absolute floor: a parameter whose gradient nearly cancels over the batch (tiny norm, e.g.
-    # an SE bias) has a meaningless relative error; compare it against the typical grad norm
+    # a parameter whose fp32 gradient is numerically zero (norm < 1e-6 x the median gradient
+    # norm: e.g. a bias feeding a training-mode BatchNorm) has no meaningful relative error
     norms = sorted(g.norm().item() for g in gr.values() if g is not None)
     scale = norms[len(norms) // 2] if norms else 0.0
     # relative-error floor: the squeeze-excite MLP gradients (SENet / RegNetY / EfficientNet)
@@ -91,7 +91,7 @@ def compare_model(ctor, batch=32, factor=3.0, slack=0.03, check_buffers=True, wa
             continue
         en, es = errs[name]
         es = max(es, floor[_se(name)]) if _se(name) else es
-        small = (gn[name].detach().float().cpu() - g).norm().item() <= 0.02 * scale
+        small = g.norm().item() < 1e-6 * scale
         if en > factor * es + slack and not small:
             bad.append((name, round(en, 4), round(es, 4)))
     assert not bad, f"grads worse than stock bf16 (name, native, stock): {bad[:10]}"
@@ -149,7 +149,12 @@ def test_resnet18_trains():
 GPU_ZOO = ["LeNet", "VGG11", "PreActResNet18", "GoogLeNet", "densenet_cifar", "ResNeXt29_2x64d",
            "MobileNet", "MobileNetV2", "DPN26", "SENet18", "EfficientNetB0", "RegNetX_200MF",
            "RegNetY_400MF", "SimpleDLA", "DLA", "PNASNetA", "PNASNetB", "ShuffleNetG2",
-           "ShuffleNetV2_1", "ResNet50", "ResNeXt29_32x4d"]
+           "ShuffleNetV2_1", "ResNet50", "ResNeXt29_32x4d",
+           # the reference's documented workload (main_dist.py:136, train.sh) and the deep / wide
+           # variants: DenseNet161's dense3 / dense4 (2112 / 2208 channels) exceed the row-tiled BN
+           # kernels' 2048 and must take the copying concat there
+           "ResNet152", "PreActResNet152", "DenseNet121", "DenseNet161", "DenseNet201", "DPN92",
+           "ResNeXt29_8x64d", "VGG19"]
 
 
 @pytest.fixture

@@ -25,9 +25,40 @@ CONFIGS = [("ResNet18", 1024), ("ResNet18", 512), ("ResNet18", 256), ("ResNet18"
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "pytorch_cifar_amd", "tune", "mi355x.json"))
+    ap.add_argument("--configs", default="",
+                    help="Model:batch,... to measure instead of the BASELINE set")
+    ap.add_argument("--merge", nargs="*", default=None,
+                    help="keep the rows of --out and add only geometries it lacks: from these "
+                         "PCA_TUNE_CACHE files if given (no GPU needed), else measured")
     args = ap.parse_args()
+    configs = ([(c.split(":")[0], int(c.split(":")[1])) for c in args.configs.split(",")]
+               if args.configs else CONFIGS)
     rows, runs = {}, []
-    for model, batch in CONFIGS:
+    old = None
+    if args.merge is not None:
+        with open(args.out) as fh:
+            old = json.load(fh)
+        for r in old["rows"]:
+            rows[tuple(r[:14])] = r
+        runs = list(old.get("configs", []))
+        if args.merge:
+            added = 0
+            for path in args.merge:
+                with open(path) as fh:
+                    for r in json.load(fh):
+                        if tuple(r[:14]) not in rows:
+                            rows[tuple(r[:14])] = r
+                            added += 1
+                runs.append({"cache": os.path.basename(path)})
+            from pytorch_cifar_amd.engine.tuning import selection_hash
+
+            old.update(rows=sorted(rows.values()), configs=runs,
+                       hash=selection_hash(rows.values()))
+            with open(args.out, "w") as fh:
+                json.dump(old, fh, indent=0)
+            print("merged", added, "rows ->", len(rows), "hash", old["hash"])
+            return
+    for model, batch in configs:
         with tempfile.TemporaryDirectory() as d:
             cache = os.path.join(d, "tune.json")
             env = dict(os.environ, PCA_TUNE_TABLE="0", PCA_TUNE_CACHE=cache)
@@ -39,14 +70,19 @@ def main():
             with open(cache) as fh:
                 got = json.load(fh)
             for r in got:
-                rows[tuple(r[:14])] = r
+                if old is None or tuple(r[:14]) not in rows:
+                    rows[tuple(r[:14])] = r
             runs.append({"model": model, "batch": batch, "rows": len(got)})
             print(model, batch, len(got), flush=True)
     from pytorch_cifar_amd import _native
     from pytorch_cifar_amd.engine.tuning import selection_hash
 
     lib = _native.lib()
-    out = {"version": lib.tune_version(), "arch": "gfx950", "configs": runs,
+    import torch
+
+    props = torch.cuda.get_device_properties(0)
+    out = {"version": lib.tune_version(), "arch": "gfx950", "cus": props.multi_processor_count,
+           "configs": runs,
            "rows": sorted(rows.values()), "hash": selection_hash(rows.values())}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
