@@ -486,7 +486,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     const float* __restrict__ gamma2, int training, float* __restrict__ dgamma,
     float* __restrict__ dbeta, float* __restrict__ dgamma2, float* __restrict__ dbeta2,
     float* __restrict__ coef, int accumulate, float* __restrict__ zero1, int zero1_n,
-    float* __restrict__ zero2, int zero2_n) {
+    float* __restrict__ zero2, int zero2_n, float* __restrict__ dbias) {
   __shared__ float red[16][64][3];
   // block 0 also clears the forward accumulators this BN consumed (sharded-sum mode)
   if (blockIdx.x == 0) {
@@ -536,6 +536,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     float* dbo = b == 0 ? dbeta : dbeta2;
     if (dgo) dgo[c] = accumulate ? dgo[c] + dg : dg;
     if (dbo) dbo[c] = accumulate ? dbo[c] + db : db;
+    // bias of the conv feeding this BN (its only consumer): sum_m dY = A*sum dz + B*sum y + D*M
+    if (dbias && b == 0) dbias[c] += A * db + Bc * (count * mean) + D * count;
   }
 }
 
@@ -776,6 +778,7 @@ struct BnFin {
   int zero_n;
   const float* krow;     // forward: the shift K the producers subtracted (acc K row), or nullptr
   float* pilot;          // forward: block 0 writes the batch mean here (the next step's K)
+  float* dbias;          // backward: += sum_m dY (bias gradient of the conv feeding this BN)
 };
 
 // The fold of the R shard rows is spread over the block: TPC lanes (consecutive threads, a
@@ -861,6 +864,8 @@ __device__ __forceinline__ void bn_fin_backward(const BnFin& f, const BnFin& f2,
       if (blockIdx.x == 0) {
         if (b.dgamma) b.dgamma[c] += dg;
         if (b.dbeta) b.dbeta[c] += db;
+        if (k == 0 && f.dbias)
+          f.dbias[c] += o[c] * db + o[C + c] * (f.count * mean) + o[2 * C + c] * f.count;
       }
     }
   }
@@ -1045,6 +1050,14 @@ void bn_bwd_reduce_launch(const bf16* dout, const bf16* out, const uint8_t* mask
   }
 }
 
+// Bias gradient of the conv whose output this BN alone consumes (googlenet.py / vgg.py
+// Conv2d(bias=True) -> BatchNorm2d): added by the next BN-backward launches' finalize from the
+// per-channel sums they already hold — sum_m dY = A * sum dz + B * sum y + D * M with
+// sum y = M * mean — instead of a column-sum pass over dY (exactly 0 in exact arithmetic for a
+// training-mode BN; bindings scope it per call).
+static float* g_bn_dbias = nullptr;
+void set_bn_dbias(float* p) { g_bn_dbias = p; }
+
 void bn_bwd_finalize_launch(const float* stat, int R, int NS, int C, float count,
                             const float* aux, const float* gamma, const float* aux2,
                             const float* gamma2, int training, float* dgamma, float* dbeta,
@@ -1054,11 +1067,11 @@ void bn_bwd_finalize_launch(const float* stat, int R, int NS, int C, float count
   if (NS == 3)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<3>, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C,
                        count, aux, gamma, aux2, gamma2, training, dgamma, dbeta, dgamma2, dbeta2,
-                       coef, accumulate, zero1, zero1_n, zero2, zero2_n);
+                       coef, accumulate, zero1, zero1_n, zero2, zero2_n, g_bn_dbias);
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<2>, dim3(cdiv(C, 64)), dim3(1024), 0, st, stat, R, C,
                        count, aux, gamma, aux2, gamma2, training, dgamma, dbeta, dgamma2, dbeta2,
-                       coef, accumulate, zero1, zero1_n, zero2, zero2_n);
+                       coef, accumulate, zero1, zero1_n, zero2, zero2_n, g_bn_dbias);
 }
 
 void bn_bwd_apply_launch(const bf16* dout, const bf16* out, const uint8_t* mask, const bf16* y,
@@ -1165,6 +1178,7 @@ bool bn_bwd_apply_acc_launch(const bf16* dout, const uint8_t* mask, const bf16* 
     return false;
   BnFin f{acc, R, count, gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, aux, dgamma,
           dbeta, zero, zero_n};
+  f.dbias = g_bn_dbias;
   BnFin f2{acc, R, count, gamma2, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, aux2,
            dgamma2, dbeta2, zero2, zero2_n};
   const dim3 gr(acc_rows_grid(M, C)), bl(256);

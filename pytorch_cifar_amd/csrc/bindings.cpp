@@ -47,6 +47,7 @@ void wgrad_clear_tuned();
 std::vector<std::vector<int>> tune_export();
 void c64_set_prof(int64_t* p);
 int c64_grid_size(int N, int H);
+void set_bn_dbias(float* p);
 void copy_rows_launch(const bf16* src, int lds, bf16* dst, int ldd, int P, int C, hipStream_t st,
                       const bf16* add = nullptr, int lda = 0);
 // batchnorm.hip: row strides of the next BN launches' tensors (0 = dense; common.h BnLd)
@@ -58,7 +59,7 @@ void set_bn_ld(const BnLd& ld);
 int c64_version(int v);
 int tune_import(const std::vector<std::vector<int>>& rows);
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                       int groups, int Ho, int Wo);
+                       int groups, int Ho, int Wo, bool has_bias);
 void set_conv_tile(int kind, int idx);
 void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int, int, int, int,
                        int, int, int, int, hipStream_t, const bf16* addend, float* ws,
@@ -440,7 +441,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
       auto yt = at::empty({N, Ho, Wo, Cout}, x.options());
       Tensor stt, wst;
       if (want_stats) {
-        const int gm = pca::conv_fwd_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+        const int gm = pca::conv_fwd_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo,
+                                               has_bias0);
         stt = at::empty({gm, 2, Cout}, x.options().dtype(at::kFloat));
       }
       const int64_t n = pca::conv_fwd_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups,
@@ -459,7 +461,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
     check_acc(*stat_acc, acc_rows, 2, Cout);
     stats = *stat_acc;
   } else if (want_stats) {
-    const int gm = pca::conv_fwd_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
+    const int gm = pca::conv_fwd_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo,
+                                               has_bias0);
     stats = at::empty({gm, 2, Cout}, x.options().dtype(at::kFloat));
   }
   ShardScope shards(use_acc ? acc_rows : 0);
@@ -658,7 +661,10 @@ Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride,
                 "dw out shape");
     dw = *out;
   } else {
-    dw = at::zeros({Cout, KH, KW, Cin / groups}, x.options().dtype(at::kFloat));
+    // (zeroed by the runtime's fill on this stream, not an at::native kernel)
+    dw = at::empty({Cout, KH, KW, Cin / groups}, x.options().dtype(at::kFloat));
+    TORCH_CHECK(hipMemsetAsync(dw.data_ptr(), 0, dw.numel() * sizeof(float), cur_stream()) ==
+                    hipSuccess, "conv_wgrad: zero fill failed");
   }
   if (g_autotune && !stream_capturing(cur_stream()) &&
       pca::wgrad_needs_tune(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
@@ -1029,7 +1035,19 @@ std::vector<Tensor> bn_backward(const Tensor& dout, const optional<Tensor>& out,
                                 const optional<Tensor>& partial_in,
                                 const optional<Tensor>& acc_in, int acc_rows, bool acc_filled,
                                 const optional<Tensor>& zero1, const optional<Tensor>& zero2,
-                                const optional<Tensor>& dx_out, bool dx_acc) {
+                                const optional<Tensor>& dx_out, bool dx_acc,
+                                const optional<Tensor>& dbias_acc) {
+  // dbias_acc: the bias gradient of the conv that feeds only this BN, added by the finalize
+  float* dbias = nullptr;
+  if (dbias_acc.has_value() && dbias_acc->defined() && training) {
+    check_f32(*dbias_acc, "dbias_acc");
+    TORCH_CHECK(dbias_acc->numel() == y.size(-1), "dbias_acc size");
+    dbias = ptr<float>(*dbias_acc);
+  }
+  struct DbiasScope {
+    explicit DbiasScope(float* p) { pca::set_bn_dbias(p); }
+    ~DbiasScope() { pca::set_bn_dbias(nullptr); }
+  } dbias_scope(dbias);
   const bool extra = need_dres || (y2.has_value() && y2->defined()) ||
                      (dx_out.has_value() && dx_out->defined());
   const Tensor yd = bn_odd_strided(y) && extra ? y.contiguous() : y;
@@ -2152,7 +2170,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dbeta_acc"), py::arg("dgamma2_acc"), py::arg("dbeta2_acc"),
         py::arg("partial_in") = py::none(), py::arg("acc") = py::none(), py::arg("acc_rows") = 0,
         py::arg("acc_filled") = false, py::arg("zero1") = py::none(),
-        py::arg("zero2") = py::none(), py::arg("dx_out") = py::none(), py::arg("dx_acc") = false);
+        py::arg("zero2") = py::none(), py::arg("dx_out") = py::none(), py::arg("dx_acc") = false,
+        py::arg("dbias_acc") = py::none());
   m.def("bn_apply_acc", &bn_apply_acc, py::arg("y"), py::arg("acc"), py::arg("R"),
         py::arg("count"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
         py::arg("nbt"), py::arg("momentum"), py::arg("eps"), py::arg("res"), py::arg("y2"),

@@ -2298,9 +2298,12 @@ void conv_record_tuned(int kind, int N, int H, int W, int Cin, int Cout, int KH,
 int conv_tuned_count() { return (int)g_tuned.size(); }
 void conv_clear_tuned() { g_tuned.clear(); }
 
+// (must pick the kernel conv_fwd_launch picks: a biased 64->64 layer-1-shaped conv — VGG16/19's
+// second conv — runs on the igemm, whose statistics grid is larger than the c64 kernel's)
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                       int groups, int Ho, int Wo) {
-  if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+                       int groups, int Ho, int Wo, bool has_bias) {
+  if (g_igemm_override < 0 && !has_bias &&
+      conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
     return conv_c64_stat_rows(N, H);
   if (g_igemm_override < 0 && conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
     return conv_stem_stat_rows(N, H);

@@ -47,28 +47,41 @@ __device__ __forceinline__ void row_max3(const bf16* row, int w, int W, int C, f
   }
 }
 
+// A thread walks a strip of kStrip rows (more threads in flight than whole columns: the first
+// version, one thread per column, ran GoogLeNet's 32x32 pools latency-bound; a strip re-reads
+// one halo row on each side).
+constexpr int kStrip = 8;
+
 __global__ __launch_bounds__(256) void maxpool3s1_fwd_kernel(const bf16* __restrict__ x,
                                                              Pool3Geom g, bf16* __restrict__ y,
                                                              uint8_t* __restrict__ arg) {
-  const int total = g.N * g.W * g.G;
+  const int strips = (g.H + kStrip - 1) / kStrip;
+  const int total = g.N * strips * g.W * g.G;
   const int C = g.G * 8;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int gi = i % g.G;
-    const int q = i / g.G;
+    int q = i / g.G;
     const int w = q % g.W;
-    const int n = q / g.W;
+    q /= g.W;
+    const int sidx = q % strips;
+    const int n = q / strips;
+    const int r0 = sidx * kStrip, r1 = min(r0 + kStrip, g.H);
     const bf16* xn = x + (size_t)n * g.H * g.W * C + gi * 8;
     const size_t ybase = ((size_t)n * g.H * g.W + w) * C + gi * 8;
-    // rows ih-1 (p), ih (c), ih+1 (nx) of the current output row ih
+    // row maxima of input rows oh-1 (p), oh (c), oh+1 (n) for the current output row oh
     float mp[8], mc[8], mn[8];
     uint32_t ap[8], ac[8], an[8];
+    if (r0 > 0) {
+      row_max3(xn + (size_t)(r0 - 1) * g.W * C, w, g.W, C, mp, ap);
+    } else {
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      mp[v] = -INFINITY;
-      ap[v] = 0;
+      for (int v = 0; v < 8; ++v) {
+        mp[v] = -INFINITY;
+        ap[v] = 0;
+      }
     }
-    row_max3(xn, w, g.W, C, mc, ac);
-    for (int oh = 0; oh < g.H; ++oh) {
+    row_max3(xn + (size_t)r0 * g.W * C, w, g.W, C, mc, ac);
+    for (int oh = r0; oh < r1; ++oh) {
       if (oh + 1 < g.H) {
         row_max3(xn + (size_t)(oh + 1) * g.W * C, w, g.W, C, mn, an);
       } else {
@@ -143,27 +156,33 @@ __device__ __forceinline__ void out_row_parts(const bf16* dyr, const uint8_t* ar
 __global__ __launch_bounds__(256) void maxpool3s1_bwd_kernel(const bf16* __restrict__ dy,
                                                              const uint8_t* __restrict__ arg,
                                                              Pool3Geom g, bf16* __restrict__ dx) {
-  const int total = g.N * g.W * g.G;
+  const int strips = (g.H + kStrip - 1) / kStrip;
+  const int total = g.N * strips * g.W * g.G;
   const int C = g.G * 8;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int gi = i % g.G;
-    const int q = i / g.G;
+    int q = i / g.G;
     const int w = q % g.W;
-    const int n = q / g.W;
+    q /= g.W;
+    const int sidx = q % strips;
+    const int n = q / strips;
+    const int r0 = sidx * kStrip, r1 = min(r0 + kStrip, g.H);
     const size_t nb = (size_t)n * g.H * g.W * C + gi * 8;
     const size_t xo = nb + (size_t)w * C;
     // Output row oh feeds input row oh - 1 + kh with its kh part. Input row ih is summed in the
     // generic kernel's order kh 0 (output row ih + 1), kh 1 (row ih), kh 2 (row ih - 1), so it is
     // complete once row ih + 1 has been read: h1 / h2 hold the kh 1 / kh 2 parts of the row
-    // being completed, n2 the kh 2 part of the row after it.
+    // being completed, n2 the kh 2 part of the row after it. The strip's input rows [r0, r1)
+    // read output rows r0 - 1 .. r1.
     float h1[8], h2[8], n2[8];
 #pragma unroll
     for (int v = 0; v < 8; ++v) h1[v] = h2[v] = n2[v] = 0.f;
-    for (int oh = 0; oh < g.H; ++oh) {
+    const int o0 = max(r0 - 1, 0), o1 = min(r1, g.H - 1);
+    for (int oh = o0; oh <= o1; ++oh) {
       float part[3][8];
       out_row_parts(dy + nb + (size_t)oh * g.W * C, arg + nb + (size_t)oh * g.W * C, w, g.W, C,
                     part);
-      if (oh > 0) {
+      if (oh - 1 >= r0) {
         float s[8];
 #pragma unroll
         for (int v = 0; v < 8; ++v) s[v] = ((0.f + part[0][v]) + h1[v]) + h2[v];
@@ -176,17 +195,19 @@ __global__ __launch_bounds__(256) void maxpool3s1_bwd_kernel(const bf16* __restr
         n2[v] = part[2][v];
       }
     }
-    float s[8];
+    if (r1 == g.H) {   // the last row has no kh 0 contributor
+      float s[8];
 #pragma unroll
-    for (int v = 0; v < 8; ++v) s[v] = (0.f + h1[v]) + h2[v];
-    *reinterpret_cast<uint4*>(dx + xo + (size_t)(g.H - 1) * g.W * C) = pack8(s);
+      for (int v = 0; v < 8; ++v) s[v] = (0.f + h1[v]) + h2[v];
+      *reinterpret_cast<uint4*>(dx + xo + (size_t)(g.H - 1) * g.W * C) = pack8(s);
+    }
   }
 }
 
 void maxpool3s1_fwd_launch(const bf16* x, int N, int H, int W, int C, bf16* y, uint8_t* arg,
                            hipStream_t st) {
   const Pool3Geom g{N, H, W, C / 8};
-  const int total = N * W * (C / 8);
+  const int total = N * ((H + kStrip - 1) / kStrip) * W * (C / 8);
   const int blocks = std::min((total + 255) / 256, 16384);
   hipLaunchKernelGGL(maxpool3s1_fwd_kernel, dim3(blocks), dim3(256), 0, st, x, g, y, arg);
 }
@@ -194,7 +215,7 @@ void maxpool3s1_fwd_launch(const bf16* x, int N, int H, int W, int C, bf16* y, u
 void maxpool3s1_bwd_launch(const bf16* dy, const uint8_t* arg, int N, int H, int W, int C, bf16* dx,
                            hipStream_t st) {
   const Pool3Geom g{N, H, W, C / 8};
-  const int total = N * W * (C / 8);
+  const int total = N * ((H + kStrip - 1) / kStrip) * W * (C / 8);
   const int blocks = std::min((total + 255) / 256, 16384);
   hipLaunchKernelGGL(maxpool3s1_bwd_kernel, dim3(blocks), dim3(256), 0, st, dy, arg, g, dx);
 }

@@ -42,8 +42,14 @@ class Conv2d(nn.Conv2d):
         if want_stats and self.__dict__.get("_pca_acc_ok") and OF.acc_enabled(self.out_channels, x.device):
             acc = OF.stat_acc(self, "fwd", self.out_channels, 2, x.device)
         pilot = OF.conv_pilot(self, x.device) if want_stats else None
+        brec = None
+        if (self.bias is not None and self.bias.requires_grad and self.training
+                and torch.is_grad_enabled() and not OF._ref(x)):
+            brec = OF.BiasRec(self.bias)
         y, stats = OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.groups,
-                             want_stats, acc, pilot)
+                             want_stats, acc, pilot, brec)
+        if brec is not None:
+            y._pca_bias_rec = brec
         if stats is not None:
             setattr(y, _STATS_ATTR, stats)
             y._pca_stats_src = self
@@ -119,6 +125,11 @@ class Sequential(nn.Sequential):
                 i += 1
                 continue
             x = m(x)
+            if (isinstance(m, Conv2d) and m.bias is not None and i + 1 < len(mods)
+                    and isinstance(mods[i + 1], BatchNorm2d)):
+                # only the next BatchNorm reads this conv output: its backward may deliver the
+                # conv's bias gradient (ops.functional.BiasRec)
+                x._pca_bias_sole = True
             i += 1
         return x
 

@@ -159,6 +159,19 @@ def _slot_for_conv(x):
     return s, False
 
 
+class BiasRec:
+    """Hand-off of a conv bias gradient to the BatchNorm that alone consumes the conv's output
+    (googlenet.py / vgg.py ``Conv2d(bias=True) -> BatchNorm2d``, the fused Sequential marks the
+    pair): the BN backward adds sum_m dY from the per-channel sums it already holds (its
+    finalize, csrc/batchnorm.hip set_bn_dbias) and the conv backward skips its column-sum pass."""
+    __slots__ = ("bias", "armed", "done")
+
+    def __init__(self, bias):
+        self.bias = bias
+        self.armed = False    # the conv kernel path can hand its bias gradient over
+        self.done = False     # the BN backward added it
+
+
 def _slot_for_residual(x):
     if not (_FUSE_GRAD and x is not None and x.requires_grad):
         return None
@@ -673,10 +686,13 @@ class _ConvMFMA(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, groups, want_stats, cin_pad, slot=None,
-                owner=False, bnsrc=None, acc=None, pilot=None, padded=None):
+                owner=False, bnsrc=None, acc=None, pilot=None, padded=None, brec=None):
         # padded = (wb, wt, remap): operands of the per-group zero-padded form of ``weight``
         # (_conv_group_padded, from the plan); the weight gradient is gathered back by ``remap``
         C = _C()
+        ctx.brec = brec
+        if brec is not None:
+            brec.armed = bias is not None and padded is None and not cin_pad
         ctx.padded = padded[2:] if padded is not None else None
         ctx.slot, ctx.owner = slot, owner
         ctx.bnsrc = bnsrc
@@ -736,7 +752,7 @@ class _ConvMFMA(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return (None,) * 14
+            return (None,) * 15
         C = _C()
         x, wt = ctx.saved_tensors
         stride, padding, groups, cin_pad, H, W = ctx.geom
@@ -758,9 +774,9 @@ class _ConvMFMA(torch.autograd.Function):
                     dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, add)
                 elif slot is None:
                     dx = _dgrad_bn(C, src, dy, wt, H, W, stride, padding, groups, None)
-                elif (slot.s2c and stride == 2 and padding == 0 and groups == 1 and
-                      wt.shape[1] == 1 and wt.shape[2] == 1 and H == 2 * dy.shape[1] and
-                      W == 2 * dy.shape[2]):
+                elif (slot.s2c and slot.grad is None and stride == 2 and padding == 0 and
+                      groups == 1 and wt.shape[1] == 1 and wt.shape[2] == 1 and
+                      H == 2 * dy.shape[1] and W == 2 * dy.shape[2]):
                     # 1x1 stride-2 projection shortcut: its dX is nonzero only at the even-even
                     # pixels — computed compact as a plain 1x1 dgrad (a GEMM, no parity classes
                     # writing zeros) and added by the owner's parity dgrad in its class 0
@@ -772,17 +788,23 @@ class _ConvMFMA(torch.autograd.Function):
                         dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups)
                 else:
                     # another consumer's gradient already waiting in the slot (GoogLeNet's
-                    # Inception input feeds three 1x1 convs and a max-pool): this dgrad adds it in
+                    # Inception input feeds three 1x1 convs and a max-pool; a DLA level-2 tree
+                    # input feeds two blocks with projection shortcuts): this dgrad adds it in
                     # its epilogue and hands the sum on, so the owner finally stores the total —
-                    # no autograd add between the branches
+                    # no autograd add between the branches. A compact stride-2 pending gradient
+                    # is added by a 3x3 / stride-2 dgrad's parity class 0 (or expanded by the
+                    # binding when the selected kernel cannot).
                     pend = slot.grad
-                    if (pend is None or getattr(pend, "_pca_s2c", False) or pend.dim() != 4
-                            or tuple(pend.shape) != (dy.shape[0], H, W, wt.shape[0])
-                            or not pend.is_contiguous() or pend.dtype != dy.dtype):
-                        pend = None
+                    s2c = pend is not None and getattr(pend, "_pca_s2c", False)
+                    want = ((dy.shape[0], H // 2, W // 2, wt.shape[0]) if s2c
+                            else (dy.shape[0], H, W, wt.shape[0]))
+                    if (pend is None or pend.dim() != 4 or tuple(pend.shape) != want
+                            or not pend.is_contiguous() or pend.dtype != dy.dtype
+                            or (s2c and (stride != 2 or H % 2 or W % 2))):
+                        pend, s2c = None, False
                     else:
                         slot.grad = None
-                    dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups, pend)
+                    dx = C.conv_dgrad(dy, wt, H, W, stride, padding, groups, pend, s2c)
                     if slot.offer(dx):
                         dx = None                # delivered through the owner's epilogue
 
@@ -794,6 +816,24 @@ class _ConvMFMA(torch.autograd.Function):
             # stem conv: dedicated small-Cin wgrad adds straight into the fp32 gradient
             sbuf = G.grad_buffer(weight)
             if sbuf is not None and C.stem_wgrad(x, dy, stride, padding, sbuf):
+                G.fire(weight)
+                weight = None
+        if weight is not None and weight.requires_grad and cin_pad and weight.is_leaf and groups == 1:
+            # other channel-padded convs (stems the dedicated kernel does not cover: GoogLeNet's
+            # 3 -> 192, ShuffleNetV2's 3 -> 24): the padded dW accumulates in a persistent buffer
+            # whose real entries one native remap adds into the arena and zeroes (its padding
+            # entries stay exact zeros: the padded input channels are zero) — no fill, no slice
+            # + autograd add
+            buf = G.grad_buffer(weight)
+            Co, Ci = weight.shape[0], weight.shape[1]
+            if buf is not None and tuple(buf.shape) == (Co, KH, KW, Ci):
+                pbuf = weight.__dict__.get("_pca_pad_dw")
+                if pbuf is None or pbuf.shape != (Co, KH, KW, cin_pad) or pbuf.device != x.device:
+                    pbuf = torch.zeros((Co, KH, KW, cin_pad), dtype=torch.float32, device=x.device)
+                    weight.__dict__["_pca_pad_dw"] = pbuf
+                C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, pbuf)
+                _weight_pad_remap(1, Co, Co, Ci, cin_pad, KH * KW).apply(
+                    pbuf, inverse=True, acc=buf, clear_src=True)
                 G.fire(weight)
                 weight = None
         if weight is not None and weight.requires_grad and ctx.padded is not None:
@@ -838,6 +878,8 @@ class _ConvMFMA(torch.autograd.Function):
                     dw_ret = dw.permute(0, 3, 1, 2)
         if side_first:
             do_dgrad()
+        if ctx.brec is not None and ctx.brec.done:
+            bias = None                      # added by the consuming BN's backward finalize
         if bias is not None and bias.requires_grad:
             bbuf = G.grad_buffer(bias) if bias.is_leaf else None
             if bbuf is not None:
@@ -849,7 +891,7 @@ class _ConvMFMA(torch.autograd.Function):
                     G.accumulate(bias, db)
                 else:
                     db_ret = db
-        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dw_ret, db_ret, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _ConvDirect(torch.autograd.Function):
@@ -976,7 +1018,7 @@ _DW_BN_FUSE = os.environ.get("PCA_DW_BN_FUSE", "0") == "1"
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False, acc=None,
-           pilot=None):
+           pilot=None, brec=None):
     """NCHW-shaped conv. On GPU returns (y, stats) where stats are BN partials (a slab tensor, or
     ``acc`` — a :class:`StatAcc` the epilogue added into — when one is given), or None. With
     ``pilot`` (the consuming BN's shift, :func:`link_pilot`) the MFMA paths sum x - pilot."""
@@ -1010,7 +1052,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, groups=1, want_stats=False
         slot, owner = _slot_for_conv(x)
         bnsrc = getattr(x, "_pca_bnsrc", None) if x.requires_grad else None
         y, stats = _ConvMFMA.apply(to_nhwc(x), weight, bias, stride, padding, groups, want_stats, 0,
-                                   slot, owner, bnsrc, acc if want_stats else None, pilot)
+                                   slot, owner, bnsrc, acc if want_stats else None, pilot, None,
+                                   brec)
         if want_stats and acc is not None:
             return to_nchw(y), acc
         return to_nchw(y), (stats if want_stats else None)
@@ -1257,7 +1300,7 @@ def add_bias(y_nhwc, bias):
 # -------------------------------------------------------------------------- batch norm
 class _BNCfg:
     __slots__ = ("bn", "bn2", "act", "training", "count", "src", "bacc", "faccs", "pilot", "pilot2",
-                 "dest", "dslot", "padslot")
+                 "dest", "dslot", "padslot", "brec")
 
     def __init__(self, bn, bn2, act, training, count):
         self.bn, self.bn2, self.act, self.training, self.count = bn, bn2, act, training, count
@@ -1268,6 +1311,7 @@ class _BNCfg:
         self.bacc = None      # the BN's backward StatAcc (sharded sums of dz, dz*xhat[, dz*xhat2])
         self.faccs = ()       # forward StatAccs this BN consumed (cleared by its backward kernel)
         self.padslot = None   # zero-padded conv output read in place: its dY goes back padded
+        self.brec = None      # BiasRec of the conv whose output only this BN reads
 
 
 def _bn_aux(C, bn, y, stats, training, count, pilot=None, kin=None, zero=None):
@@ -1440,6 +1484,12 @@ class _BatchNormAct(torch.autograd.Function):
         dgx = cfg.dslot.take() if cfg.dslot is not None else None
         if dgx is not None:
             dgx = _rows_view(dgx)
+        dbias = None
+        rec = cfg.brec
+        if rec is not None and rec.armed and cfg.training and ctx.needs_input_grad[0]:
+            cb = rec.bias
+            if cb.requires_grad and cb.is_leaf:
+                dbias = G.grad_buffer(cb)
         dy, dres, dy2, dg, db, dg2, db2 = C.bn_backward(
             dout, out, mask, y, aux,
             bn.weight.detach() if bn.weight is not None else None,
@@ -1447,7 +1497,10 @@ class _BatchNormAct(torch.autograd.Function):
             bn2.weight.detach() if (bn2 is not None and bn2.weight is not None) else None,
             ACT[cfg.act], cfg.training or bn.running_mean is None, ctx.has_res, g1, b1, g2, b2, part,
             acc.buf if acc is not None else None, acc.R if acc is not None else 0, filled,
-            zeros[0], zeros[1], dgx, dgx is not None)
+            zeros[0], zeros[1], dgx, dgx is not None, dbias)
+        if dbias is not None:
+            rec.done = True
+            G.fire(rec.bias)
         ps = cfg.padslot
         if ps is not None and dy is not None and not dy.is_contiguous() and dy.dim() == 4:
             # dY written into zero-padded rows (the binding's pad_dy): the producer conv takes
@@ -1547,6 +1600,8 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None,
         cfg.dest = out
     cfg.dslot = getattr(x, "_pca_dense_slot", None)
     cfg.padslot = getattr(x, "_pca_padslot", None) if not y.is_contiguous() else None
+    if training and residual is None and residual_bn is None and getattr(x, "_pca_bias_sole", False):
+        cfg.brec = getattr(x, "_pca_bias_rec", None)
     if cfg.dslot is not None and torch.is_grad_enabled():
         cfg.dslot.claimed = True
     if training and bn.running_mean is not None:

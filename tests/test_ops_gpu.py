@@ -703,3 +703,33 @@ def test_padded_conv_output_read_in_place(name, monkeypatch):
             assert torch.equal(res[0][1][n], res[1][1][n]), n
     finally:
         pca.set_deterministic(False)
+
+
+def test_conv_bias_grad_from_bn_backward():
+    """Conv2d(bias) -> BatchNorm2d (googlenet.py / vgg.py): the BN backward delivers the conv's
+    bias gradient from its per-channel sums (ops.functional.BiasRec) — exactly zero for a
+    training-mode BN up to rounding, as the fp32 oracle's is — and every other gradient is
+    unchanged; in eval mode the conv's own column-sum kernel runs and matches fp32."""
+    from pytorch_cifar_amd.nn import BatchNorm2d, Conv2d, ReLU, Sequential
+
+    torch.manual_seed(3)
+    ref = Sequential(Conv2d(16, 32, 3, padding=1), BatchNorm2d(32), ReLU(True))
+    for train in (True, False):
+        ref.train(train)
+        nat = copy.deepcopy(ref).cuda()
+        x = torch.randn(8, 16, 16, 16)
+        g = torch.randn(8, 32, 16, 16)
+        ref.zero_grad()
+        ref(x).backward(g)
+        out = nat(x.cuda().contiguous(memory_format=torch.channels_last))
+        out.backward(g.cuda().to(out.dtype).contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+        wscale = ref[0].weight.grad.norm().item()
+        db_n, db_r = nat[0].bias.grad.float().cpu(), ref[0].bias.grad
+        if train:
+            assert db_r.abs().max().item() < 1e-4 * wscale     # the oracle's is rounding noise
+            assert db_n.abs().max().item() < 1e-4 * wscale
+        else:
+            assert rel(db_n, db_r) < 2e-2
+        assert rel(nat[0].weight.grad, ref[0].weight.grad) < 2e-2
+        assert rel(nat[1].weight.grad, ref[1].weight.grad) < 2e-2
