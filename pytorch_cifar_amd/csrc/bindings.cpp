@@ -48,6 +48,11 @@ std::vector<std::vector<int>> tune_export();
 void c64_set_prof(int64_t* p);
 int c64_grid_size(int N, int H);
 void set_bn_dbias(float* p);
+bool winograd_applicable(int N, int H, int W, int Ci, int Co);
+int winograd_stat_rows(int N, int H, int W);
+void winograd_filter_launch(const float* w, int Co, int Ci, bf16* U, hipStream_t st);
+void winograd_fwd_launch(const bf16* x, const bf16* U, bf16* y, float* stats, int N, int H, int W,
+                         int Ci, int Co, hipStream_t st);
 void copy_rows_launch(const bf16* src, int lds, bf16* dst, int ldd, int P, int C, hipStream_t st,
                       const bf16* add = nullptr, int lda = 0);
 // batchnorm.hip: row strides of the next BN launches' tensors (0 = dense; common.h BnLd)
@@ -1260,6 +1265,35 @@ std::vector<Tensor> bn_backward_impl(const Tensor& dout, const optional<Tensor>&
   return {dy, dres, dy2, dgamma, dbeta, dgamma2, dbeta2};
 }
 
+// ---- fused Winograd F(2x2,3x3) forward (csrc/winograd.hip) ----
+// w: fp32 [Co][3][3][Ci] (the physical channels_last master) -> U bf16 [16][Co][Ci]
+Tensor winograd_filter(const Tensor& w) {
+  check_f32(w, "w");
+  TORCH_CHECK(w.dim() == 4 && w.size(1) == 3 && w.size(2) == 3, "w must be [Co][3][3][Ci]");
+  const int Co = w.size(0), Ci = w.size(3);
+  auto U = at::empty({16, Co, Ci}, w.options().dtype(at::kBFloat16));
+  pca::winograd_filter_launch(ptr<float>(w), Co, Ci, ptr<bf16>(U), cur_stream());
+  return U;
+}
+
+// x NHWC bf16, U [16][Co][Ci] -> (y NHWC bf16, BN partial sums [rows][2][Co] or empty)
+std::vector<Tensor> winograd_fwd(const Tensor& x, const Tensor& U, bool want_stats) {
+  check_bf16(x, "x");
+  check_bf16(U, "U");
+  TORCH_CHECK(x.dim() == 4 && U.dim() == 3 && U.size(0) == 16 && U.size(2) == x.size(3),
+              "winograd_fwd: x [N,H,W,Ci], U [16,Co,Ci]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), Ci = x.size(3), Co = U.size(1);
+  TORCH_CHECK(pca::winograd_applicable(N, H, W, Ci, Co),
+              "winograd_fwd: needs even H, W, Ci % 32 == 0, Co % 64 == 0");
+  auto y = at::empty({N, H, W, Co}, x.options());
+  Tensor st = want_stats ? at::empty({pca::winograd_stat_rows(N, H, W), 2, Co},
+                                     x.options().dtype(at::kFloat))
+                         : at::empty({0}, x.options().dtype(at::kFloat));
+  pca::winograd_fwd_launch(ptr<bf16>(x), ptr<bf16>(U), ptr<bf16>(y),
+                           want_stats ? ptr<float>(st) : nullptr, N, H, W, Ci, Co, cur_stream());
+  return {y, st};
+}
+
 // ------------------------------------------------------------------------------ misc
 Tensor nchw_to_nhwc(const Tensor& x, int Cp) {
   check_f32(x, "x");
@@ -2183,6 +2217,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "training BN(+act/+res/+BN2) with the finalize folded in from sharded accumulators");
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("copy_rows", &copy_rows, "dst <- src for NHWC tensors, either a row-strided channel slice");
+  m.def("winograd_filter", &winograd_filter, "U = G g G^T: fp32 [Co][3][3][Ci] -> bf16 [16][Co][Ci]");
+  m.def("winograd_fwd", &winograd_fwd, py::arg("x"), py::arg("U"), py::arg("want_stats") = false,
+        "fused Winograd F(2x2,3x3) 3x3/s1/p1 forward -> (y, BN partial sums [rows][2][Co])");
+  m.def("winograd_applicable", &pca::winograd_applicable);
   m.def("add_rows", &add_rows, "dst <- src + add for NHWC tensors (each dense or row-strided)");
   m.def("nhwc_to_nchw", &nhwc_to_nchw);
   m.def("augment", &augment);

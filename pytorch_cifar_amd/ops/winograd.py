@@ -2,8 +2,15 @@
 north star "implicit-GEMM / Winograd"; reference models/resnet.py:23-27, 98.9 % of ResNet-18's
 MACs).
 
-This is the measured *candidate* behind the decision recorded in README ("Winograd: measured and
-rejected"): input transform V = B^T d B of every 4x4 input tile (stride 2), filter transform
+Two forms:
+
+* :func:`conv3x3_winograd_fused` — the fused gfx950 kernel (csrc/winograd.hip): input transform
+  in registers per 4x4 patch, the 16 per-point GEMMs on MFMA out of LDS, output transform and the
+  BatchNorm-statistics epilogue in registers; the filter transform U = G g G^T is one small native
+  launch from the fp32 master. Measured per call against the tuned native direct kernels by
+  ``tools/winograd_ab.py`` (README records the decision).
+* the unfused stock-op harness below (einsum / bmm on hipBLASLt; also the CPU reference): input
+  transform V = B^T d B of every 4x4 input tile (stride 2), filter transform
 U = G g G^T, 16 batched GEMMs M = V U over the transform points (bf16 operands, fp32
 accumulation), output transform Y = A^T M A. It runs on stock PyTorch ops (einsum / bmm ->
 hipBLASLt) so the three stages can be timed separately against the native implicit-GEMM kernels
@@ -66,3 +73,13 @@ def conv3x3_winograd(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     N, H, W, _ = x.shape
     assert H % 2 == 0 and W % 2 == 0 and w.shape[2:] == (3, 3)
     return output_transform(batched_gemm(input_transform(x), filter_transform(w)), N, H, W)
+
+
+def conv3x3_winograd_fused(x: torch.Tensor, w: torch.Tensor, want_stats: bool = False):
+    """Fused native Winograd F(2x2,3x3) forward of NHWC bf16 ``x`` with ``w`` [Cout, Cin, 3, 3]
+    (any layout; fp32): returns (y NHWC bf16, BN partial sums [rows][2][Cout] or empty)."""
+    from .. import _native
+
+    C = _native.lib()
+    U = C.winograd_filter(w.float().permute(0, 2, 3, 1).contiguous())
+    return C.winograd_fwd(x.contiguous(), U, want_stats)

@@ -60,6 +60,16 @@ def main():
                    err_native=err(y_n), err_wino=err(y_w),
                    transformed_bytes=V.numel() * 2 + M.numel() * M.element_size())
         row["wino_total_us"] = row["wino_input_us"] + row["wino_gemm_us"] + row["wino_output_us"]
+        if C.winograd_applicable(N, H, H, Cin, Cout):
+            # the fused kernel (csrc/winograd.hip), with its BN-statistics epilogue like the
+            # native forward it would replace; the filter transform is timed apart (it would run
+            # once per step in the fused optimizer launch)
+            wp = w.permute(0, 2, 3, 1).contiguous()
+            Uf = C.winograd_filter(wp)
+            y_f, _ = C.winograd_fwd(x, Uf, True)
+            row.update(fused_us=timeit(lambda: C.winograd_fwd(x, Uf, True)),
+                       fused_filter_us=timeit(lambda: C.winograd_filter(wp)), err_fused=err(y_f))
+            row["fused_vs_native"] = row["fused_us"] / row["native_us"]
         print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in row.items()}), flush=True)
 
 
