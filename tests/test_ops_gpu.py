@@ -730,7 +730,15 @@ def test_conv_bias_grad_from_bn_backward():
             assert db_r.abs().max().item() < 1e-4 * wscale     # the oracle's is rounding noise
             assert db_n.abs().max().item() < 1e-4 * wscale
         else:
-            assert rel(db_n, db_r) < 2e-2
+            # eval: db = sum dY over the batch, a random-sign sum, so the few ReLU-mask flips of a
+            # bf16 conv output near zero move it by a few % against the fp32 oracle (as they move
+            # the weight gradient below). Exact check: the fp32 sum of dY under the native mask
+            bn = nat[1]
+            s = (bn.weight / torch.sqrt(bn.running_var + bn.eps)).detach().float()
+            m = (out.detach().float() > 0).float()
+            db_o = (g.cuda().to(out.dtype).float() * m * s.view(1, -1, 1, 1)).sum((0, 2, 3)).cpu()
+            assert rel(db_n, db_o) < 1e-2
+            assert rel(db_n, db_r) < 6e-2
         # (bf16 through a training-mode BN backward at batch 8: a few % like the stock bf16 path)
         assert rel(nat[0].weight.grad, ref[0].weight.grad) < 6e-2
         assert rel(nat[1].weight.grad, ref[1].weight.grad) < 6e-2
