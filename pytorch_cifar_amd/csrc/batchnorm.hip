@@ -96,7 +96,8 @@ template <int VEC>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ x, int M,
                                                        RowPar rp, int rows_per_block,
                                                        float* __restrict__ partial, int shards,
-                                                       float* __restrict__ krow, int ldx) {
+                                                       float* __restrict__ krow, int ldx, int ldc,
+                                                       bf16* __restrict__ dst, int ldd) {
   __shared__ float red[256 * VEC * 2];
   const int t = threadIdx.x;
   const int gx = t % rp.TPR, ry = t / rp.TPR;
@@ -114,6 +115,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ 
       for (int r = r0 + ry; r < r1; r += rp.RPP) {
         float f[VEC];
         load_vec<VEC>(x + (size_t)r * ldx + gi * VEC, f);
+        if (dst) store_vec<VEC>(dst + (size_t)r * ldd + gi * VEC, f);   // (bf16 -> fp32 -> bf16: exact)
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
           const float d = f[v] - k[v];
@@ -141,8 +143,8 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ 
       for (int v = 0; v < VEC; ++v) {
         const int c = gi * VEC + v;
         if (c < rp.C) {
-          stat_out(partial, blockIdx.x, shards, 2 * rp.C, c, s[v]);
-          stat_out(partial, blockIdx.x, shards, 2 * rp.C, rp.C + c, q[v]);
+          stat_out(partial, blockIdx.x, shards, 2 * ldc, c, s[v]);
+          stat_out(partial, blockIdx.x, shards, 2 * ldc, ldc + c, q[v]);
         }
       }
     }
@@ -779,6 +781,7 @@ struct BnFin {
   const float* krow;     // forward: the shift K the producers subtracted (acc K row), or nullptr
   float* pilot;          // forward: block 0 writes the batch mean here (the next step's K)
   float* dbias;          // backward: += sum_m dY (bias gradient of the conv feeding this BN)
+  int ldc;               // forward: row pitch of acc (0 = C; a channel suffix of a wider cache)
 };
 
 // The fold of the R shard rows is spread over the block: TPC lanes (consecutive threads, a
@@ -812,7 +815,7 @@ __device__ __forceinline__ void bn_fin_forward(const BnFin& f, int C, float* sc,
   for (int cb = 0; cb < C; cb += cpp) {
     const int c = cb + threadIdx.x / tpc;
     float sum[2];
-    fin_fold<2>(f.acc, f.R, 2, C, c, j, tpc, c < C, sum);
+    fin_fold<2>(f.acc, f.R, 2, f.ldc ? f.ldc : C, c, j, tpc, c < C, sum);
     if (j != 0 || c >= C) continue;
     const double m = (double)sum[0] / f.count;     // mean of x - K (shifted sums)
     double v = (double)sum[1] / f.count - m * m;
@@ -954,7 +957,27 @@ void bn_stats_launch(const bf16* x, int M, int C, float* partial, int P, hipStre
 #define PCA_STATS(V)                                                                              \
   case V: {                                                                                       \
     RowPar rp = make_rowpar(C, V);                                                                \
-    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial, g_stat_shards, krow, ld_or(g_bn_ld.y, C)); \
+    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, partial, g_stat_shards, krow, ld_or(g_bn_ld.y, C), C, (bf16*)nullptr, 0); \
+    break;                                                                                        \
+  }
+    PCA_STATS(8) PCA_STATS(4) PCA_STATS(2) PCA_STATS(1)
+#undef PCA_STATS
+  }
+}
+
+// Copy + statistics in one pass (DenseNet's concat slab, ops/functional.py DenseSlab): dst rows
+// (row stride ldd) <- x rows (ldx), and the channels' centred sums (K = row 0) added into R shard
+// rows of a wider [R][2][ldc] accumulator (acc points at this tensor's first channel) whose K row
+// starts at krow. The slab caches every channel's batch sums as it is produced, so each dense
+// layer's BatchNorm folds its suffix of the cache instead of re-reducing the whole suffix.
+void bn_stats_copy_launch(const bf16* x, int ldx, int M, int C, bf16* dst, int ldd, float* acc,
+                          int ldc, int R, int P, float* krow, hipStream_t st) {
+  const int rows = cdiv(M, P);
+  switch (bn_vec(C)) {
+#define PCA_STATS(V)                                                                              \
+  case V: {                                                                                       \
+    RowPar rp = make_rowpar(C, V);                                                                \
+    hipLaunchKernelGGL(bn_stats_kernel<V>, dim3(P), dim3(256), 0, st, x, M, rp, rows, acc, R, krow, ldx, ldc, dst, ldd); \
     break;                                                                                        \
   }
     PCA_STATS(8) PCA_STATS(4) PCA_STATS(2) PCA_STATS(1)
@@ -1137,13 +1160,18 @@ bool bn_apply_acc_launch(const bf16* y, int C, int M, float count, float* acc, i
                          int64_t* nbt2, float momentum2, float eps2, float* aux2, const bf16* res,
                          const bf16* y2, int act, bf16* out, uint8_t* mask, float* zero,
                          int zero_n, hipStream_t st, bool shifted, float* pilot, bool shifted2,
-                         float* pilot2) {
+                         float* pilot2, int acc_off, int acc_ld) {
   if (!(rows_enabled() && C % 8 == 0 && C <= 2048 &&
         (act == ACT_RELU || act == ACT_NONE || (act == ACT_SWISH && !res && !y2)) && !(res && y2)))
     return false;
   // K rows of shifted accumulators follow their [R][2][C] sums
   BnFin f{acc, R, count, gamma, beta, rmean, rvar, nbt, momentum, eps, aux, nullptr, nullptr, nullptr,
           zero, zero_n, shifted ? acc + (size_t)R * 2 * C : nullptr, pilot};
+  if (acc_ld > 0) {   // channels [acc_off, acc_off + C) of a [R][2][acc_ld] accumulator + K row
+    f.acc = acc + acc_off;
+    f.ldc = acc_ld;
+    f.krow = shifted ? acc + (size_t)R * 2 * acc_ld + acc_off : nullptr;
+  }
   BnFin f2{acc2, R2, count, gamma2, beta2, rmean2, rvar2, nbt2, momentum2, eps2, aux2, nullptr,
            nullptr, nullptr, nullptr, 0, (shifted2 && acc2) ? acc2 + (size_t)R2 * 2 * C : nullptr,
            pilot2};

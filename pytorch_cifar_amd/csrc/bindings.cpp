@@ -73,6 +73,7 @@ void conv_dgrad_launch(const bf16*, const bf16*, bf16*, int, int, int, int, int,
 int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
 void conv_set_bn_dual(const bf16* y2, const float* aux2);
+void conv_set_bn_ldy(int ld);
 void conv_set_addend_s2c(int on);
 bool conv_dgrad_s2c_ok(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
@@ -89,6 +90,8 @@ void wgrad_defer_scope(bool on);
 int wgrad_deferred_count();
 void wgrad_flush_launch(hipStream_t st);
 void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t, float* krow = nullptr);
+void bn_stats_copy_launch(const bf16* x, int ldx, int M, int C, bf16* dst, int ldd, float* acc,
+                          int ldc, int R, int P, float* krow, hipStream_t st);
 int colsum_launch(const float*, int, int, float*, hipStream_t);
 void bias_grad_fold_launch(const float*, int, int, int, float*, hipStream_t);
 void bn_finalize_launch(const float*, int, int, double, const float*, const float*, float*, float*,
@@ -117,7 +120,7 @@ bool bn_apply_acc_launch(const bf16* y, int C, int M, float count, float* acc, i
                          int64_t* nbt2, float momentum2, float eps2, float* aux2, const bf16* res,
                          const bf16* y2, int act, bf16* out, uint8_t* mask, float* zero,
                          int zero_n, hipStream_t st, bool shifted = false, float* pilot = nullptr,
-                         bool shifted2 = false, float* pilot2 = nullptr);
+                         bool shifted2 = false, float* pilot2 = nullptr, int acc_off = 0, int acc_ld = 0);
 bool bn_bwd_apply_acc_launch(const bf16* dout, const uint8_t* mask, const bf16* y, int C, int M,
                              float count, float* acc, int R, const float* aux, const float* gamma,
                              float* dgamma, float* dbeta, const float* aux2, const float* gamma2,
@@ -288,6 +291,35 @@ void copy_rows(const Tensor& src, const Tensor& dst) {
   const int C = src.size(3);
   TORCH_CHECK(C % 8 == 0, "copy_rows needs C % 8 == 0");
   pca::copy_rows_launch(ptr<bf16>(src), ls, ptr<bf16>(dst), ld, (int)(src.numel() / C), C, cur_stream());
+}
+
+// dst <- src (NHWC rows, either row-strided) and src's per-channel centred sums (K = row 0) added
+// into channels [acc_off, acc_off + C) of a [R][2][acc_ld] + K-row fp32 cache (zeroed by the
+// caller before the first producer of a step)
+static int acc_reduce_blocks(int M, int C, int R);
+void bn_stats_copy(const Tensor& src, const Tensor& dst, const Tensor& acc, int acc_off, int acc_ld,
+                   int R) {
+  const int ls = rows_ld(src, "src"), ld = rows_ld(dst, "dst");
+  TORCH_CHECK(src.sizes() == dst.sizes() && src.dim() == 4, "bn_stats_copy: shape mismatch");
+  const int C = src.size(3);
+  TORCH_CHECK(C % 8 == 0, "bn_stats_copy needs C % 8 == 0");
+  TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat && acc.is_contiguous(),
+              "acc must be contiguous fp32 on the GPU");
+  TORCH_CHECK(R >= 1 && acc_off >= 0 && acc_off + C <= acc_ld &&
+                  acc.numel() >= (int64_t)R * 2 * acc_ld + acc_ld,
+              "bn_stats_copy: acc must be [R][2][acc_ld] + K row");
+  const int M = (int)(src.numel() / C);
+  float* a = ptr<float>(acc);
+  pca::bn_stats_copy_launch(ptr<bf16>(src), ls, M, C, ptr<bf16>(dst), ld, a + acc_off, acc_ld, R,
+                            acc_reduce_blocks(M, C, R), a + (size_t)R * 2 * acc_ld + acc_off,
+                            cur_stream());
+}
+
+// t <- 0 on the current stream (the runtime's fill: a memset node under hipGraph capture)
+void zero_(const Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: contiguous GPU tensor");
+  TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()) ==
+                  hipSuccess, "zero_: fill failed");
 }
 
 // dst <- src + add (NHWC rows; every operand dense or row-strided)
@@ -533,8 +565,15 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
     }
   }
   const bool want_bn = bn_y.has_value() && bn_y->defined();
+  int bn_ldy = 0;   // y a row-strided channel slice (a DenseNet BatchNorm's slab suffix)
   if (want_bn) {
-    check_bf16(*bn_y, "bn_y");
+    if (bn_y->is_contiguous()) {
+      check_bf16(*bn_y, "bn_y");
+    } else {
+      TORCH_CHECK(bn_y->dim() == 4 && bn_y->size(-1) == Cin, "bn_y must be NHWC [N,H,W,Cin]");
+      bn_ldy = rows_ld(*bn_y, "bn_y");
+      TORCH_CHECK(!(bn_y2.has_value() && bn_y2->defined()), "row-strided bn_y: single BN only");
+    }
     TORCH_CHECK(bn_y->numel() == (int64_t)N * H * W * Cin, "bn_y must match dx (NHWC)");
     TORCH_CHECK(bn_mask.has_value() && bn_mask->defined() && bn_mask->is_contiguous() &&
                     bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == bn_y->numel(),
@@ -554,6 +593,15 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& wt, int H, i
     TORCH_CHECK(bn_aux2->numel() >= 2 * Cin, "bn_aux2 [mean|istd|...][C]");
   }
   const int NS = dual ? 3 : 2;
+  struct LdyScope {
+    bool on;
+    explicit LdyScope(int ld) : on(ld != 0) {
+      if (on) pca::conv_set_bn_ldy(ld);
+    }
+    ~LdyScope() {
+      if (on) pca::conv_set_bn_ldy(0);
+    }
+  } ldy_scope(bn_ldy);
   struct DualScope {
     bool on;
     DualScope(bool d, const bf16* y2, const float* a2) : on(d) {
@@ -939,13 +987,25 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
                                  const optional<Tensor>& nbt2, double momentum2, double eps2,
                                  int act, bool want_mask, const optional<Tensor>& zero,
                                  bool shifted, const optional<Tensor>& pilot, bool shifted2,
-                                 const optional<Tensor>& pilot2, const optional<Tensor>& out_opt) {
+                                 const optional<Tensor>& pilot2, const optional<Tensor>& out_opt,
+                                 int acc_off, int acc_ld) {
   const int ldy = rows_ld(y, "y");
   const int C = y.size(-1);
   const int M = y.numel() / C;
-  check_acc(acc, R, 2, C);
+  if (acc_ld > 0) {
+    // channels [acc_off, acc_off + C) of a wider [R][2][acc_ld] accumulator + its K row (a
+    // DenseNet slab's statistics cache): fused form only, single BN
+    check_f32(acc, "acc");
+    TORCH_CHECK(acc_off >= 0 && acc_off + C <= acc_ld && shifted &&
+                    acc.numel() >= (int64_t)R * 2 * acc_ld + acc_ld,
+                "acc view: [R][2][acc_ld] + K row, channels [acc_off, acc_off + C)");
+    TORCH_CHECK(!(y2.has_value() && y2->defined()), "acc view: single BN only");
+  } else {
+    check_acc(acc, R, 2, C);
+  }
   // shifted accumulators carry the producers' K row after the sums; the pilots get the means
-  TORCH_CHECK(!shifted || acc.numel() >= (int64_t)R * 2 * C + C, "shifted accumulator needs its K row");
+  TORCH_CHECK(acc_ld > 0 || !shifted || acc.numel() >= (int64_t)R * 2 * C + C,
+              "shifted accumulator needs its K row");
   for (const auto* pt : {&pilot, &pilot2})
     if (pt->has_value() && (*pt)->defined()) {
       check_f32(**pt, "pilot");
@@ -995,7 +1055,8 @@ std::vector<Tensor> bn_apply_acc(const Tensor& y, const Tensor& acc, int R, doub
       (float)momentum2, (float)eps2, dual ? ptr<float>(aux2) : nullptr, optr<bf16>(res),
       optr<bf16>(y2), act, ptr<bf16>(out), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr,
       has_zero ? ptr<float>(*zero) : nullptr, has_zero ? (int)zero->numel() : 0, st, shifted,
-      optr<float>(pilot), shifted2, optr<float>(pilot2));
+      optr<float>(pilot), shifted2, optr<float>(pilot2), acc_off, acc_ld);
+  TORCH_CHECK(fused || acc_ld == 0, "acc view needs the fused row kernels");
   if (!fused) {
     pca::bn_finalize_launch(ptr<float>(acc), R, C, count, optr<float>(gamma), optr<float>(beta),
                             ptr<float>(rmean), ptr<float>(rvar), optr<int64_t>(nbt),
@@ -2213,8 +2274,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rvar2"), py::arg("nbt2"), py::arg("momentum2"), py::arg("eps2"), py::arg("act"),
         py::arg("want_mask"), py::arg("zero") = py::none(), py::arg("shifted") = false,
         py::arg("pilot") = py::none(), py::arg("shifted2") = false, py::arg("pilot2") = py::none(),
-        py::arg("out") = py::none(),
+        py::arg("out") = py::none(), py::arg("acc_off") = 0, py::arg("acc_ld") = 0,
         "training BN(+act/+res/+BN2) with the finalize folded in from sharded accumulators");
+  m.def("zero_", &zero_, "t <- 0 (runtime fill on the current stream)");
+  m.def("bn_stats_copy", &bn_stats_copy, py::arg("src"), py::arg("dst"), py::arg("acc"),
+        py::arg("acc_off"), py::arg("acc_ld"), py::arg("R"),
+        "dst <- src (NHWC rows) with the channels' centred sums added into a wider sharded cache");
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("copy_rows", &copy_rows, "dst <- src for NHWC tensors, either a row-strided channel slice");
   m.def("winograd_filter", &winograd_filter, "U = G g G^T: fp32 [Co][3][3][Ci] -> bf16 [16][Co][Ci]");

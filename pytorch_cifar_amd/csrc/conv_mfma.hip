@@ -84,6 +84,9 @@ struct ConvGeom {
   // conv reading the same input (ResNet projection shortcut), nonzero only at the even-even
   // pixels: parity class 0 adds it at its own row index, the other classes add nothing
   int addend_s2c;
+  // fused BN reduce: row stride of bn_y (0 = dense, Co) — a DenseNet BatchNorm reads a channel
+  // suffix of its block's concat slab in place (ops/functional.py DenseSlab)
+  int bn_ldy;
 };
 
 // dz = dX * relu'(y), accumulated as (sum dz, sum dz * xhat) for 8 channels
@@ -692,7 +695,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
         e.av = *reinterpret_cast<const uint4*>(addend + oa);
       }
       if (bnf) {
-        e.yv = *reinterpret_cast<const uint4*>(g.bn_y + e.o);
+        const size_t yo = g.bn_ldy ? (e.ok ? pix * g.bn_ldy + (size_t)grp * g.Cn + gc : 0) : e.o;
+        e.yv = *reinterpret_cast<const uint4*>(g.bn_y + yo);
         e.mk = g.bn_mask[e.o >> 3];
       }
       if (dual) e.y2v = *reinterpret_cast<const uint4*>(g.bn_y2 + e.o);
@@ -737,7 +741,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
 #else
 #pragma unroll 1
     for (int it0 = 0; it0 < EIT; it0 += EU) {
-      size_t o[EU];
+      size_t o[EU], yo[EU];
       bool ok[EU];
       uint4 av[EU], yv[EU], y2v[EU];
       uint8_t mk[EU];
@@ -754,6 +758,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
           pix = ((size_t)n * g.Ho + 2 * h + ph) * g.Wo + 2 * w + pw;
         }
         o[u] = ok[u] ? pix * g.Co + (size_t)grp * g.Cn + gc : 0;
+        yo[u] = g.bn_ldy ? (ok[u] ? pix * g.bn_ldy + (size_t)grp * g.Cn + gc : 0) : o[u];
       }
       const bool add_on = addend != nullptr && (!PARITY || !g.addend_s2c || cls == 0);
       if (add_on) {
@@ -767,7 +772,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_kernel(const bf16* __
       if (bnf) {
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
-          yv[u] = *reinterpret_cast<const uint4*>(g.bn_y + o[u]);
+          yv[u] = *reinterpret_cast<const uint4*>(g.bn_y + yo[u]);
           mk[u] = g.bn_mask[o[u] >> 3];
         }
       }
@@ -1574,7 +1579,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                            int shards,
                                                            const bf16* __restrict__ bn_y2,
                                                            const float* __restrict__ bn_aux2,
-                                                           const float* __restrict__ kshift) {
+                                                           const float* __restrict__ kshift,
+                                                           int bn_ldy) {
   __shared__ float red[3 * 2048];
   const int NSB = bn_y2 ? 3 : 2;      // fused BN sums per channel (3: dual BN)
   const int CG = Co >> 3;             // 8-channel groups per row (Co <= 2048: CG <= 256)
@@ -1632,7 +1638,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
         for (int q = 0; q < 8; ++q) a[q] += d[q];
       }
       const uint4 pv = pack8(a);
-      if (bnp) bn_fuse_acc(pv, bn_y + o, bn_mask[o >> 3], bmean, bistd, bs1, bs2);
+      if (bnp) bn_fuse_acc(pv, bn_y + (bn_ldy ? (size_t)r * bn_ldy + cg * 8 : o), bn_mask[o >> 3],
+                           bmean, bistd, bs1, bs2);
       if (bnp && bn_y2) bn_fuse_acc3s(pv, bn_y2 + o, bn_mask[o >> 3], bmean2, bistd2, bs3);
       *reinterpret_cast<uint4*>(Y + o) = pv;
     }
@@ -1722,6 +1729,7 @@ static ConvGeom make_geom(int N, int Hs, int Ws, int Cs, int Ho, int Wo, int Co,
   g.shards = stat_shards();
   g.kshift = stat_shift();
   g.addend_s2c = 0;
+  g.bn_ldy = 0;
   return g;
 }
 
@@ -1889,11 +1897,11 @@ static void launch_igemm(const bf16* A, const bf16* B, bf16* Y, float* stats, co
     if (stats)
       hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
                          rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2,
-                         g.kshift);
+                         g.kshift, 0);
     else
       hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(gx), dim3(256), 0, st, ws, S, M, g.Co,
                          rpb, bias, addend, Y, stats, g.bn_y, g.bn_mask, g.bn_aux, g.bn_part, g.shards, g.bn_y2, g.bn_aux2,
-                         nullptr);
+                         nullptr, g.bn_ldy);
     return;
   }
   const ConvGeom& g = g0;
@@ -2187,6 +2195,11 @@ static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int K
   return g;
 }
 
+// Row stride of the fused BN reduce's y for the next dgrad launch(es) (0 = dense; bindings scope it
+// around one call): generic igemm / split-K stride-1 dgrads only
+static int g_bn_ldy = 0;
+void conv_set_bn_ldy(int ld) { g_bn_ldy = ld; }
+
 void conv_set_bn_dual(const bf16* y2, const float* aux2) {
   g_dual_y2 = y2;
   g_dual_aux2 = aux2;
@@ -2206,9 +2219,11 @@ int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
     return !(e && e[0] == '0');
   }();
   if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
-    return c64_fuse && !dual ? conv_c64_stat_rows(N, H) : 0;
+    return c64_fuse && !dual && !g_bn_ldy ? conv_c64_stat_rows(N, H) : 0;
   const ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   if (g.Co % 8 != 0) return 0;
+  // a row-strided y: the generic igemm / split-K stride-1 dgrads only
+  if (g_bn_ldy && (dual || g.mode != 1 || ph_cfg<1>(g) >= 0 || use_hx<1>(g))) return 0;
   if (dual && (g.mode != 1 || ph_cfg<1>(g) >= 0 || (use_hx<1>(g) && !conv_hx_dual()))) return 0;
   if (g.mode == 2) {
     if (use_hx<2>(g)) return hx_grid<2>(g);   // one slab row per (tile group, class-channel block)
@@ -2344,6 +2359,7 @@ void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, i
   g.bn_aux = bn_aux;
   g.bn_part = bn_part;
   g.addend_s2c = g.mode == 2 ? g_addend_s2c : 0;
+  g.bn_ldy = bn_y ? g_bn_ldy : 0;
   if (bn_part && g_dual_y2 && g.mode == 1 && ph_cfg<1>(g) < 0 && (!use_hx<1>(g) || conv_hx_dual())) {
     g.bn_y2 = g_dual_y2;
     g.bn_aux2 = g_dual_aux2;

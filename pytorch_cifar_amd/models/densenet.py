@@ -32,7 +32,7 @@ def dense_block(block, x):
     layers = list(block)
     g = layers[0].conv2.out_channels
     if F.DenseSlab.usable(x, g, len(layers)):
-        slab = F.DenseSlab(x, g, len(layers))
+        slab = F.DenseSlab(x, g, len(layers), training=layers[0].bn1.training)
         x = slab.start(x)
         for layer in layers:
             x = layer(x, slab)

@@ -490,6 +490,14 @@ _FUSE_BN_NOACT = os.environ.get("PCA_FUSE_BN_NOACT", "1") != "0"
 _ONES_MASK = {}
 
 
+# A BatchNorm reading a row-strided slab slice (DenseNet's suffix BNs) hands its backward reduce
+# to the consumer conv's dgrad epilogue too (PCA_STRIDED_BN_FUSE=0: separate reduce + finalize)
+_STRIDED_BN_FUSE = os.environ.get("PCA_STRIDED_BN_FUSE", "1") != "0"
+# DenseNet slabs cache each channel's batch sums as it is produced (PCA_SLAB_STATS=0: every
+# suffix BatchNorm runs its own statistics + finalize passes)
+_SLAB_STATS = os.environ.get("PCA_SLAB_STATS", "1") != "0"
+
+
 def _ones_mask(numel, device):
     key = (int(numel), device.index if device.index is not None else torch.cuda.current_device())
     m = _ONES_MASK.get(key)
@@ -576,6 +584,18 @@ class StatAcc:
         self.ensure_clean()
         self.state = "filled"
         self.shifted = False
+
+
+class _SlabStats(StatAcc):
+    """Channels [off, off + C) of a dense slab's statistics cache ([R][2][ld] centred sums + K row,
+    ``DenseSlab.sbuf``): read in place by the fused finalize+apply kernel (acc_off / acc_ld)."""
+
+    __slots__ = ("off", "ld")
+
+    def __init__(self, buf, R, off, ld, C):
+        self.buf, self.R, self.off, self.ld, self.C, self.NS = buf, R, off, ld, C, 2
+        self.state = "filled"
+        self.shifted = True
 
 
 # ------------------------------------------------- shifted (robust) BatchNorm forward sums
@@ -977,7 +997,8 @@ class _ConvDepthwise(torch.autograd.Function):
         ctx.bnsrc = None
         if ctx.needs_input_grad[0]:
             H, W, Cx = x.shape[1], x.shape[2], x.shape[3]
-            if src is not None and src.acc is not None and src.y2 is None:   # (no dual-BN sums)
+            if (src is not None and src.acc is not None and src.y2 is None   # (no dual-BN sums)
+                    and src.y.is_contiguous()):
                 src.acc.begin()
                 dx, ok = C.dw_dgrad_bn(dy, wT, H, W, Cx, KH, KW, stride, padding, src.y, src.mask,
                                        src.aux, src.act, src.acc.buf, src.acc.R)
@@ -1379,11 +1400,15 @@ class _BatchNormAct(torch.autograd.Function):
                 mom(bn2) if a2 is not None else 0.1, bn2.eps if a2 is not None else 1e-5,
                 ACT[cfg.act], relu, cfg.bacc.buf if cfg.bacc is not None else None,
                 stats.shifted, cfg.pilot, a2.shifted if a2 is not None else False,
-                cfg.pilot2 if a2 is not None else None, cfg.dest)
+                cfg.pilot2 if a2 is not None else None, cfg.dest,
+                acc_off=stats.off if isinstance(stats, _SlabStats) else 0,
+                acc_ld=stats.ld if isinstance(stats, _SlabStats) else 0)
             if cfg.bacc is not None:
                 cfg.bacc.state = "clean"      # block 0 cleared this BN's backward accumulator
             stats.state = "used"
             cfg.faccs = (stats,) if a2 is None else (stats, a2)
+            if isinstance(stats, _SlabStats):
+                cfg.faccs = ()   # (the slab's cache is shared by the block's later BNs)
             if a2 is not None:
                 a2.state = "used"
             if aux2 is not None and not aux2.numel():
@@ -1410,8 +1435,11 @@ class _BatchNormAct(torch.autograd.Function):
         ctx.save_for_backward(y, out if (relu and not has_mask) else None, mask if has_mask else None,
                               aux, y2, aux2)
         ctx.bnsrc = None
-        if not y.is_contiguous():
-            cfg.src = None    # (the consumer dgrad's fused reduce reads y densely: not a slab slice)
+        if not y.is_contiguous() and not (y2 is None and y.shape[-1] % 8 == 0 and _nhwc_rows(y)
+                                          and _STRIDED_BN_FUSE):
+            # (the consumer dgrad's fused reduce reads a dense y, or a row-strided channel slice:
+            # a DenseNet BatchNorm's slab suffix, the igemm / split-K dgrads only)
+            cfg.src = None
         # (grad mode is off inside Function.forward: the caller decided it in cfg.src)
         if cfg.src is not None and relu and has_mask and y2 is None:
             ctx.bnsrc = cfg.src = _BNSrc(y, mask, aux, cfg.bacc)
@@ -1615,6 +1643,11 @@ def batch_norm_act(bn, x, act=None, residual=None, residual_bn=None, stats=None,
                 cfg.pilot2 = link_pilot(p2, Cc, y.device)
     if _FUSE_BN_BWD and torch.is_grad_enabled() and training:
         cfg.src = True                # request: forward replaces it with the _BNSrc record
+    if (stats is None and training and residual is None and bn2 is None
+            and bn.running_mean is not None and act in ("relu", None)):
+        ds = getattr(x, "_pca_dense_stats", None)
+        if ds is not None and ds.C == Cc and _bn_fusable(Cc, act, False, False, bn):
+            stats = ds                # the dense slab's cached sums of this suffix
     if training and acc_enabled(Cc, y.device) and \
             _bn_fusable(Cc, act, residual is not None, bn2 is not None, bn, bn2):
         # (also without grad: the forward kernel then just keeps it clear)
@@ -1878,6 +1911,7 @@ class _PoolLinear(torch.autograd.Function):
         # 20 -> 74 us; so only while N / R <= 64)
         ok = (bnsrc is not None and bnsrc.act == 1 and bnsrc.mask is not None and bnsrc.y2 is None
               and bnsrc.acc is not None and C % 8 == 0 and 256 % (C // 8) == 0
+              and bnsrc.y.is_contiguous()
               and x.shape[0] <= 64 * bnsrc.acc.R)
         ctx.bnsrc = bnsrc if ok else None
         return logits
@@ -2650,12 +2684,21 @@ class DenseSlab:
     adds its own contribution into that memory (bn_backward dx_acc), so nothing is summed or split
     by copies either."""
 
-    def __init__(self, x0, growth, layers):
+    def __init__(self, x0, growth, layers, training=False):
         N, C0, H, W = x0.shape
         self.g = growth
         self.C = C0 + growth * layers
         self.buf = torch.empty((N, H, W, self.C), dtype=COMPUTE_DTYPE, device=x0.device)
         self.c0 = self.C - C0      # first channel of the current suffix
+        # statistics cache (training): every channel's centred batch sums, added as the channel is
+        # copied into the slab (bn_stats_copy), so each layer's BatchNorm folds its suffix of the
+        # cache in its apply kernel instead of a stats + finalize pass over the whole suffix (the
+        # O(L^2) reduction of the block); zeroed once per step before the first producer
+        self.sbuf = None
+        if training and _SLAB_STATS and acc_enabled(self.C, x0.device):
+            self.R = acc_shards(self.C)
+            self.sbuf = torch.empty(self.R * 2 * self.C + self.C, dtype=torch.float32,
+                                    device=x0.device)
 
     @staticmethod
     def usable(x0, growth, layers):
@@ -2666,10 +2709,11 @@ class DenseSlab:
                 and x0.shape[1] % 8 == 0 and x0.shape[1] + growth * layers <= _bn_rows_max_c()
                 and os.environ.get("PCA_ZERO_COPY_CAT", "1") != "0")
 
-    @staticmethod
-    def _suffix(t_nhwc, slot):
+    def _suffix(self, t_nhwc, slot):
         v = to_nchw(t_nhwc)
         v._pca_dense_slot = slot
+        if self.sbuf is not None:
+            v._pca_dense_stats = _SlabStats(self.sbuf, self.R, self.c0, self.C, self.C - self.c0)
         return v
 
     def start(self, x0):
@@ -2687,7 +2731,11 @@ class _SlabPut(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, slab, c0):
         dst = _slab_alias(slab.buf, c0, slab.C)
-        _C().copy_rows(x, dst)
+        if slab.sbuf is not None:
+            _C().zero_(slab.sbuf)
+            _C().bn_stats_copy(x, dst, slab.sbuf, c0, slab.C, slab.R)
+        else:
+            _C().copy_rows(x, dst)
         return dst
 
     @staticmethod
@@ -2702,7 +2750,11 @@ class _DenseAppend(torch.autograd.Function):
     def forward(ctx, out, x, slab, c0, xslot, yslot):
         ctx.g = out.shape[-1]
         ctx.xslot, ctx.yslot = xslot, yslot
-        _C().copy_rows(out, _slab_alias(slab.buf, c0, c0 + ctx.g))
+        if slab.sbuf is not None:
+            _C().bn_stats_copy(out, _slab_alias(slab.buf, c0, c0 + ctx.g), slab.sbuf, c0, slab.C,
+                               slab.R)
+        else:
+            _C().copy_rows(out, _slab_alias(slab.buf, c0, c0 + ctx.g))
         return _slab_alias(slab.buf, c0, slab.C)
 
     @staticmethod

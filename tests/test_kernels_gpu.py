@@ -904,3 +904,77 @@ def test_avgpool_window_eq_stride(C, k, HW, Cc):
     assert rel_err(nchw(y), ref) < 4e-3
     dx = C.avgpool_bwd(nhwc(dy).bfloat16(), HW, HW, k, k, 0)
     assert rel_err(nchw(dx), g) < 4e-3
+
+
+@pytest.mark.parametrize("case", [(8, 16, 96, 128, 32, -1), (8, 8, 256, 128, 64, -1),
+                                  (4, 4, 512, 128, 128, 4)])
+def test_dgrad_bn_fuse_row_strided_y(C, case):
+    """The fused BatchNorm-backward reduce of a 1x1 dgrad reading a row-strided y (a DenseNet
+    BatchNorm's input: a channel suffix of its block's concat slab, ops/functional.py DenseSlab):
+    dX and the per-block sums are bitwise those of the same call on a dense copy of y (igemm and
+    split-K forms), and the sums match fp32."""
+    N, H, Cin, Cout, extra, split = case
+    torch.manual_seed(11)
+    slab = torch.randn(N, H, H, Cin + extra, device="cuda").to(torch.bfloat16)
+    ys = slab[..., extra:]                       # row stride Cin + extra
+    assert not ys.is_contiguous()
+    yd = ys.contiguous()
+    w = bf(torch.randn(Cout, Cin, 1, 1, device="cuda") * (1.0 / Cin) ** 0.5)
+    _, wt = C.weight_prep(w.permute(0, 2, 3, 1).contiguous(), 1, True)
+    dy = torch.randn(N, H, H, Cout, device="cuda").to(torch.bfloat16)
+    mask_b = torch.rand(N, H, H, Cin, device="cuda") > 0.4
+    bits = (mask_b.view(-1, 8).to(torch.int32) << torch.arange(8, device="cuda")).sum(1).to(torch.uint8)
+    mean, istd = torch.randn(Cin, device="cuda") * 0.1, torch.rand(Cin, device="cuda") + 0.5
+    aux = torch.cat([mean, istd])
+    C.set_conv_tile(2, split)
+    try:
+        dx_d, p_d = C.conv_dgrad_bn(dy, wt, H, H, 1, 0, 1, None, yd, bits, aux)
+        dx_s, p_s = C.conv_dgrad_bn(dy, wt, H, H, 1, 0, 1, None, ys, bits, aux)
+    finally:
+        C.set_conv_tile(2, -1)
+    torch.cuda.synchronize()
+    assert p_d.numel() > 0 and p_s.shape == p_d.shape
+    assert torch.equal(dx_s, dx_d) and torch.equal(p_s, p_d)
+    dz = torch.where(mask_b, dx_s.float(), torch.zeros_like(dx_s, dtype=torch.float32))
+    s1 = dz.sum((0, 1, 2))
+    s2 = (dz * (yd.float() - mean) * istd).sum((0, 1, 2))
+    assert rel_err(p_s[:, 0, :].sum(0), s1) < 1e-3 and rel_err(p_s[:, 1, :].sum(0), s2) < 1e-3
+
+
+@pytest.mark.parametrize("shape", [(8, 16, 32, 64, 96), (4, 8, 48, 256, 512)])
+def test_bn_stats_copy_and_acc_view(C, shape):
+    """DenseNet slab statistics cache: bn_stats_copy copies a tensor into its slab slice and adds
+    its centred channel sums into a wider [R][2][ld] + K-row cache; bn_apply_acc reading a
+    channel range of that cache (acc_off / acc_ld) gives the BatchNorm of the slab suffix —
+    the copy bitwise, the output and running stats against fp32 batch statistics."""
+    N, H, g, C0, Ctot = shape
+    torch.manual_seed(5)
+    R = 4
+    cache = torch.empty(R * 2 * Ctot + Ctot, device="cuda")
+    C.zero_(cache)
+    slab = torch.zeros(N, H, H, Ctot, device="cuda", dtype=torch.bfloat16)
+    x0 = (torch.randn(N, H, H, C0, device="cuda") * 3 + 20).to(torch.bfloat16)
+    out = (torch.randn(N, H, H, g, device="cuda") * 0.5 - 4).to(torch.bfloat16)
+    c0 = Ctot - C0
+    C.bn_stats_copy(x0, slab[..., c0:], cache, c0, Ctot, R)
+    c1 = c0 - g
+    C.bn_stats_copy(out, slab[..., c1:c0], cache, c1, Ctot, R)
+    torch.cuda.synchronize()
+    assert torch.equal(slab[..., c0:], x0) and torch.equal(slab[..., c1:c0], out)
+    y = slab[..., c1:]
+    Cs = Ctot - c1
+    yf = y.float().reshape(-1, Cs)
+    gamma = torch.rand(Cs, device="cuda") + 0.5
+    beta = torch.randn(Cs, device="cuda")
+    rm, rv = torch.zeros(Cs, device="cuda"), torch.ones(Cs, device="cuda")
+    nbt = torch.zeros(1, dtype=torch.long, device="cuda")
+    o, mask, aux, _ = C.bn_apply_acc(y, cache, R, float(yf.shape[0]), gamma, beta, rm, rv, nbt, 0.1,
+                                     1e-5, None, None, None, 0, None, None, None, None, None, 0.1,
+                                     1e-5, 1, True, None, True, None, False, None, None,
+                                     acc_off=c1, acc_ld=Ctot)
+    m = yf.mean(0)
+    v = yf.var(0, unbiased=False)
+    ref = torch.relu((yf - m) / torch.sqrt(v + 1e-5) * gamma + beta)
+    assert rel_err(aux[0], m) < 1e-5 and rel_err(aux[1], 1 / torch.sqrt(v + 1e-5)) < 1e-4
+    assert rel_err(o.float().reshape(-1, Cs), ref) < 1e-2
+    assert rel_err(rm, 0.1 * m) < 1e-5 and int(nbt.item()) == 1

@@ -205,11 +205,12 @@ def static_tiles():
 
 @pytest.mark.parametrize("name", ["ResNet18", "ResNet50", "PreActResNet18", "MobileNetV2",
                                   "EfficientNetB0", "RegNetY_400MF", "densenet_cifar", "DLA",
-                                  "SENet18"])
+                                  "SENet18", "DenseNet121"])
 def test_bn_accumulators_match_reference(name, static_tiles):
     """Steps after the first route every conv->BN statistic and every BN-backward sum through the
-    sharded accumulators (fused finalize in the BN kernels): still as close to fp32 as stock
-    bf16, running stats / num_batches_tracked exact in count, and after the step every forward
+    sharded accumulators (fused finalize in the BN kernels; DenseNet121: the dense slabs'
+    statistics cache and the suffix BNs' backward sums from row-strided dgrad epilogues): still
+    as close to fp32 as stock bf16, running stats / num_batches_tracked exact in count, and after the step every forward
     accumulator is back at zero (cleared by its BN's backward kernel); the backward ones are
     cleared by the next forward."""
     from pytorch_cifar_amd import models
