@@ -12,6 +12,7 @@
 //           dy = a*dz + b*y + d  (dz = dout * act'(z), the residual gradient is dz itself).
 // Every reduction is a deterministic slab fold (no float atomics).
 #include "common.h"
+#include "slab_reduce.h"
 
 #include <cstdlib>
 
@@ -112,10 +113,30 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16* __restrict__ 
     for (int v = 0; v < VEC; ++v) s[v] = q[v] = k[v] = 0.f;
     if (krow && gi < rp.G) load_vec<VEC>(x + gi * VEC, k);
     if (ry < rp.RPP && gi < rp.G) {
-      for (int r = r0 + ry; r < r1; r += rp.RPP) {
+      // 4 rows in flight per thread (the rows are independent loads; one at a time left these
+      // small-grid reductions latency bound: ~12 us for 1 MB)
+      int r = r0 + ry;
+      for (; r + 3 * rp.RPP < r1; r += 4 * rp.RPP) {
+        float f[4][VEC];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load_vec<VEC>(x + (size_t)(r + u * rp.RPP) * ldx + gi * VEC, f[u]);
+        if (dst) {   // (bf16 -> fp32 -> bf16: exact)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) store_vec<VEC>(dst + (size_t)(r + u * rp.RPP) * ldd + gi * VEC, f[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) {
+            const float d = f[u][v] - k[v];
+            s[v] += d;
+            q[v] += d * d;
+          }
+      }
+      for (; r < r1; r += rp.RPP) {
         float f[VEC];
         load_vec<VEC>(x + (size_t)r * ldx + gi * VEC, f);
-        if (dst) store_vec<VEC>(dst + (size_t)r * ldd + gi * VEC, f);   // (bf16 -> fp32 -> bf16: exact)
+        if (dst) store_vec<VEC>(dst + (size_t)r * ldd + gi * VEC, f);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
           const float d = f[v] - k[v];
@@ -666,7 +687,8 @@ template <bool RES, bool DUAL, int KIND>
 __device__ __forceinline__ void bn_bwd_apply_rows_body(
     const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
     const float* coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
-    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux, BnLd ld) {
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux, BnLd ld,
+    int nblk) {
   constexpr bool MASK = KIND == 1;
   const int ldd = ld_or(ld.dout, C), ldy = ld_or(ld.y, C), ldx = ld_or(ld.dx, C);
   constexpr int U = kRowsInFlight;
@@ -690,7 +712,8 @@ __device__ __forceinline__ void bn_bwd_apply_rows_body(
       cd2[v] = coef[5 * C + c0 + v];
     }
   }
-  const int rstep = gridDim.x * RPB;
+  const int rstep = nblk * RPB;   // (nblk: the workgroups of this pass; gridDim.x unless the
+                                  // launch also carries slab-reduce workgroups)
   for (int r0 = blockIdx.x * RPB + ro; r0 < M; r0 += U * rstep) {
     uint4 vd[U], vy[U], v2[U], vx[U];
     uint32_t vm[U];
@@ -749,7 +772,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows_kernel(
     const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
     const float* __restrict__ coef, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
     const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux, BnLd ld) {
-  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, coef, C, M, dy, dres, y2, dy2, aux, ld);
+  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, coef, C, M, dy, dres, y2, dy2, aux, ld,
+                                          gridDim.x);
 }
 
 // ---- fused finalize + apply (sharded accumulators, no finalize launch) ----
@@ -903,8 +927,39 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_rows_kernel(
   bn_fin_zero(f);
   bn_fin_zero(f2);
   __syncthreads();
-  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, lds, C, M, dy, dres, y2, dy2, aux, ld);
+  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, lds, C, M, dy, dres, y2, dy2, aux, ld,
+                                          gridDim.x);
 }
+
+// The same with the pending weight-gradient slab reductions of the preceding wgrads riding along
+// as extra workgroups [napply, gridDim.x) (conv_halo.hip wgrad_take_pending): on the small
+// per-rank shard each reduce was a ~10 us latency-bound launch of its own between the wgrad and
+// this kernel; here it runs beside the BatchNorm pass it is independent of (the slab was just
+// written: L2 / MALL resident, unlike the end-of-pass batch of PCA_WGRAD_DEFER=1).
+template <bool RES, bool DUAL, int KIND>
+__global__ __launch_bounds__(256) void bn_bwd_apply_acc_rows_red_kernel(
+    const bf16* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16* __restrict__ y,
+    BnFin f, BnFin f2, int C, int M, bf16* __restrict__ dy, bf16* __restrict__ dres,
+    const bf16* __restrict__ y2, bf16* __restrict__ dy2, const float* __restrict__ aux, BnLd ld,
+    int napply, SlabRedBatch rb) {
+  if ((int)blockIdx.x >= napply) {   // (block-uniform: a reduce workgroup)
+    __shared__ float4 red[4][64];
+    slab_reduce_multi_body<4>(rb, (int)blockIdx.x - napply, red);
+    return;
+  }
+  extern __shared__ float lds[];   // coef [3|6][C]
+  constexpr int NS = DUAL ? 3 : 2;
+  bn_fin_backward<NS>(f, f2, C, lds);
+  bn_fin_zero(f);
+  bn_fin_zero(f2);
+  __syncthreads();
+  bn_bwd_apply_rows_body<RES, DUAL, KIND>(dout, mask, y, lds, C, M, dy, dres, y2, dy2, aux, ld,
+                                          napply);
+}
+
+int wgrad_take_pending(SlabRedBatch* b);
+static bool g_wgrad_piggy = false;
+void set_wgrad_piggy(bool on) { g_wgrad_piggy = on; }
 
 static bool rows_enabled() {
   static const bool on = [] {
@@ -1211,8 +1266,18 @@ bool bn_bwd_apply_acc_launch(const bf16* dout, const uint8_t* mask, const bf16* 
            dgamma2, dbeta2, zero2, zero2_n};
   const dim3 gr(acc_rows_grid(M, C)), bl(256);
   const size_t lds = (size_t)(y2 ? 6 : 3) * C * sizeof(float);
-#define PCA_BWD(R_, D, K) \
-  hipLaunchKernelGGL((bn_bwd_apply_acc_rows_kernel<R_, D, K>), gr, bl, lds, st, dout, mask, y, f, f2, C, M, dy, dres, y2, dy2, aux, g_bn_ld)
+  SlabRedBatch rb{};
+  const int nred = g_wgrad_piggy ? wgrad_take_pending(&rb) : 0;
+#define PCA_BWD(R_, D, K)                                                                             \
+  do {                                                                                                \
+    if (nred)                                                                                         \
+      hipLaunchKernelGGL((bn_bwd_apply_acc_rows_red_kernel<R_, D, K>), dim3(gr.x + nred), bl, lds,   \
+                         st, dout, mask, y, f, f2, C, M, dy, dres, y2, dy2, aux, g_bn_ld,            \
+                         (int)gr.x, rb);                                                              \
+    else                                                                                              \
+      hipLaunchKernelGGL((bn_bwd_apply_acc_rows_kernel<R_, D, K>), gr, bl, lds, st, dout, mask, y,   \
+                         f, f2, C, M, dy, dres, y2, dy2, aux, g_bn_ld);                               \
+  } while (0)
   if (masked) {
     if (dres && y2) PCA_BWD(true, true, 1);
     else if (dres) PCA_BWD(true, false, 1);

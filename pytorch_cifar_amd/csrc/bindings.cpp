@@ -89,6 +89,7 @@ int bn_rows_max_c();
 void wgrad_defer_scope(bool on);
 int wgrad_deferred_count();
 void wgrad_flush_launch(hipStream_t st);
+void set_wgrad_piggy(bool on);
 void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t, float* krow = nullptr);
 void bn_stats_copy_launch(const bf16* x, int ldx, int M, int C, bf16* dst, int ldd, float* acc,
                           int ldc, int R, int P, float* krow, hipStream_t st);
@@ -297,6 +298,7 @@ void copy_rows(const Tensor& src, const Tensor& dst) {
 // into channels [acc_off, acc_off + C) of a [R][2][acc_ld] + K-row fp32 cache (zeroed by the
 // caller before the first producer of a step)
 static int acc_reduce_blocks(int M, int C, int R);
+constexpr int kAccDepth = 16;
 void bn_stats_copy(const Tensor& src, const Tensor& dst, const Tensor& acc, int acc_off, int acc_ld,
                    int R) {
   const int ls = rows_ld(src, "src"), ld = rows_ld(dst, "dst");
@@ -310,9 +312,11 @@ void bn_stats_copy(const Tensor& src, const Tensor& dst, const Tensor& acc, int 
               "bn_stats_copy: acc must be [R][2][acc_ld] + K row");
   const int M = (int)(src.numel() / C);
   float* a = ptr<float>(acc);
+  // (up to 4 x kAccDepth workgroups per shard row: the copy's bytes need the wider grid, and
+  // each workgroup adds only 2 x C sums at its end)
+  const int P = std::max(1, std::min({2 * pca::bn_row_blocks(M, C), 4 * kAccDepth * R, 1024}));
   pca::bn_stats_copy_launch(ptr<bf16>(src), ls, M, C, ptr<bf16>(dst), ld, a + acc_off, acc_ld, R,
-                            acc_reduce_blocks(M, C, R), a + (size_t)R * 2 * acc_ld + acc_off,
-                            cur_stream());
+                            P, a + (size_t)R * 2 * acc_ld + acc_off, cur_stream());
 }
 
 // t <- 0 on the current stream (the runtime's fill: a memset node under hipGraph capture)
@@ -763,6 +767,9 @@ Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride,
   return dw;
 }
 
+// pending wgrad slab reductions ride along in the next fused BatchNorm-backward launch
+void wgrad_piggy(bool on) { pca::set_wgrad_piggy(on); }
+
 // every deferred slab reduction in one launch (per 20) on the current stream; returns how many
 int wgrad_flush() {
   const int n = pca::wgrad_deferred_count();
@@ -822,7 +829,7 @@ std::vector<Tensor> bn_stats_centered(const Tensor& x) {
 // Reduce-kernel grid when it adds into an R-row sharded accumulator: at most kAccDepth
 // workgroups per shard row, so the same-address fp32 atomics stay shallow (deeper queues — 1024
 // blocks into 16 rows — cost more than the finalize launch they remove).
-constexpr int kAccDepth = 16;
+
 static int acc_reduce_blocks(int M, int C, int R) {
   return std::max(1, std::min(pca::bn_row_blocks(M, C), kAccDepth * R));
 }
@@ -1250,6 +1257,7 @@ std::vector<Tensor> bn_backward_impl(const Tensor& dout, const optional<Tensor>&
     Tensor dres, dy2;
     if (need_dres) dres = at::empty(y.sizes(), y.options());
     if (dual) dy2 = at::empty(y.sizes(), y.options());
+    const int pend = pca::wgrad_deferred_count();
     const bool fused = pca::bn_bwd_apply_acc_launch(
         ptr<bf16>(dout), mk, ptr<bf16>(y), C, M, (float)M, ptr<float>(acc), acc_rows,
         ptr<float>(aux), optr<float>(gamma), ptr<float>(dgamma), ptr<float>(dbeta),
@@ -1257,6 +1265,9 @@ std::vector<Tensor> bn_backward_impl(const Tensor& dout, const optional<Tensor>&
         dual ? ptr<float>(dbeta2) : nullptr, act, ptr<bf16>(dy),
         need_dres ? ptr<bf16>(dres) : nullptr, optr<bf16>(y2), dual ? ptr<bf16>(dy2) : nullptr,
         zp1, zn1, zp2, zn2, st);
+    // (the launch took the pending wgrad slab reductions along: their workspaces may be reused
+    // by later allocations, which are stream-ordered after it)
+    if (pend && pca::wgrad_deferred_count() == 0) g_deferred_ws.clear();
     if (!fused) {
       auto coef = at::empty({dual ? 6 : 3, C}, fopt);
       pca::bn_bwd_finalize_launch(ptr<float>(acc), acc_rows, NS, C, (float)M, ptr<float>(aux),
@@ -2206,6 +2217,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("KH"), py::arg("KW"),
         py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("out"),
         py::arg("defer") = false);
+  m.def("wgrad_piggy", &wgrad_piggy, "pending wgrad slab reductions ride along in the next fused BN-backward launch");
   m.def("wgrad_flush", &wgrad_flush,
         "launch every deferred weight-gradient slab reduction (one batched kernel); returns count");
   m.def("wgrad_deferred", &pca::wgrad_deferred_count, "pending deferred slab reductions");

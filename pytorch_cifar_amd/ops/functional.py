@@ -241,7 +241,15 @@ def join_wgrad_streams():
 # right after the wgrad wrote it (L2-resident); deferred, every slab is re-read from MALL / HBM at
 # the end of the pass, which costs more than the ~11 launches it saves (ResNet-152 bs128: 779 us
 # for the 3 batched launches).
-_WGRAD_DEFER = os.environ.get("PCA_WGRAD_DEFER", "0") == "1"
+_DEFER_MODE = os.environ.get("PCA_WGRAD_DEFER", "piggy")
+_WGRAD_DEFER = _DEFER_MODE == "1"
+# Default ("piggy"): the recorded reductions ride along in the NEXT fused BatchNorm-backward launch
+# as extra workgroups (csrc/batchnorm.hip bn_bwd_apply_acc_rows_red_kernel) — right after their
+# wgrad, beside the BN pass they are independent of, so the slabs are still cache-resident and no
+# launch of their own is left; whatever no BN launch took is flushed as above. (Not bitwise the
+# per-conv kernels: 4 split lanes per column instead of up to 16; still a fixed order.)
+_WGRAD_PIGGY = _DEFER_MODE == "piggy"
+_piggy_set = [None]
 _defer_queued = {"on": False}
 
 
@@ -884,8 +892,13 @@ class _ConvMFMA(torch.autograd.Function):
                 _schedule_join()
                 G.fire(weight)
             elif buf is not None:
-                C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, buf, defer=_WGRAD_DEFER)
-                if _WGRAD_DEFER and C.wgrad_deferred():
+                piggy = _WGRAD_PIGGY and not _WGRAD_DEFER
+                if _piggy_set[0] != piggy:
+                    C.wgrad_piggy(piggy)
+                    _piggy_set[0] = piggy
+                C.conv_wgrad(x, dy, KH, KW, stride, padding, groups, buf,
+                             defer=_WGRAD_DEFER or piggy)
+                if (_WGRAD_DEFER or piggy) and C.wgrad_deferred():
                     _after_deferred_wgrad()
                 G.fire(weight)
             else:
