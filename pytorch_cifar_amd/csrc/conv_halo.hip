@@ -441,6 +441,11 @@ static bool g_defer_on = false;            // set around a production wgrad laun
 static std::vector<SlabRedDesc> g_deferred;
 
 void wgrad_defer_scope(bool on) { g_defer_on = on; }
+// drop the reductions recorded after the first n (tuning trials on scratch gradients; the real
+// pending ones of the backward pass in progress stay)
+void wgrad_truncate_pending(int n) {
+  if ((size_t)n < g_deferred.size()) g_deferred.resize(n);
+}
 int wgrad_deferred_count() { return (int)g_deferred.size(); }
 
 static int split_lanes(int splits) {
