@@ -1884,8 +1884,8 @@ Tensor chan_remap(const Tensor& x, const Tensor& cmap, const optional<Tensor>& r
   TORCH_CHECK(Q < (int64_t)1 << 31 && J > 0, "chan_remap: size");
   Tensor out;
   if (acc.has_value() && acc->defined()) {
-    TORCH_CHECK(fp32 && acc->scalar_type() == at::kFloat && acc->is_contiguous() && acc->numel() == Q * J,
-                "chan_remap: fp32 accumulator of Q*J elements");
+    TORCH_CHECK(acc->scalar_type() == x.scalar_type() && acc->is_contiguous() && acc->numel() == Q * J,
+                "chan_remap: accumulator of Q*J elements, the input's dtype");
     out = *acc;
   } else {
     out = at::empty({Q, J}, x.options());

@@ -2238,7 +2238,9 @@ __global__ __launch_bounds__(256) void chan_remap_kernel(T* __restrict__ in, T* 
 // 16-byte (or the widest dividing) loads, then writes RB output rows gathering from LDS — every
 // global access coalesced and vectorized (the per-element gather above issues V scalar loads
 // per output vector: slower than a stock pad on DPN / RegNet's padded groups).
-template <typename T, int VIN, int V>
+// ACC (bf16 activations): out += the remapped rows, summed in fp32 (a gradient junction: the
+// unpad of a zero-padded conv's dX adding the other consumer's gradient in the same pass)
+template <typename T, int VIN, int V, bool ACC = false>
 __global__ __launch_bounds__(256) void chan_remap_rows_kernel(const T* __restrict__ in,
                                                               T* __restrict__ out,
                                                               const int* __restrict__ cmap, int Q,
@@ -2266,12 +2268,17 @@ __global__ __launch_bounds__(256) void chan_remap_rows_kernel(const T* __restric
         const int c = smap[gi * V + u];
         v.v[u] = c >= 0 ? rows[r * Cin + c] : T(0.f);
       }
+      if constexpr (ACC) {
+        const VecO a = o[i];
+#pragma unroll
+        for (int u = 0; u < V; ++u) v.v[u] = T((float)a.v[u] + (float)v.v[u]);
+      }
       o[i] = v;
     }
   }
 }
 
-template <typename T>
+template <typename T, bool ACC = false>
 static bool chan_remap_rows(const T* in, T* out, const int* cmap, int Q, int Cin, int J,
                             hipStream_t st) {
   constexpr int VMAX = 16 / sizeof(T);
@@ -2287,7 +2294,7 @@ static bool chan_remap_rows(const T* in, T* out, const int* cmap, int Q, int Cin
   const int blocks = (int)std::min<int64_t>(cdiv64(Q, RB), 4096);
 #define PCA_RR(VI, VO)                                                                       \
   if (vin == VI && v == VO) {                                                                \
-    hipLaunchKernelGGL((chan_remap_rows_kernel<T, VI, VO>), dim3(blocks), dim3(256), lds, st, \
+    hipLaunchKernelGGL((chan_remap_rows_kernel<T, VI, VO, ACC>), dim3(blocks), dim3(256), lds, st, \
                        in, out, cmap, Q, Cin, J, RB);                                        \
     return true;                                                                             \
   }
@@ -2305,6 +2312,9 @@ static void chan_remap_dispatch(T* in, T* out, const int* cmap, const int* rmap,
                                 int Cin, int J, hipStream_t st) {
   if constexpr (!ACC && !CLR) {
     if (!rmap && chan_remap_rows<T>(in, out, cmap, Q, Cin, J, st)) return;
+  }
+  if constexpr (ACC && !CLR && sizeof(T) == 2) {
+    if (!rmap && chan_remap_rows<T, true>(in, out, cmap, Q, Cin, J, st)) return;
   }
   constexpr int VMAX = 16 / sizeof(T);
   int V = VMAX;
@@ -2337,6 +2347,9 @@ void chan_remap_launch(const void* in, void* out, bool fp32, bool accumulate, co
       chan_remap_dispatch<float, false, true>(i, (float*)out, cmap, rmap, Q, K, Cin, J, st);
     else
       chan_remap_dispatch<float, false>(i, (float*)out, cmap, rmap, Q, K, Cin, J, st);
+  } else if (accumulate) {
+    chan_remap_dispatch<bf16, true>(const_cast<bf16*>(static_cast<const bf16*>(in)), (bf16*)out,
+                                    cmap, rmap, Q, K, Cin, J, st);
   } else {
     chan_remap_dispatch<bf16, false>(const_cast<bf16*>(static_cast<const bf16*>(in)), (bf16*)out,
                                      cmap, rmap, Q, K, Cin, J, st);

@@ -1243,7 +1243,14 @@ def _conv_group_padded(x, weight, bias, stride, padding, groups, want_stats):
     else:
         xn = to_nhwc(x)
         N, H, W, _ = xn.shape
-        if cp != Cg:
+        if cp != Cg and groups == 1:
+            # x feeds other consumers too (ShuffleNetV2 DownBlock: this 1x1 conv3 and the left
+            # depthwise conv1, shufflenetv2.py:84-90): the unpad of this conv's dX adds their
+            # gradient in the same pass (_PadInput)
+            pslot, powner = _slot_for_conv(x)
+            xn = _PadInput.apply(xn, _group_pad_remap(groups, Cg, cp), (N, H, W, groups * cp),
+                                 pslot if powner else None)
+        elif cp != Cg:
             xn = _RemapFn.apply(xn, _group_pad_remap(groups, Cg, cp), (N, H, W, groups * cp), None)
     # weight [Cout, Cg, KH, KW] -> [G*op, cp, KH, KW], channels_last (the MFMA B layout): with a
     # plan, the padded bf16 operands are written by its batched launch (or the fused optimizer
@@ -2360,6 +2367,31 @@ class _RemapFn(torch.autograd.Function):
                 G.fire(leaf)
                 return None, None, None, None
         return ctx.remap.apply(dy, inverse=True).view(ctx.in_shape), None, None, None
+
+
+class _PadInput(torch.autograd.Function):
+    """Zero-pad the channels of an activation (one remap launch); the backward's unpad adds the
+    gradient another consumer left in ``slot`` (its owner is this conv) in the same launch —
+    no autograd add (csrc/misc.hip chan_remap_rows_kernel ACC)."""
+
+    @staticmethod
+    def forward(ctx, x, remap, out_shape, slot):
+        ctx.remap, ctx.in_shape, ctx.slot = remap, x.shape, slot
+        return remap.apply(x).view(out_shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        slot, ctx.slot = ctx.slot, None
+        other = slot.take() if slot is not None else None
+        if (other is not None and other.dtype == dy.dtype and other.is_contiguous()
+                and tuple(other.shape) == tuple(ctx.in_shape)):
+            ctx.remap.apply(dy, inverse=True, acc=other)     # other += unpad(dy)
+            return other, None, None, None
+        dx = ctx.remap.apply(dy, inverse=True).view(ctx.in_shape)
+        if other is not None:
+            dx = dx + other.reshape(dx.shape)
+        return dx, None, None, None
 
 
 def _remap_param(p, remap, phys_shape):

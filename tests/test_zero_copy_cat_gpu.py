@@ -322,3 +322,34 @@ def test_interleave2_split_matches_reference():
         dy = torch.cat([dlo, dhi], 1).reshape(4, c, 2, 5, 3)
         assert torch.equal(a.grad.float(), dy[:, :, 0].float()), c
         assert torch.equal(b.grad.float(), dy[:, :, 1].float()), c
+
+
+def test_shufflenetv2_no_stock_add():
+    """ShuffleNetV2's DownBlock input feeds the left depthwise conv and the right 1x1 conv3 (a
+    zero-padded odd-width input at 116 / 232 channels): the unpad of conv3's dX adds the depthwise
+    dgrad's gradient in the same remap pass (ops/functional.py _PadInput), so no stock add is
+    left in the step; gradients vs the autograd sum within bf16 rounding of one add."""
+    from pytorch_cifar_amd.models import ShuffleNetV2
+    from pytorch_cifar_amd.ops import functional as OF
+
+    torch.manual_seed(0)
+    m0 = ShuffleNetV2(1).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        m0(x).float().sum().backward()
+        torch.cuda.synchronize()
+    adds = [e.name for e in prof.events() if "CUDAFunctor_add" in e.name]
+    assert not adds, adds
+    g0 = {n: p.grad.clone() for n, p in m0.named_parameters()}
+    m1 = copy.deepcopy(m0)
+    for p in m1.parameters():
+        p.grad = None
+    saved = OF._FUSE_GRAD
+    OF._FUSE_GRAD = False            # every branch gradient summed by autograd
+    try:
+        m1(x).float().sum().backward()
+    finally:
+        OF._FUSE_GRAD = saved
+    for n in ("layer2.0.conv3.weight", "layer2.0.conv1.weight", "layer1.2.conv3.weight",
+              "conv1.weight"):
+        _close(g0[n].float(), m1.state_dict(keep_vars=True)[n].grad.float(), n, tol=3e-2)

@@ -19,7 +19,7 @@ int64_t conv_fwd_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int K
 int64_t conv_dgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                              int pad, int groups, int Ho, int Wo);
 int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                       int groups, int Ho, int Wo);
+                       int groups, int Ho, int Wo, bool has_bias);
 int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                        int groups, int Ho, int Wo);
 int64_t conv_wgrad_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
@@ -83,7 +83,7 @@ int main() {
             const int64_t ws = pca::conv_fwd_ws_floats(N, sh.H, sh.H, sh.Cin, sh.Cout, sh.k, sh.k,
                                                        sh.s, sh.p, sh.g, Ho, Ho, false);
             const int rows = pca::conv_fwd_stat_rows(N, sh.H, sh.H, sh.Cin, sh.Cout, sh.k, sh.k,
-                                                     sh.s, sh.p, sh.g, Ho, Ho);
+                                                     sh.s, sh.p, sh.g, Ho, Ho, false);
             CHECK(ws >= 0 && ws <= (int64_t)8 * N * Ho * Ho * sh.Cout, "fwd ws %lld N=%d cfg=%d",
                   (long long)ws, N, c.first);
             CHECK(rows >= 1 && rows <= 4096, "fwd stat rows %d N=%d cfg=%d", rows, N, c.first);
