@@ -91,6 +91,7 @@ int wgrad_deferred_count();
 void wgrad_flush_launch(hipStream_t st);
 void set_wgrad_piggy(bool on);
 void wgrad_truncate_pending(int n);
+int64_t conv_nk_min_m(int64_t v);
 void bn_stats_launch(const bf16*, int, int, float*, int, hipStream_t, float* krow = nullptr);
 void bn_stats_copy_launch(const bf16* x, int ldx, int M, int C, bf16* dst, int ldd, float* acc,
                           int ldc, int R, int P, float* krow, hipStream_t st);
@@ -2314,6 +2315,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pilot") = py::none(), py::arg("shifted2") = false, py::arg("pilot2") = py::none(),
         py::arg("out") = py::none(), py::arg("acc_off") = 0, py::arg("acc_ld") = 0,
         "training BN(+act/+res/+BN2) with the finalize folded in from sharded accumulators");
+  m.def("conv_nk_min_m", [](int64_t v) { return pca::conv_nk_min_m(v); }, py::arg("v") = -1,
+        "pixel count from which 1x1 narrow-K forwards take conv1x1_nk (returns the previous)");
   m.def("zero_", &zero_, "t <- 0 (runtime fill on the current stream)");
   m.def("bn_stats_copy", &bn_stats_copy, py::arg("src"), py::arg("dst"), py::arg("acc"),
         py::arg("acc_off"), py::arg("acc_ld"), py::arg("R"),

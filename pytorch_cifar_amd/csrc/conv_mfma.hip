@@ -2200,6 +2200,12 @@ static ConvGeom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int K
 static int g_bn_ldy = 0;
 void conv_set_bn_ldy(int ld) { g_bn_ldy = ld; }
 
+bool conv1x1_nk_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                           int pad, int groups);
+int conv1x1_nk_stat_rows(int N, int H, int W);
+void conv1x1_nk_launch(const bf16* x, const bf16* w, bf16* y, float* stats, int N, int H, int W,
+                       int Cin, int Cout, hipStream_t st);
+
 void conv_set_bn_dual(const bf16* y2, const float* aux2) {
   g_dual_y2 = y2;
   g_dual_aux2 = aux2;
@@ -2257,7 +2263,9 @@ bool conv_needs_tune(int kind, int N, int H, int W, int Cin, int Cout, int KH, i
   if (kind == 0) {
     ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
                            Cout / groups);
-    return tunable(g, c64 || conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups));
+    return tunable(g, c64 || conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) ||
+                          (!has_bias && conv1x1_nk_applicable(N, H, W, Cin, Cout, KH, KW, stride,
+                                                              pad, groups)));
   }
   return tunable(dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo), c64);
 }
@@ -2322,6 +2330,9 @@ int conv_fwd_stat_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
     return conv_c64_stat_rows(N, H);
   if (g_igemm_override < 0 && conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
     return conv_stem_stat_rows(N, H);
+  if (g_igemm_override < 0 && !has_bias &&
+      conv1x1_nk_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return conv1x1_nk_stat_rows(N, H, W);
   ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,
                          Cout / groups);
   return igemm_grid_x<0>(g);
@@ -2337,6 +2348,11 @@ void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, f
   }
   if (g_igemm_override < 0 && conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
     conv_stem_fwd_launch(x, w, bias, y, stats, N, H, Cout, st);
+    return;
+  }
+  if (g_igemm_override < 0 && bias == nullptr &&
+      conv1x1_nk_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
+    conv1x1_nk_launch(x, w, y, stats, N, H, W, Cin, Cout, st);
     return;
   }
   ConvGeom g = make_geom(N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, groups, Cin / groups,

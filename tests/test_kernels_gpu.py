@@ -978,3 +978,38 @@ def test_bn_stats_copy_and_acc_view(C, shape):
     assert rel_err(aux[0], m) < 1e-5 and rel_err(aux[1], 1 / torch.sqrt(v + 1e-5)) < 1e-4
     assert rel_err(o.float().reshape(-1, Cs), ref) < 1e-2
     assert rel_err(rm, 0.1 * m) < 1e-5 and int(nbt.item()) == 1
+
+
+@pytest.mark.parametrize("shape", [(8, 32, 16, 96), (4, 32, 24, 144), (9, 16, 32, 192),
+                                   (4, 16, 40, 240), (3, 8, 24, 144), (2, 7, 16, 96)])
+def test_conv1x1_narrow_k(C, shape):
+    """Narrow-K 1x1 forward (csrc/conv1x1_nk.hip: the MobileNetV2 / EfficientNet expand convs,
+    K <= 64, Cout = 96..240): output vs fp32 F.conv2d, BN statistics as slab rows (sum /
+    sumsq of the stored bf16 values) and as shifted sums into a sharded accumulator + K row.
+    (2, 7, 16, 96): 98 pixels, a partial 16-pixel group."""
+    N, H, Cin, Cout = shape
+    torch.manual_seed(3)
+    x = bf(torch.randn(N, Cin, H, H, device="cuda"))
+    w = bf(torch.randn(Cout, Cin, 1, 1, device="cuda") * (1.0 / Cin) ** 0.5)
+    ref = F.conv2d(x, w)
+    x_n = nhwc(x).to(torch.bfloat16)
+    wb, _ = C.weight_prep(w.permute(0, 2, 3, 1).contiguous(), 1, False)
+    prev = C.conv_nk_min_m(0)          # (production takes it from 512K pixels on)
+    try:
+        y, stats = C.conv_fwd(x_n, wb, None, 1, 0, 1, True)
+        K = torch.randn(Cout, device="cuda")
+        R = 4
+        acc = torch.zeros(R * 2 * Cout + Cout, device="cuda")
+        y2, _ = C.conv_fwd(x_n, wb, None, 1, 0, 1, True, acc, R, K)
+    finally:
+        C.conv_nk_min_m(prev)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < 1e-2
+    yf = y.float().reshape(-1, Cout)
+    assert rel_err(stats[:, 0, :].sum(0), yf.sum(0)) < 1e-4
+    assert rel_err(stats[:, 1, :].sum(0), (yf ** 2).sum(0)) < 1e-4
+    assert torch.equal(y2, y)
+    a = acc[:R * 2 * Cout].view(R, 2, Cout).sum(0)
+    d = yf - K
+    assert rel_err(a[0], d.sum(0)) < 1e-4 and rel_err(a[1], (d ** 2).sum(0)) < 1e-4
+    assert torch.equal(acc[R * 2 * Cout:], K)
