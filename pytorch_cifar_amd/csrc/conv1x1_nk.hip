@@ -21,16 +21,31 @@ namespace pca {
 int stat_shards();
 const float* stat_shift();
 
-template <int KS, int CT, bool STG>
+// The same GEMM shape is the data gradient of a narrow-output 1x1 conv (the inverted-residual
+// project conv, Cout = K: dX[M][CO] = dY[M][K] . W^T with W^T = its [CO][K] dgrad operand). DGRAD
+// replaces the statistics epilogue by the dgrad one: the residual addend, and the fused backward
+// reduce of the BatchNorm(+ReLU) that produced the conv input (sums of dz = dX * relu'(mask) and
+// dz * (y - mean), istd applied at the flush: the igemm dgrad epilogue's slab-row / sharded form).
+struct NkBn {
+  const bf16* addend;
+  const bf16* y;            // that BN's input (its mean | istd in aux)
+  const uint8_t* mask;      // its 1-bit ReLU mask (all ones for a BN without activation)
+  const float* aux;
+  float* part;              // [rows][2][CO] slab rows, or the sharded accumulator
+};
+
+template <int KS, int CT, bool STG, bool DGRAD>
 __global__ __launch_bounds__(256) void conv1x1_nk_kernel(const bf16* __restrict__ x,
                                                          const bf16* __restrict__ w,
                                                          bf16* __restrict__ y, int M, int K,
                                                          float* __restrict__ stats, int shards,
-                                                         const float* __restrict__ kshift) {
+                                                         const float* __restrict__ kshift,
+                                                         NkBn bn) {
   constexpr int CO = CT * 16;
   constexpr int KP = KS * 32;   // zero-padded reduction width (MFMA K steps of 32)
   __shared__ __attribute__((aligned(16))) bf16 ws[CO * KP];
-  __shared__ float kks[CO];
+  __shared__ float kks[CO];     // forward: the statistics shift; dgrad: the BN mean
+  __shared__ float kis[DGRAD ? CO : 1];   // dgrad: the BN istd
   __shared__ float red[4][2][CO];
   // STG: each wave's 16 x CO output tile is staged in a private LDS region and leaves as whole
   // contiguous 16-byte row pieces (the direct form stores 8 bytes per lane, 32 bytes per pixel
@@ -43,7 +58,15 @@ __global__ __launch_bounds__(256) void conv1x1_nk_kernel(const bf16* __restrict_
     if (kc < K) v = *reinterpret_cast<const uint4*>(w + (size_t)co * K + kc);
     *reinterpret_cast<uint4*>(ws + co * KP + kc) = v;
   }
-  for (int c = tid; c < CO; c += 256) kks[c] = kshift ? kshift[c] : 0.f;
+  const bool fuse = DGRAD && bn.part != nullptr;
+  if constexpr (DGRAD) {
+    for (int c = tid; c < CO; c += 256) {
+      kks[c] = fuse ? bn.aux[c] : 0.f;
+      kis[c] = fuse ? bn.aux[CO + c] : 0.f;
+    }
+  } else {
+    for (int c = tid; c < CO; c += 256) kks[c] = kshift ? kshift[c] : 0.f;
+  }
   __syncthreads();
 
   const int r = lane & 15, kq = lane >> 4;
@@ -52,7 +75,7 @@ __global__ __launch_bounds__(256) void conv1x1_nk_kernel(const bf16* __restrict_
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
     for (int j = 0; j < 4; ++j) s[ct][j] = q[ct][j] = 0.f;
-  const bool want = stats != nullptr;
+  const bool want = DGRAD ? fuse : stats != nullptr;
 
   const int ngroups = (M + 15) >> 4;
   const int gstride = gridDim.x * 4;
@@ -87,6 +110,16 @@ __global__ __launch_bounds__(256) void conv1x1_nk_kernel(const bf16* __restrict_
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bcur[ks], acc, 0, 0, 0);
       }
       // D[row = channel ct*16 + 4kq + j][col = pixel r]: four consecutive channels of pixel r
+      const size_t eo = (size_t)px * CO + ct * 16 + kq * 4;   // (element offset, pixel r)
+      if constexpr (DGRAD) {
+        if (bn.addend && pok) {
+          const uint2 av = *reinterpret_cast<const uint2*>(bn.addend + eo);
+          acc[0] += __uint_as_float(av.x << 16);
+          acc[1] += __uint_as_float(av.x & 0xffff0000u);
+          acc[2] += __uint_as_float(av.y << 16);
+          acc[3] += __uint_as_float(av.y & 0xffff0000u);
+        }
+      }
       const uint32_t lo = pack2(acc[0], acc[1]), hi = pack2(acc[2], acc[3]);
       if constexpr (STG)
         *reinterpret_cast<uint2*>(stg + wid * 16 * CO + r * CO + ct * 16 + kq * 4) = make_uint2(lo, hi);
@@ -95,11 +128,25 @@ __global__ __launch_bounds__(256) void conv1x1_nk_kernel(const bf16* __restrict_
       if (want && pok) {
         const float f[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                             __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+        if constexpr (DGRAD) {
+          // dz = dX * relu'(mask) of the stored dX; sums of dz and dz * (y - mean)
+          const uint2 yv = *reinterpret_cast<const uint2*>(bn.y + eo);
+          const float yy[4] = {__uint_as_float(yv.x << 16), __uint_as_float(yv.x & 0xffff0000u),
+                               __uint_as_float(yv.y << 16), __uint_as_float(yv.y & 0xffff0000u)};
+          const uint32_t mb = (uint32_t)bn.mask[eo >> 3] >> (eo & 7);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float d = f[j] - kks[ct * 16 + kq * 4 + j];   // the stored value, shifted
-          s[ct][j] += d;
-          q[ct][j] = fmaf(d, d, q[ct][j]);
+          for (int j = 0; j < 4; ++j) {
+            const float dz = ((mb >> j) & 1u) ? f[j] : 0.f;
+            s[ct][j] += dz;
+            q[ct][j] = fmaf(dz, yy[j] - kks[ct * 16 + kq * 4 + j], q[ct][j]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = f[j] - kks[ct * 16 + kq * 4 + j];   // the stored value, shifted
+            s[ct][j] += d;
+            q[ct][j] = fmaf(d, d, q[ct][j]);
+          }
         }
       }
     }
@@ -134,13 +181,14 @@ __global__ __launch_bounds__(256) void conv1x1_nk_kernel(const bf16* __restrict_
       }
     }
   __syncthreads();
+  float* out = DGRAD ? bn.part : stats;
   for (int c = tid; c < CO; c += 256) {
-    stat_out(stats, blockIdx.x, shards, 2 * CO, c,
+    const float q2 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    stat_out(out, blockIdx.x, shards, 2 * CO, c,
              red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c]);
-    stat_out(stats, blockIdx.x, shards, 2 * CO, CO + c,
-             red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c]);
+    stat_out(out, blockIdx.x, shards, 2 * CO, CO + c, DGRAD ? q2 * kis[c] : q2);
   }
-  stat_krow(stats, shards, 2 * CO, kshift, CO);
+  if constexpr (!DGRAD) stat_krow(stats, shards, 2 * CO, kshift, CO);
 }
 
 static int nk_cus() {
@@ -194,6 +242,25 @@ int conv1x1_nk_stat_rows(int N, int H, int W) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((groups + 3) / 4, std::min(4 * nk_cus(), 1024)));
 }
 
+template <bool DGRAD>
+static void nk_dispatch(const bf16* x, const bf16* w, bf16* y, float* stats, int M, int K, int CO,
+                        int grid, int sh, const float* k, const NkBn& b, bool stg, hipStream_t st) {
+  const int ks = K <= 32 ? 1 : 2;
+#define PCA_NK(KS_, CT_)                                                                          \
+  if (ks == KS_ && CO == CT_ * 16) {                                                             \
+    if (stg)                                                                                      \
+      hipLaunchKernelGGL((conv1x1_nk_kernel<KS_, CT_, true, DGRAD>), dim3(grid), dim3(256), 0, st, \
+                         x, w, y, M, K, stats, sh, k, b);                                         \
+    else                                                                                          \
+      hipLaunchKernelGGL((conv1x1_nk_kernel<KS_, CT_, false, DGRAD>), dim3(grid), dim3(256), 0,   \
+                         st, x, w, y, M, K, stats, sh, k, b);                                     \
+    return;                                                                                       \
+  }
+  PCA_NK(1, 6) PCA_NK(1, 9) PCA_NK(1, 12) PCA_NK(1, 15)
+  PCA_NK(2, 6) PCA_NK(2, 9) PCA_NK(2, 12) PCA_NK(2, 15)
+#undef PCA_NK
+}
+
 // x [M][Cin] bf16, w [Cout][Cin] bf16 -> y [M][Cout] bf16; stats: slab rows
 // [conv1x1_nk_stat_rows][2][Cout] (shards 0) or the sharded accumulator (stat_shards() > 0)
 void conv1x1_nk_launch(const bf16* x, const bf16* w, bf16* y, float* stats, int N, int H, int W,
@@ -202,24 +269,27 @@ void conv1x1_nk_launch(const bf16* x, const bf16* w, bf16* y, float* stats, int 
   const int grid = conv1x1_nk_stat_rows(N, H, W);
   const int sh = stat_shards();
   const float* k = stats ? stat_shift() : nullptr;
-  const int ks = Cin <= 32 ? 1 : 2;
   static const bool stg = [] {
     const char* e = getenv("PCA_NK_STG");
     return !(e && e[0] == '0');
   }();
-#define PCA_NK(KS_, CT_)                                                                        \
-  if (ks == KS_ && Cout == CT_ * 16) {                                                         \
-    if (stg)                                                                                    \
-      hipLaunchKernelGGL((conv1x1_nk_kernel<KS_, CT_, true>), dim3(grid), dim3(256), 0, st, x, w, \
-                         y, M, Cin, stats, sh, k);                                              \
-    else                                                                                        \
-      hipLaunchKernelGGL((conv1x1_nk_kernel<KS_, CT_, false>), dim3(grid), dim3(256), 0, st, x,  \
-                         w, y, M, Cin, stats, sh, k);                                           \
-    return;                                                                                     \
-  }
-  PCA_NK(1, 6) PCA_NK(1, 9) PCA_NK(1, 12) PCA_NK(1, 15)
-  PCA_NK(2, 6) PCA_NK(2, 9) PCA_NK(2, 12) PCA_NK(2, 15)
-#undef PCA_NK
+  nk_dispatch<false>(x, w, y, stats, M, Cin, Cout, grid, sh, k, NkBn{}, stg, st);
+}
+
+// dX [M][Cin] = dY [M][Cout] . W^T of a 1x1 / stride-1 conv with Cout <= 64 (wt = its [Cin][Cout]
+// dgrad operand): the narrow-K form with the dgrad epilogue (conv_dgrad_launch)
+void conv1x1_nk_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, int W,
+                             int Cin, int Cout, const bf16* addend, const bf16* bn_y,
+                             const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
+                             hipStream_t st) {
+  const int M = N * H * W;
+  const int grid = conv1x1_nk_stat_rows(N, H, W);
+  static const bool stg = [] {
+    const char* e = getenv("PCA_NK_STG");
+    return !(e && e[0] == '0');
+  }();
+  NkBn b{addend, bn_y, bn_mask, bn_aux, bn_part};
+  nk_dispatch<true>(dy, wt, dx, nullptr, M, Cout, Cin, grid, stat_shards(), nullptr, b, stg, st);
 }
 
 }  // namespace pca

@@ -2205,6 +2205,13 @@ bool conv1x1_nk_applicable(int N, int H, int W, int Cin, int Cout, int KH, int K
 int conv1x1_nk_stat_rows(int N, int H, int W);
 void conv1x1_nk_launch(const bf16* x, const bf16* w, bf16* y, float* stats, int N, int H, int W,
                        int Cin, int Cout, hipStream_t st);
+void conv1x1_nk_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, int W,
+                             int Cin, int Cout, const bf16* addend, const bf16* bn_y,
+                             const uint8_t* bn_mask, const float* bn_aux, float* bn_part,
+                             hipStream_t st);
+// the data gradient of a 1x1 conv with a narrow output (Cout <= 64) is the narrow-K GEMM
+static bool nk_dgrad_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                int pad, int groups);
 
 void conv_set_bn_dual(const bf16* y2, const float* aux2) {
   g_dual_y2 = y2;
@@ -2230,6 +2237,9 @@ int conv_dgrad_bn_rows(int N, int H, int W, int Cin, int Cout, int KH, int KW, i
   if (g.Co % 8 != 0) return 0;
   // a row-strided y: the generic igemm / split-K stride-1 dgrads only
   if (g_bn_ldy && (dual || g.mode != 1 || ph_cfg<1>(g) >= 0 || use_hx<1>(g))) return 0;
+  if (!dual && !g_bn_ldy && g_igemm_override < 0 &&
+      nk_dgrad_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups))
+    return conv1x1_nk_stat_rows(N, H, W);
   if (dual && (g.mode != 1 || ph_cfg<1>(g) >= 0 || (use_hx<1>(g) && !conv_hx_dual()))) return 0;
   if (g.mode == 2) {
     if (use_hx<2>(g)) return hx_grid<2>(g);   // one slab row per (tile group, class-channel block)
@@ -2267,7 +2277,17 @@ bool conv_needs_tune(int kind, int N, int H, int W, int Cin, int Cout, int KH, i
                           (!has_bias && conv1x1_nk_applicable(N, H, W, Cin, Cout, KH, KW, stride,
                                                               pad, groups)));
   }
-  return tunable(dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo), c64);
+  return tunable(dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo),
+                 c64 || nk_dgrad_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups));
+}
+
+static bool nk_dgrad_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                int pad, int groups) {
+  static const bool on = [] {
+    const char* e = getenv("PCA_CONV_NK_DGRAD");
+    return !(e && e[0] == '0');
+  }();
+  return on && conv1x1_nk_applicable(N, H, W, Cout, Cin, KH, KW, stride, pad, groups);
 }
 
 // candidate (cfg, split) list for a geometry: tile shapes from 64x64 to 128x128, split-K 1..8
@@ -2367,6 +2387,12 @@ void conv_dgrad_launch(const bf16* dy, const bf16* wt, bf16* dx, int N, int H, i
                        const uint8_t* bn_mask, const float* bn_aux, float* bn_part) {
   if (g_igemm_override < 0 && conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
     conv_c64_launch(dy, wt, dx, nullptr, addend, N, H, true, st, bn_y, bn_mask, bn_aux, bn_part);
+    return;
+  }
+  if (g_igemm_override < 0 && !g_bn_ldy && !(bn_part && g_dual_y2) &&
+      nk_dgrad_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
+    conv1x1_nk_dgrad_launch(dy, wt, dx, N, H, W, Cin, Cout, addend, bn_y, bn_mask, bn_aux, bn_part,
+                            st);
     return;
   }
   ConvGeom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);

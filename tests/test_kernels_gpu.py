@@ -1013,3 +1013,44 @@ def test_conv1x1_narrow_k(C, shape):
     d = yf - K
     assert rel_err(a[0], d.sum(0)) < 1e-4 and rel_err(a[1], (d ** 2).sum(0)) < 1e-4
     assert torch.equal(acc[R * 2 * Cout:], K)
+
+
+@pytest.mark.parametrize("shape", [(8, 32, 144, 24), (4, 16, 192, 32), (9, 16, 240, 40),
+                                   (2, 7, 96, 16)])
+def test_conv1x1_narrow_k_dgrad(C, shape):
+    """Narrow-K kernel as the data gradient of a narrow-output 1x1 conv (the inverted-residual
+    project conv: dX[M][Cin] = dY[M][Cout] . W^T, Cout <= 64): plain, and with the residual addend
+    + fused BatchNorm-backward reduce (slab rows and sharded accumulator), vs fp32."""
+    N, H, Cin, Cout = shape
+    torch.manual_seed(4)
+    w = bf(torch.randn(Cout, Cin, 1, 1, device="cuda") * (1.0 / Cin) ** 0.5)
+    dy = bf(torch.randn(N, Cout, H, H, device="cuda"))
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), w, dy)
+    _, wt = C.weight_prep(w.permute(0, 2, 3, 1).contiguous(), 1, True)
+    dy_n = nhwc(dy).to(torch.bfloat16)
+    ybn = torch.randn(N, H, H, Cin, device="cuda").to(torch.bfloat16)
+    mask_b = torch.rand(N, H, H, Cin, device="cuda") > 0.4
+    bits = (mask_b.view(-1, 8).to(torch.int32) << torch.arange(8, device="cuda")).sum(1).to(torch.uint8)
+    mean, istd = torch.randn(Cin, device="cuda") * 0.1, torch.rand(Cin, device="cuda") + 0.5
+    aux = torch.cat([mean, istd])
+    add = torch.randn(N, H, H, Cin, device="cuda").to(torch.bfloat16)
+    prev = C.conv_nk_min_m(0)
+    try:
+        dx = C.conv_dgrad(dy_n, wt, H, H, 1, 0, 1)
+        dx2, part = C.conv_dgrad_bn(dy_n, wt, H, H, 1, 0, 1, add, ybn, bits, aux)
+        R = 4
+        bacc = torch.zeros(R * 2 * Cin, device="cuda")
+        dx3, _ = C.conv_dgrad_bn(dy_n, wt, H, H, 1, 0, 1, add, ybn, bits, aux, bacc, R)
+    finally:
+        C.conv_nk_min_m(prev)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(dx), ref) < 1e-2
+    full = nhwc(ref) + add.float()
+    assert rel_err(dx2, full) < 1e-2 and torch.equal(dx3, dx2)
+    dz = torch.where(mask_b, dx2.float(), torch.zeros_like(full))
+    s1 = dz.sum((0, 1, 2))
+    s2 = (dz * (ybn.float() - mean) * istd).sum((0, 1, 2))
+    assert part.numel() > 0
+    assert rel_err(part[:, 0, :].sum(0), s1) < 1e-4 and rel_err(part[:, 1, :].sum(0), s2) < 1e-4
+    a = bacc.view(R, 2, Cin).sum(0)
+    assert rel_err(a[0], s1) < 1e-4 and rel_err(a[1], s2) < 1e-4
