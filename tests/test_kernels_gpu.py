@@ -981,7 +981,9 @@ def test_bn_stats_copy_and_acc_view(C, shape):
 
 
 @pytest.mark.parametrize("shape", [(8, 32, 16, 96), (4, 32, 24, 144), (9, 16, 32, 192),
-                                   (4, 16, 40, 240), (3, 8, 24, 144), (2, 7, 16, 96)])
+                                   (4, 16, 40, 240), (3, 8, 24, 144), (2, 7, 16, 96),
+                                   (8, 32, 144, 24), (4, 16, 96, 16), (2, 7, 240, 40),
+                                   (3, 8, 256, 64), (4, 8, 72, 48)])
 def test_conv1x1_narrow_k(C, shape):
     """Narrow-K 1x1 forward (csrc/conv1x1_nk.hip: the MobileNetV2 / EfficientNet expand convs,
     K <= 64, Cout = 96..240): output vs fp32 F.conv2d, BN statistics as slab rows (sum /
@@ -1016,7 +1018,8 @@ def test_conv1x1_narrow_k(C, shape):
 
 
 @pytest.mark.parametrize("shape", [(8, 32, 144, 24), (4, 16, 192, 32), (9, 16, 240, 40),
-                                   (2, 7, 96, 16)])
+                                   (2, 7, 96, 16), (8, 32, 24, 144), (3, 8, 40, 240),
+                                   (2, 7, 16, 96)])
 def test_conv1x1_narrow_k_dgrad(C, shape):
     """Narrow-K kernel as the data gradient of a narrow-output 1x1 conv (the inverted-residual
     project conv: dX[M][Cin] = dY[M][Cout] . W^T, Cout <= 64): plain, and with the residual addend
