@@ -47,6 +47,12 @@ void wgrad_clear_tuned();
 std::vector<std::vector<int>> tune_export();
 void c64_set_prof(int64_t* p);
 int c64_grid_size(int N, int H);
+void conv_c64_set_xf(const float* xf, uint8_t* mask);
+bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                         int pad, int groups);
+void set_halo_xf(const float* xf);
+int64_t wgrad_halo_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                             int pad, int groups);
 void set_bn_dbias(float* p);
 bool winograd_applicable(int N, int H, int W, int Ci, int Co);
 int winograd_stat_rows(int N, int H, int W);
@@ -462,10 +468,44 @@ struct ShiftScope {
   ~ShiftScope() { pca::set_stat_shift(prev); }
 };
 
+// The BatchNorm+ReLU producing a conv's input applied on that conv's operand loads (the layer-1
+// c64 forward and the halo wgrad): x is the PRE-BN y, xf the BN's aux [mean|istd|scale|shift][C].
+bool conv_xf_supported(const Tensor& x, const Tensor& wb, int stride, int pad, int groups) {
+  if (x.dim() != 4 || wb.dim() != 4) return false;
+  const int N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  const int Cout = wb.size(0), KH = wb.size(1), KW = wb.size(2);
+  return pca::conv_c64_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) &&
+         pca::c64_version(-1) == 2 &&
+         pca::wgrad_halo_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups) >= 0;
+}
+
+struct XfScope {
+  bool fwd, on;
+  XfScope(bool f, const float* xf, uint8_t* mask) : fwd(f), on(xf != nullptr) {
+    if (!on) return;
+    if (fwd) pca::conv_c64_set_xf(xf, mask);
+    else pca::set_halo_xf(xf);
+  }
+  ~XfScope() {
+    if (!on) return;
+    if (fwd) pca::conv_c64_set_xf(nullptr, nullptr);
+    else pca::set_halo_xf(nullptr);
+  }
+};
+
+static const float* check_xf(const optional<Tensor>& xf, int C) {
+  if (!(xf.has_value() && xf->defined())) return nullptr;
+  check_f32(*xf, "xf (BN aux)");
+  TORCH_CHECK(xf->numel() >= 4 * C, "xf: BN aux [mean|istd|scale|shift][C]");
+  return ptr<float>(*xf) + 2 * C;
+}
+
 std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<Tensor>& bias,
                              int stride, int pad, int groups, bool want_stats,
                              const optional<Tensor>& stat_acc, int acc_rows,
-                             const optional<Tensor>& stat_shift) {
+                             const optional<Tensor>& stat_shift,
+                             const optional<Tensor>& xf = c10::nullopt,
+                             const optional<Tensor>& xf_mask = c10::nullopt) {
   check_bf16(x, "x");
   check_bf16(wb, "weight");
   TORCH_CHECK(x.dim() == 4 && wb.dim() == 4, "conv_fwd expects x[N,H,W,C], w[Cout,KH,KW,Cin/G]");
@@ -478,6 +518,16 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
   const int Ho = out_dim(H, KH, stride, pad), Wo = out_dim(W, KW, stride, pad);
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
   const bool has_bias0 = bias.has_value() && bias->defined();
+  const float* xfp = check_xf(xf, Cin);
+  uint8_t* xmask = nullptr;
+  if (xfp) {
+    TORCH_CHECK(conv_xf_supported(x, wb, stride, pad, groups) && !has_bias0 && want_stats,
+                "conv_fwd xf: only the layer-1 c64 forward (no bias, with statistics)");
+    TORCH_CHECK(xf_mask.has_value() && xf_mask->defined() && xf_mask->is_contiguous() &&
+                    xf_mask->scalar_type() == at::kByte && xf_mask->numel() * 8 == x.numel(),
+                "xf_mask: one bit per input element");
+    xmask = xf_mask->data_ptr<uint8_t>();
+  }
   if (g_autotune && !stream_capturing(cur_stream()) &&
       pca::conv_needs_tune(0, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, has_bias0)) {
     autotune_conv(0, N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo, [&] {
@@ -527,6 +577,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& wb, const optional<T
                                               Wo, has_bias);
   Tensor ws;
   if (wsn > 0) ws = at::empty({wsn}, x.options().dtype(at::kFloat));
+  XfScope xf_scope(true, xfp, xmask);
   pca::conv_fwd_launch(ptr<bf16>(x), ptr<bf16>(wb), optr<float>(bias), ptr<bf16>(y),
                        want_stats ? ptr<float>(stats) : nullptr, N, H, W, Cin, Cout, KH, KW,
                        stride, pad, groups, Ho, Wo, cur_stream(),
@@ -713,10 +764,15 @@ static std::vector<Tensor> g_deferred_ws;
 // defer: a split-K slab reduction is recorded (one batched launch at wgrad_flush) instead of
 // launched; only for `out` = the gradient buffer the caller flushes before anyone reads it
 Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride, int pad,
-                  int groups, const optional<Tensor>& out, bool defer) {
+                  int groups, const optional<Tensor>& out, bool defer,
+                  const optional<Tensor>& xf = c10::nullopt) {
   check_bf16(x, "x");
   check_bf16(dy, "dy");
   const int N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  const float* xfp = check_xf(xf, Cin);
+  if (xfp)
+    TORCH_CHECK(pca::wgrad_halo_ws_floats(N, H, W, Cin, dy.size(3), KH, KW, stride, pad, groups) >= 0,
+                "conv_wgrad xf: only the halo (3x3 / stride-1) wgrad transforms its X operand");
   const int Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
   TORCH_CHECK(dy.size(0) == N, "batch mismatch");
   TORCH_CHECK(out_dim(H, KH, stride, pad) == Ho && out_dim(W, KW, stride, pad) == Wo,
@@ -778,6 +834,8 @@ Tensor conv_wgrad(const Tensor& x, const Tensor& dy, int KH, int KW, int stride,
     pca::wgrad_set_trial(-1, -1);
     pca::wgrad_record_tuned(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, pick.first, pick.second);
   }
+  // (after tuning: the trials time the plain selection; the X transform forces a halo config)
+  XfScope xf_scope(false, xfp, nullptr);
   // slab workspace of the wide kernel (partial tiles, reduced into dw in a fixed order)
   const int64_t wsn = pca::conv_wgrad_ws_floats(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   Tensor ws;
@@ -2230,7 +2288,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "hipGetLastError() of this thread as a string ('' = no error); clears it");
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wb"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("groups"), py::arg("want_stats"), py::arg("stat_acc") = py::none(),
-        py::arg("acc_rows") = 0, py::arg("stat_shift") = py::none());
+        py::arg("acc_rows") = 0, py::arg("stat_shift") = py::none(), py::arg("xf") = py::none(),
+        py::arg("xf_mask") = py::none(),
+        "xf (BN aux [mean|istd|scale|shift][Cin]) + xf_mask: x is the pre-BN y and relu(BN(y)) is "
+        "applied on the loads (layer-1 c64 forward only), its 1-bit ReLU mask written to xf_mask");
+  m.def("conv_xf_supported", &conv_xf_supported, py::arg("x"), py::arg("wb"), py::arg("stride"),
+        py::arg("pad"), py::arg("groups"),
+        "can conv_fwd / conv_wgrad apply the producing BN+ReLU on their operand loads here?");
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("addend") = py::none(),
         py::arg("addend_s2c") = false);
@@ -2243,7 +2307,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "with bn_y2 / bn_aux2 (dual BN, accumulator mode) the accumulator gets [R][3][C] sums");
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("KH"), py::arg("KW"),
         py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("out"),
-        py::arg("defer") = false);
+        py::arg("defer") = false, py::arg("xf") = py::none());
   m.def("wgrad_piggy", &wgrad_piggy, "pending wgrad slab reductions ride along in the next fused BN-backward launch");
   m.def("wgrad_flush", &wgrad_flush,
         "launch every deferred weight-gradient slab reduction (one batched kernel); returns count");

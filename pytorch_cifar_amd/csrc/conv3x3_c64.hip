@@ -34,6 +34,11 @@ struct C64Geom {
   int shards;       // stats / bn_part: 0 = slab rows, >0 = sharded atomic accumulator
   int64_t* prof;    // diagnostics: per-wave shader-clock stamps (c64_set_prof), else nullptr
   const float* kshift;   // forward stats: per-channel shift K (common.h stat_shift), or nullptr
+  // forward input transform (the BatchNorm+ReLU that produced the input, applied on the halo
+  // instead of by its own pass): x = relu(a * xf[c] + xf[64 + c]) (BN scale | shift = aux rows
+  // 2-3) and its 1-bit ReLU mask of every tile interior into xf_mask (conv3x3_c64_kernel<.., XF>)
+  const float* xf;
+  uint8_t* xf_mask;
 };
 
 namespace c64 {
@@ -61,14 +66,22 @@ static_assert(BBYTES + 2 * HBYTES <= 160 * 1024, "LDS budget");
 // they idled the matrix core).
 __device__ __forceinline__ int c64_perm(int n) { return ((n >> 2) & 3) * 16 + (n >> 4) * 4 + (n & 3); }
 
-template <bool DGRAD, bool STATS, bool PROF = false>
+// XF (forward only): the input is the PRE-BatchNorm y of the previous conv; every halo piece is
+// transformed in LDS right after it lands (x = relu(y * scale + shift) with the BN apply pass's
+// exact arithmetic; the zero padding stays zero) and the tile interior's ReLU mask is written for
+// the BN backward — the BN's own apply pass (read y, write x + mask) disappears.
+template <bool DGRAD, bool STATS, bool PROF = false, bool XF = false>
 __global__ __launch_bounds__(256)
 void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
                         bf16* __restrict__ Y, float* __restrict__ stats,
                         const bf16* __restrict__ addend, const C64Geom g) {
   using namespace c64;
-  __shared__ __attribute__((aligned(16))) char smem[BBYTES + 2 * HBYTES + 1024];
+  static_assert(!(XF && DGRAD), "input transform: forward only");
+  // (XF: + the transform's scale | shift and the statistics shift K, LDS-resident: the kernel runs
+  // at the 512-register limit)
+  __shared__ __attribute__((aligned(16))) char smem[BBYTES + 2 * HBYTES + 1024 + (XF ? 768 : 0)];
   char* const Bs = smem + 2 * HBYTES;
+  float* const xfs = reinterpret_cast<float*>(smem + BBYTES + 2 * HBYTES + 1024);   // [sc|sh][64]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -138,11 +151,12 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
 
   // per-lane BatchNorm sums of channels q*16 + e, accumulated over every tile (forward; shifted
   // by kk = the consumer BN's pilot mean when given)
-  float st_s[16], st_q[16], kk[16];
+  float st_s[16], st_q[16], kk[XF ? 1 : 16];
+  float* const kks = xfs + 128;                   // XF: K in LDS [64]
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     st_s[e] = st_q[e] = 0.f;
-    kk[e] = (STATS && g.kshift) ? g.kshift[q * 16 + e] : 0.f;
+    if constexpr (!XF) kk[e] = (STATS && g.kshift) ? g.kshift[q * 16 + e] : 0.f;
   }
   // fused BN-backward reduce (dgrad): sums of dz and dz * xhat of channels q*16 + e
   const bool bnf = DGRAD && g.bn_part != nullptr;
@@ -191,7 +205,7 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
       // needed register-pair moves; the empty asm keeps the SLP vectorizer from re-pairing them
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        float d = v[e] - kk[e];
+        float d = v[e] - (XF ? kks[q * 16 + e] : kk[e]);
         asm volatile("" : "+v"(d));
         st_s[e] += d;
         st_q[e] = fmaf(d, d, st_q[e]);
@@ -228,6 +242,49 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
     *reinterpret_cast<uint4*>(dst + 8) = o1;
   };
 
+  // XF: this wave's own halo pieces of tile t (they landed: counted wait above) are transformed
+  // in place before the tile barrier publishes them, relu(y * scale + shift) with the BN apply
+  // pass's arithmetic. A lane's 16-byte pieces all hold the same logical 8-channel chunk
+  // ((lane & 7) ^ (hr & 7) with hr & 7 == lane >> 3). Pieces of padding pixels (DMA'd as zeros)
+  // stay zero; interior pixels also get their mask byte (bit v = channel c8*8 + v > 0), exactly
+  // as the BN apply pass writes it. One piece at a time with its scale / shift re-read from LDS:
+  // the kernel runs at the 512-register limit (every variant that kept more live — the pieces
+  // of a group, the coefficients across pieces, the transform inside the K loop — spilled and
+  // ran 1.5-3.5x slower than this one).
+  auto xform_tile = [&](int t, int buf) {
+    const int c8 = (lane & 7) ^ (lane >> 3);
+    const int n = t / tiles_per_img, h0 = (t - n * tiles_per_img) * ROWS;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) {
+      __builtin_amdgcn_sched_barrier(0);
+      const int i = wid + NW * k;
+      if (i >= HI) continue;                      // (wave-uniform)
+      const int jr = s_jc[k] >> 8, c = s_jc[k] & 0xff;
+      const int ih = h0 + jr - 1, iw = c - 1;
+      if (s_jc[k] < 0 || (uint32_t)ih >= (uint32_t)g.H || (uint32_t)iw >= (uint32_t)W) continue;
+      uint4* p = reinterpret_cast<uint4*>(smem + buf * HBYTES + i * 1024 + lane * 16);
+      float f[8], sc[8], sh[8];
+      unpack8(*p, f);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        sc[v] = xfs[c8 * 8 + v];
+        sh[v] = xfs[64 + c8 * 8 + v];
+      }
+      uint32_t b = 0;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        float a = f[v] * sc[v] + sh[v];
+        a = apply_act(a, ACT_RELU);
+        b |= (a > 0.f ? 1u : 0u) << v;
+        f[v] = a;
+      }
+      *p = pack8(f);
+      if (jr >= 1 && jr <= ROWS)
+        g.xf_mask[((size_t)(n * g.H + ih) * W + iw) * 8 + c8] = (uint8_t)b;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
   // (dgrad keeps the epilogue after its K loop: its fused addend / BN-reduce operands and sums
   // with a second accumulator set exceed the 512 registers)
   constexpr bool DEFER = !DGRAD;
@@ -241,6 +298,7 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
     // this tile's halo landed (every piece was issued before the previous tile's 8 deferred
     // stores, which may stay in flight)
     wait_vmcnt<STORES>();
+    if constexpr (XF) xform_tile(t, buf);
     raw_barrier();
     int64_t* pst = nullptr;
     if constexpr (PROF) {
@@ -312,6 +370,11 @@ void conv3x3_c64_kernel(const bf16* __restrict__ A, const bf16* __restrict__ Wm,
     }
   };
   f32x4 accA[4][4], accB[4][4];
+  if constexpr (XF) {
+    if (tid < 128) xfs[tid] = g.xf[tid];
+    else if (tid < 192) kks[tid - 128] = g.kshift ? g.kshift[tid - 128] : 0.f;
+    __syncthreads();
+  }
   wait_vmcnt<0>();                                // weights + first halo
   {
     int t = blockIdx.x, it = 0;
@@ -1057,6 +1120,16 @@ bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW,
 
 int conv_c64_stat_rows(int N, int H) { return c64_grid(N * H / 8); }
 
+// forward input transform of the next conv_c64_launch(es) (bindings.cpp conv_fwd xf=...):
+// scale | shift [2][64] and the ReLU-mask destination, or nullptr
+static const float* g_c64_xf = nullptr;
+static uint8_t* g_c64_xf_mask = nullptr;
+void conv_c64_set_xf(const float* xf, uint8_t* mask) {
+  g_c64_xf = xf;
+  g_c64_xf_mask = mask;
+}
+bool conv_c64_xf_active() { return g_c64_xf != nullptr; }
+
 void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const bf16* addend,
                      int N, int H, bool dgrad, hipStream_t st, const bf16* bn_y,
                      const uint8_t* bn_mask, const float* bn_aux, float* bn_part) {
@@ -1072,7 +1145,18 @@ void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const 
   g.shards = stat_shards();
   g.kshift = (!dgrad && stats) ? stat_shift() : nullptr;
   g.prof = nullptr;
+  g.xf = dgrad ? nullptr : g_c64_xf;
+  g.xf_mask = dgrad ? nullptr : g_c64_xf_mask;
   const dim3 grid(c64_grid(g.tiles)), block(256);
+  if (g.xf) {
+    if (!stats || !g.xf_mask) {
+      fprintf(stderr, "[pca] c64 input transform needs the statistics form and a mask\n");
+      abort();
+    }
+    hipLaunchKernelGGL((conv3x3_c64_kernel<false, true, false, true>), grid, block, 0, st, a, w, y,
+                       stats, addend, g);
+    return;
+  }
   const int ver = c64_version(-1);
   g.prof = g_c64_prof;
   if (g.prof) {

@@ -38,6 +38,9 @@ struct HaloGeom {
   int ablate;             // diagnostics (PCA_HALO_ABLATE): 1 = no DMA, 2 = no MFMA phase, 4 = no epilogue
   int xcd;                // XCD-aware block order (PCA_HALO_XCD=1; default: dispatch order)
   int ilv;                // next stage's DMA pieces issued between this stage's MFMAs (PCA_HALO_ILV=0: off)
+  // X input transform (X is the PRE-BatchNorm y; the conv consumed relu(BN(y)), applied on its
+  // loads — conv3x3_c64.hip XF): x = relu(y * xf[c] + xf[Cx + c]) (BN scale | shift rows), or null
+  const float* xf;
   uint32_t x_bytes, dy_bytes;
   FastDiv fd_hw, fd_w;
 };
@@ -58,19 +61,6 @@ __device__ __forceinline__ bf16x8 tr_frag_rows(const char* base, int r0, int r1,
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_rt(int n) {
-  // counted wait with a wave-uniform runtime count (n <= N)
-  if constexpr (N > 0) {
-    if (n >= N) {
-      wait_vmcnt<N>();
-      return;
-    }
-    wait_vmcnt_rt<N - 1>(n);
-  } else {
-    wait_vmcnt<0>();
-  }
-}
 
 // Compile-time stage geometry for a square W x W image (W | KP): a stage is KP output pixels =
 // RS rows of IMGS images; the halo is IMGS x (RS+2) x W2P rows (row pitch W2P = W+2 rounded up to
@@ -93,15 +83,16 @@ template <int W, int MB, int KP>
 constexpr int halo_stage_bytes() {
   return HaloShape<W, KP>::HBYTES + MB * KP * 128 + 1024;
 }
+constexpr int kHaloXfBytes = 512;   // the X transform's scale | shift of the 64-channel block
 template <int W, int MB, int KP, int ST = 3>
 constexpr bool halo_fits() {
-  return ST * halo_stage_bytes<W, MB, KP>() <= 160 * 1024;
+  return ST * halo_stage_bytes<W, MB, KP>() + kHaloXfBytes <= 160 * 1024;
 }
 
 // ST = LDS stages in the ring (ST - 1 stages in flight): the small-image shapes of the 8-GPU
 // shard (layer 4 at bs128: 96 tiles, 32 short stages per tile, DMA-latency bound with 2 stages in
 // flight) take 6 stages of 32 pixels instead of 3 of 64.
-template <int W, int MB, int WM, int WN, int KP, int TG = 9, int ST = 3>
+template <int W, int MB, int WM, int WN, int KP, int TG = 9, int ST = 3, bool XF = false>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wgrad_halo_kernel(const bf16* __restrict__ X,
                                                                   const bf16* __restrict__ DY,
                                                                   float* __restrict__ out,
@@ -127,7 +118,8 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   constexpr int W2P = SH::W2P;
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
   static_assert(32 % W == 0, "image width");
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE + (XF ? kHaloXfBytes : 0)];
+  float* const xfs = reinterpret_cast<float*>(smem + STAGES * STAGE);   // [sc | sh][64]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -217,6 +209,39 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
     for (int j = 0; j < SLOTS; ++j) issue_slot(pbase, buf, j);
   };
 
+  // X transform of this wave's own halo pieces of the stage at pbase (they landed: the counted
+  // wait), in place before the stage barrier publishes them; padding pieces (DMA'd zeros) stay
+  // zero. Arithmetic as the BN apply pass (batchnorm.hip bn_apply_rows_body).
+  auto xform_stage = [&](int pbase, int buf) {
+    const char* S = smem + buf * STAGE;
+    const int n0 = pbase / (W * W);
+    const int h0 = (pbase / W) % W;
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j) {
+      const int t = wid + NW * j;                // (wave-uniform)
+      if (t >= SH::HI) continue;
+      const int n = n0 + ((s_a[j] >> 16) & 0xff);
+      const int ih = h0 + ((s_a[j] >> 8) & 0xff) - 1;
+      const int iw = (s_a[j] & 0xff) - 1;
+      const bool ok = pbase < p_end && (s_a[j] >> 24) && n < g.N && (uint32_t)ih < (uint32_t)W &&
+                      (uint32_t)iw < (uint32_t)W;
+      if (!ok) continue;
+      const int c0 = ((s_b[j] >> 1) & 63) & ~7;  // chunk of the 64-channel block (8 channels)
+      uint4* p = reinterpret_cast<uint4*>(const_cast<char*>(S) + t * 1024 + lane * 16);
+      float f[8];
+      unpack8(*p, f);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) f[v] = apply_act(f[v] * xfs[c0 + v] + xfs[64 + c0 + v], ACT_RELU);
+      *p = pack8(f);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  if constexpr (XF) {   // this workgroup's 64 input channels' scale | shift
+    const int cb = grp * g.cin_g + cib * 64;
+    for (int i = tid; i < 128; i += NW * 64) xfs[i] = g.xf[(i < 64 ? 0 : g.Cx - 64) + cb + i];
+    __syncthreads();
+  }
+
   // ---- per-lane B-fragment addressing: halo rows of this lane's two pixel rows ----
   // B frag (tap kh,kw; columns c0..c0+15 of the 64-channel block) for the lane lives at
   //   row R = prow + kh*W2P + kw,  byte = R*128 + ((c0/8 ^ swz(R)) << 4) + L
@@ -253,6 +278,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2,
   for (int s = 0; s < STAGES - 1; ++s) issue(p_begin + s * KP, s);
   for (int kt = 0; kt < KT; ++kt) {
     wait_vmcnt<(STAGES - 2) * SLOTS>();   // stage kt landed (the STAGES - 2 after it may not have)
+    if constexpr (XF) xform_stage(p_begin + kt * KP, kt % STAGES);
     raw_barrier();
     const int pnext = p_begin + (kt + STAGES - 1) * KP, bnext = (kt + STAGES - 1) % STAGES;
     // the next stage's pieces: all at once here, or (g.ilv, wave-uniform) spread over this
@@ -545,6 +571,11 @@ static int halo_occupancy() {
 static int g_halo_override = -1;
 void set_halo_cfg(int cfg) { g_halo_override = cfg; }
 
+// X transform of the next halo wgrad launch(es) (bindings.cpp conv_wgrad xf=...), or nullptr
+static const float* g_halo_xf = nullptr;
+void set_halo_xf(const float* xf) { g_halo_xf = xf; }
+bool halo_xf_active() { return g_halo_xf != nullptr; }
+
 // Deterministic mode: every weight gradient is reduced through slab rows in a fixed order
 // (no fp32 atomics), so repeated runs are bitwise identical.
 static bool g_deterministic = false;
@@ -601,6 +632,7 @@ static bool halo_geom(HaloGeom& g, int N, int H, int W, int Cin, int Cout, int g
     return e && e[0] == '0' ? 0 : 1;
   }();
   g.ilv = ilv;
+  g.xf = g_halo_xf;
   return true;
 }
 
@@ -638,8 +670,19 @@ static void launch_halo(const bf16* x, const bf16* dy, float* dw, float* ws, Hal
                         hipStream_t st) {
   halo_plan<W, MB, WM, WN, KP, TG, ST>(g);
   dim3 grid(cdiv(g.cout_g, 64 * MB), (g.cin_g / 64) * (9 / TG), g.splits * g.groups);
-  hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP, TG, ST>), grid, dim3(WM * WN * 64), 0, st, x,
-                     dy, g.atomic ? dw : ws, g);
+  if (g.xf) {
+    // (the X transform is instantiated for the 32-wide layer-1 images only: conv_xf_supported)
+    if constexpr (W == 32) {
+      hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP, TG, ST, true>), grid,
+                         dim3(WM * WN * 64), 0, st, x, dy, g.atomic ? dw : ws, g);
+    } else {
+      fprintf(stderr, "[pca] halo wgrad X transform: W=%d not instantiated\n", W);
+      abort();
+    }
+  } else {
+    hipLaunchKernelGGL((wgrad_halo_kernel<W, MB, WM, WN, KP, TG, ST>), grid, dim3(WM * WN * 64), 0,
+                       st, x, dy, g.atomic ? dw : ws, g);
+  }
   if (g.atomic) return;
   constexpr int BM = 64 * MB, BN = TG * 64;
   HaloSlabMap mp;

@@ -2131,6 +2131,7 @@ void conv_stem_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16*
 bool conv_c64_applicable(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                          int pad, int groups);
 int conv_c64_stat_rows(int N, int H);
+bool conv_c64_xf_active();
 void conv_c64_launch(const bf16* a, const bf16* w, bf16* y, float* stats, const bf16* addend,
                      int N, int H, bool dgrad, hipStream_t st, const bf16* bn_y = nullptr,
                      const uint8_t* bn_mask = nullptr, const float* bn_aux = nullptr,
@@ -2366,6 +2367,10 @@ void conv_fwd_launch(const bf16* x, const bf16* w, const float* bias, bf16* y, f
     conv_c64_launch(x, w, y, stats, nullptr, N, H, false, st);
     return;
   }
+  if (conv_c64_xf_active()) {
+    fprintf(stderr, "[pca] conv input transform: only the c64 forward applies it\n");
+    abort();
+  }
   if (g_igemm_override < 0 && conv_stem_applicable(N, H, W, Cin, Cout, KH, KW, stride, pad, groups)) {
     conv_stem_fwd_launch(x, w, bias, y, stats, N, H, Cout, st);
     return;
@@ -2531,6 +2536,7 @@ int64_t wgrad_halo_ws_floats(int N, int H, int W, int Cin, int Cout, int KH, int
 void wgrad_halo_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int N, int H, int W,
                        int Cin, int Cout, int groups, hipStream_t st);
 void set_halo_cfg(int cfg);
+bool halo_xf_active();
 
 // wgrad autotuning: (cfg, split) per geometry; cfg >= 32 = halo config cfg-32, 16..21 = wide,
 // 0..7 = generic split-K; split -1 = occupancy-derived plan
@@ -2554,6 +2560,11 @@ static void wgrad_resolve(int N, int H, int W, int Cin, int Cout, int KH, int KW
       cfg = it->second.first;
       split = it->second.second;
     }
+  }
+  // an X input transform (the BN applied on the operand loads) exists only in the halo kernel
+  if (halo_xf_active() && cfg >= 0 && cfg < 32) {
+    cfg = -1;
+    split = -1;
   }
   g_weff_cfg = cfg;
   set_wgrad_split(split);
@@ -2596,6 +2607,10 @@ void conv_wgrad_launch(const bf16* x, const bf16* dy, float* dw, float* ws, int 
       wgrad_halo_launch(x, dy, dw, ws, N, H, W, Cin, Cout, groups, st);
       return;
     }
+  }
+  if (halo_xf_active()) {
+    fprintf(stderr, "[pca] wgrad X transform: the halo kernel does not apply to this geometry\n");
+    abort();
   }
   WgradGeom g = wgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, groups, Ho, Wo);
   const int target = 1024;

@@ -88,6 +88,20 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  // counted wait with a wave-uniform runtime count (n <= N; folds to one wait for a constant n)
+  if constexpr (N > 0) {
+    if (n >= N) {
+      wait_vmcnt<N>();
+      return;
+    }
+    wait_vmcnt_rt<N - 1>(n);
+  } else {
+    wait_vmcnt<0>();
+  }
+}
+
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();

@@ -30,8 +30,10 @@ class BasicBlock(tnn.Module):
             )
 
     def forward(self, x):
-        out = self.bn1(self.conv1(x), act="relu")
-        return self.bn2(self.conv2(out), act="relu", **shortcut_kwargs(self.shortcut, x))
+        # conv2(relu(bn1(conv1(x)))): on the layer-1 geometry conv2 applies bn1 + ReLU on its own
+        # loads (F.bn_act_conv; elsewhere the plain composition)
+        out = F.bn_act_conv(self.bn1, self.conv1(x), "relu", self.conv2)
+        return self.bn2(out, act="relu", **shortcut_kwargs(self.shortcut, x))
 
 
 class Bottleneck(tnn.Module):

@@ -11,6 +11,7 @@ from ..ops.functional import (  # noqa: F401
     adaptive_avg_pool2d,
     add_act,
     avg_pool2d,
+    bn_act_conv,
     bn_act_dwconv,
     cat,
     cat_shuffle2,

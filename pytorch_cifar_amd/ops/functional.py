@@ -1814,6 +1814,163 @@ def bn_act_dwconv(bn, x, act, conv):
     return v
 
 
+# ------------------------------------------- BN+ReLU applied inside the consumer 3x3 conv
+# conv2(relu(bn1(y1))) of a ResNet BasicBlock (reference models/resnet.py:47: the mid-block BN
+# whose output only conv2 reads) as ONE node: the BN's batch statistics are folded by one small
+# finalize launch, and relu(y1 * scale + shift) is applied by the consumer itself — the layer-1
+# c64 forward transforms each halo piece in LDS as it lands and writes the ReLU mask of its tile
+# interiors (csrc/conv3x3_c64.hip XF), the halo weight gradient transforms its X stages the same
+# way (conv_halo.hip XF). The BN output x1 is never written and never read back: the apply pass
+# (read y1, write x1 + mask: ~276 MB at bs1024) is gone. The backward is the unfused one: the c64
+# dgrad reduces the BN-backward sums from y1 + mask in its epilogue, one fused finalize+apply
+# pass produces dy1. Bitwise the unfused forward (same arithmetic, same kernels otherwise).
+# PCA_BN_CONV_FUSE=0: separate BN apply pass + plain conv (A/B).
+_BN_CONV_FUSE = os.environ.get("PCA_BN_CONV_FUSE", "0") == "1"
+_BN_CONV_USED = [0]   # fused nodes built (tests check the fused path ran)
+
+
+class _BNActConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, gamma, beta, weight, stats, cfg, acc2, pilot2):
+        C = _C()
+        bn = cfg.bn
+        aux = _bn_aux(C, bn, y, stats, cfg.training, cfg.count, cfg.pilot, zero=cfg.bacc)
+        cfg.faccs = (stats,) if isinstance(stats, StatAcc) else ()
+        w_phys = G.physical(weight)
+        if not w_phys.is_contiguous():
+            w_phys = w_phys.contiguous()
+        wb, wt = _prepped_weight(weight, 1, w_phys, True)
+        mask = torch.empty((y.numel() + 7) // 8, dtype=torch.uint8, device=y.device)
+        if acc2 is not None:
+            acc2.begin()
+            y2, _ = C.conv_fwd(y, wb, None, 1, 1, 1, True, acc2.buf, acc2.R, pilot2, xf=aux,
+                               xf_mask=mask)
+            acc2.shifted = pilot2 is not None
+            stats2 = None
+        else:
+            y2, stats2 = C.conv_fwd(y, wb, None, 1, 1, 1, True, None, 0, pilot2, xf=aux,
+                                    xf_mask=mask)
+            if pilot2 is not None and stats2.numel():
+                stats2._pca_kin = pilot2.clone()   # (as _ConvMFMA: the K these sums are of)
+        ctx.save_for_backward(y, wt, mask, aux)
+        ctx.cfg = cfg
+        ctx.weight = weight
+        if stats2 is None:
+            stats2 = torch.empty(0, device=y.device)
+        ctx.mark_non_differentiable(stats2)
+        ctx.set_materialize_grads(False)
+        return y2, stats2
+
+    @staticmethod
+    def backward(ctx, dy2, _dstats):
+        if dy2 is None:
+            return (None,) * 8
+        C = _C()
+        y, wt, mask, aux = ctx.saved_tensors
+        cfg, bn = ctx.cfg, ctx.cfg.bn
+        dy2 = dy2.contiguous()
+        H, W = y.shape[1], y.shape[2]
+        # dX1 with the BN-backward sums reduced in the dgrad epilogue (into the BN's accumulator)
+        src = _BNSrc(y, mask, aux, cfg.bacc)
+        dx1 = _dgrad_bn(C, src, dy2, wt, H, W, 1, 1, 1, None)
+        # dW2 from relu(BN(y1)) applied on the halo wgrad's X loads
+        w = ctx.weight
+        dw_ret = None
+        if w.requires_grad:
+            buf = G.grad_buffer(w) if w.is_leaf else None
+            if buf is not None:
+                piggy = _WGRAD_PIGGY and not _WGRAD_DEFER
+                if _piggy_set[0] != piggy:
+                    C.wgrad_piggy(piggy)
+                    _piggy_set[0] = piggy
+                C.conv_wgrad(y, dy2, 3, 3, 1, 1, 1, buf, defer=_WGRAD_DEFER or piggy, xf=aux)
+                if (_WGRAD_DEFER or piggy) and C.wgrad_deferred():
+                    _after_deferred_wgrad()
+                G.fire(w)
+            else:
+                dw = C.conv_wgrad(y, dy2, 3, 3, 1, 1, 1, None, xf=aux)
+                if w.is_leaf:
+                    G.accumulate(w, dw)
+                else:
+                    dw_ret = dw.permute(0, 3, 1, 2)
+
+        def gbuf(p):
+            if p is None or not p.requires_grad or not p.is_leaf:
+                return None
+            return G.grad_buffer(p)
+
+        g1, b1 = gbuf(bn.weight), gbuf(bn.bias)
+        acc = cfg.bacc if (cfg.training or bn.running_mean is None) else None
+        part = src.part if (src.part is not None and src.dx is dx1) else None
+        filled = False
+        zero1 = None
+        if acc is not None:
+            filled = part is not None and part.data_ptr() == acc.buf.data_ptr()
+            if not filled:
+                acc.ensure_clean()
+            part = None
+            acc.state = "used" if (filled or y.numel() <= _acc_max_elems()) else "clean"
+            for fa in cfg.faccs:
+                if fa.state == "used":
+                    zero1 = fa.buf          # cleared by the backward kernel's block 0
+                    fa.state = "clean"
+            cfg.faccs = ()
+        src.part = src.dx = None
+        dy, _, _, dg, db, _, _ = C.bn_backward(
+            dx1, None, mask, y, aux, bn.weight.detach() if bn.weight is not None else None,
+            None, None, None, ACT["relu"], cfg.training or bn.running_mean is None, False, g1, b1,
+            None, None, part, acc.buf if acc is not None else None, acc.R if acc is not None else 0,
+            filled, zero1, None, None, False, None)
+        ret = {}
+        for p, buf, val, slot in ((bn.weight, g1, dg, 1), (bn.bias, b1, db, 2)):
+            if p is None or not p.requires_grad:
+                continue
+            if not p.is_leaf:
+                ret[slot] = val
+            elif buf is not None:
+                G.fire(p)
+            else:
+                G.accumulate(p, val)
+        return dy, ret.get(1), ret.get(2), dw_ret, None, None, None, None
+
+
+def bn_act_conv(bn, x, act, conv):
+    """``conv(act(bn(x)))`` for a 3x3 / stride-1 conv whose input only this BN+ReLU produces:
+    one fused node where the consumer applies the BN on its loads (layer-1 c64 geometry, training
+    mode), the plain composition elsewhere. Returns what ``conv`` returns (statistics attached)."""
+    from ..nn.modules import _STATS_ATTR
+
+    Cc = x.shape[1]
+    ks, st, pd = conv.kernel_size, conv.stride, conv.padding
+    training = bn.training
+    if (not _BN_CONV_FUSE or _ref(x) or not training or act != "relu" or bn.running_mean is None
+            or not conv.training or conv.bias is not None or conv.groups != 1
+            or ks != (3, 3) or st != (1, 1) or pd != (1, 1) or conv.in_channels != Cc
+            or torch.is_autocast_enabled() or x.dim() != 4 or x.dtype != COMPUTE_DTYPE
+            or not acc_enabled(Cc, x.device)):
+        return conv(bn(x, act=act))
+    stats = getattr(x, _STATS_ATTR, None)
+    p1 = getattr(x, "_pca_stats_src", None)
+    y = to_nhwc(x)
+    if not (isinstance(stats, StatAcc) and p1 is not None and y.is_contiguous()
+            and _C().conv_xf_supported(y, G.physical(conv.weight), 1, 1, 1)):
+        return conv(bn(x, act=act))
+    N, _, H, W = x.shape
+    cfg = _BNCfg(bn, None, act, training, N * H * W)
+    cfg.pilot = link_pilot(p1, Cc, y.device)
+    cfg.bacc = stat_acc(bn, "bwd", Cc, 2, y.device)
+    acc2 = None
+    if conv.__dict__.get("_pca_acc_ok") and acc_enabled(conv.out_channels, y.device):
+        acc2 = stat_acc(conv, "fwd", conv.out_channels, 2, y.device)
+    pilot2 = conv_pilot(conv, y.device)
+    _BN_CONV_USED[0] += 1
+    out, stats2 = _BNActConv.apply(y, bn.weight, bn.bias, conv.weight, stats, cfg, acc2, pilot2)
+    v = to_nchw(out)
+    setattr(v, _STATS_ATTR, acc2 if acc2 is not None else stats2)
+    v._pca_stats_src = conv
+    return v
+
+
 # ------------------------------------------------------------------------ activations
 class _Act(torch.autograd.Function):
     @staticmethod

@@ -12,7 +12,7 @@ FLAGS="-x hip --offload-arch=gfx950 -O3 -Xarch_host -O1 -Xarch_host -g -std=c++1
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
   -I$CSRC -Wno-unused-result -Wno-unused-command-line-argument"
 objs=()
-for f in conv_mfma conv_halo conv3x3_c64 conv3x3_hx stem batchnorm; do
+for f in conv_mfma conv_halo conv3x3_c64 conv3x3_hx conv1x1_nk stem batchnorm; do
   $HIPCC $FLAGS -c "$CSRC/$f.hip" -o "$OUT/$f.o" &
   objs+=("$OUT/$f.o")
 done
