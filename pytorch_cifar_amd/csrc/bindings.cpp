@@ -1653,24 +1653,40 @@ static void check_se(const Tensor& x, const Tensor& w1, const Tensor& w2, int& R
   TORCH_CHECK(pca::se_mlp_supported(C, R), "squeeze-excite MLP: C % 8 == 0, C <= 2048, R <= 192");
 }
 
-// PCA_SE_FUSED=1: one-block-per-sample pool + MLP forward and ds + MLP-data backward (misc.hip
-// se_*_fused: 2 launches forward, 3 backward instead of 4 and 5). Off by default: measured at the
-// EfficientNet-B0 8-GPU shard (bs128) the 128 per-sample blocks serialise the MLP latency —
-// forward 314 us vs 329 us for pool + row-dot + col-dot, backward 493 us vs 380 us per step,
-// step 3.94 -> 4.07 ms.
+// One-block-per-sample pool + MLP forward and ds + MLP-data backward (misc.hip se_*_fused: 2
+// launches forward, 3 backward instead of 4 and 5), taken when the caller passes W2^T (ops/
+// functional.py does under PCA_SE_FUSED=1). Off by default there: the per-sample blocks serialise
+// the MLP latency — EfficientNet-B0 bs128 3.99 vs 3.87 ms, bs1024 9.12 vs 8.31 ms (round 6).
+static int g_se_fused = -1;   // -1: PCA_SE_FUSED decides; 0 / 1 set by se_fused_mode (A/B)
 static bool se_fused(int C, int R) {
   static const bool on = [] {
     const char* e = getenv("PCA_SE_FUSED");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
-  return on && pca::se_fused_supported(C, R);
+  return (g_se_fused < 0 ? on : g_se_fused == 1) && pca::se_fused_supported(C, R);
+}
+int se_fused_mode(int m) {
+  const int prev = g_se_fused;
+  g_se_fused = m;
+  return prev;
+}
+
+// w2t: W2 transposed [R][C] fp32 (the fused kernels read it coalesced); without it the split
+// kernels run
+static const float* check_w2t(const optional<Tensor>& w2t, int R, int C) {
+  if (!(w2t.has_value() && w2t->defined())) return nullptr;
+  check_f32(*w2t, "w2t");
+  TORCH_CHECK(w2t->is_contiguous() && w2t->numel() == (int64_t)R * C, "w2t must be [R][C]");
+  return ptr<float>(*w2t);
 }
 
 std::vector<Tensor> se_forward(const Tensor& x, const Tensor& w1, const optional<Tensor>& b1,
-                               const Tensor& w2, const optional<Tensor>& b2, int act) {
+                               const Tensor& w2, const optional<Tensor>& b2, int act,
+                               const optional<Tensor>& w2t = c10::nullopt) {
   check_bf16(x, "x");
   int R;
   check_se(x, w1, w2, R);
+  const float* w2tp = check_w2t(w2t, R, x.size(3));
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   TORCH_CHECK(act == 1 || act == 2, "squeeze-excite act: relu (1) / swish (2)");
   if (b1.has_value() && b1->defined()) TORCH_CHECK(b1->numel() == R, "b1");
@@ -1681,9 +1697,9 @@ std::vector<Tensor> se_forward(const Tensor& x, const Tensor& w1, const optional
   auto s = at::empty({N, C}, fopt);
   auto out = at::empty_like(x);
   auto st = cur_stream();
-  if (se_fused(C, R)) {
+  if (w2tp && se_fused(C, R)) {
     pca::se_fwd_fused_launch(ptr<bf16>(x), N, HW, C, R, ptr<float>(w1), optr<float>(b1),
-                             ptr<float>(w2), optr<float>(b2), act, ptr<float>(pooled),
+                             w2tp, optr<float>(b2), act, ptr<float>(pooled),
                              ptr<float>(hpre), ptr<float>(s), st);
   } else {
     pca::gap_fwd_launch(ptr<bf16>(x), N, HW, C, ptr<float>(pooled), st);
@@ -1702,11 +1718,13 @@ std::vector<Tensor> se_backward(const Tensor& dout, const Tensor& x, const Tenso
                                 const Tensor& hpre, const Tensor& s, const Tensor& w1,
                                 const Tensor& w2, int act, const optional<Tensor>& dw1_acc,
                                 const optional<Tensor>& db1_acc, const optional<Tensor>& dw2_acc,
-                                const optional<Tensor>& db2_acc, bool want_b1, bool want_b2) {
+                                const optional<Tensor>& db2_acc, bool want_b1, bool want_b2,
+                                const optional<Tensor>& w2t = c10::nullopt) {
   check_bf16(dout, "dout");
   check_bf16(x, "x");
   int R;
   check_se(x, w1, w2, R);
+  const float* w2tp = check_w2t(w2t, R, x.size(3));
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   TORCH_CHECK(dout.sizes() == x.sizes(), "dout shape");
   TORCH_CHECK(pooled.numel() == (int64_t)N * C && s.numel() == (int64_t)N * C &&
@@ -1727,9 +1745,9 @@ std::vector<Tensor> se_backward(const Tensor& dout, const Tensor& x, const Tenso
   auto dz = at::empty({N, R}, fopt);
   auto dx = at::empty_like(x);
   auto st = cur_stream();
-  if (se_fused(C, R)) {
+  if (w2tp && se_fused(C, R)) {
     pca::se_bwd_data_launch(ptr<bf16>(dout), ptr<bf16>(x), ptr<float>(s), N, HW, C, R,
-                            ptr<float>(w1), ptr<float>(w2), ptr<float>(hpre), act, ptr<float>(ds),
+                            ptr<float>(w1), w2tp, ptr<float>(hpre), act, ptr<float>(ds),
                             ptr<float>(dz), ptr<float>(dp), st);
     pca::se_mlp_bwd_param_launch(ptr<float>(ds), ptr<float>(dz), ptr<float>(hpre),
                                  ptr<float>(pooled), N, C, R, act, ptr<float>(dw1),
@@ -2398,8 +2416,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_wgrad", &stem_wgrad);
   m.def("gap_fwd", &gap_fwd);
   m.def("se_supported", &pca::se_mlp_supported, "fused squeeze-excite path for (C, R)?");
-  m.def("se_forward", &se_forward, "squeeze-excite: pool + MLP + sigmoid scale (NHWC bf16)");
-  m.def("se_backward", &se_backward);
+  m.def("se_forward", &se_forward, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
+        py::arg("b2"), py::arg("act"), py::arg("w2t") = py::none(),
+        "squeeze-excite: pool + MLP + sigmoid scale (NHWC bf16); with w2t ([R][C]) the fused kernels");
+  m.def("se_backward", &se_backward, py::arg("dout"), py::arg("x"), py::arg("pooled"),
+        py::arg("hpre"), py::arg("s"), py::arg("w1"), py::arg("w2"), py::arg("act"),
+        py::arg("dw1_acc"), py::arg("db1_acc"), py::arg("dw2_acc"), py::arg("db2_acc"),
+        py::arg("want_b1"), py::arg("want_b2"), py::arg("w2t") = py::none());
+  m.def("se_fused_mode", &se_fused_mode, py::arg("mode"),
+        "squeeze-excite kernels: 1 fused (2 + 3 launches), 0 split, -1 PCA_SE_FUSED; returns previous");
   m.def("head_fwd", &head_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("p") = 0.0,
         py::arg("rng") = py::none(),
         "fused global-average-pool [+ Philox dropout] + Linear -> (logits, pooled, keep mask)");

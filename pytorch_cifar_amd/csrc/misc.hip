@@ -1204,10 +1204,13 @@ __device__ __forceinline__ void se_pool8(const bf16* __restrict__ x, const bf16*
   __syncthreads();
 }
 
+// w2t: W2 transposed, [R][C] (the weight-prep plan's fp32 copy, ops/functional.py _dw_weight):
+// the layer-2 / dh reductions read it coalesced (W2's [C][R] rows put consecutive lanes 4R bytes
+// apart: 64 cache lines per load instruction, the fused path's bottleneck at C = 1152, R = 48)
 template <int NB>
 __global__ __launch_bounds__(256) void se_fwd_fused_kernel(
     const bf16* __restrict__ x, int N, int HW, int C, int R, const float* __restrict__ w1,
-    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    const float* __restrict__ b1, const float* __restrict__ w2t, const float* __restrict__ b2,
     int act, float* __restrict__ pooled, float* __restrict__ hpre, float* __restrict__ s) {
   extern __shared__ float sm[];
   float* vec = sm;                       // [NB][C]
@@ -1251,14 +1254,14 @@ __global__ __launch_bounds__(256) void se_fwd_fused_kernel(
       }
   }
   __syncthreads();
-  // layer 2: a thread per channel, its W2 row (R contiguous floats) against the block's h rows
+  // layer 2: a thread per channel against the block's h rows (W2^T rows: coalesced)
   for (int c = threadIdx.x; c < C; c += 256) {
     float a[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k) a[k] = b2 ? b2[c] : 0.f;
-    const float* wr = w2 + (size_t)c * R;
+#pragma unroll 8
     for (int r = 0; r < R; ++r) {
-      const float w = wr[r];
+      const float w = w2t[(size_t)r * C + c];
 #pragma unroll
       for (int k = 0; k < NB; ++k) a[k] += w * h[k * R + r];
     }
@@ -1271,7 +1274,7 @@ __global__ __launch_bounds__(256) void se_fwd_fused_kernel(
 template <int NB>
 __global__ __launch_bounds__(256) void se_bwd_data_kernel(
     const bf16* __restrict__ dout, const bf16* __restrict__ x, const float* __restrict__ s,
-    int N, int HW, int C, int R, const float* __restrict__ w1, const float* __restrict__ w2,
+    int N, int HW, int C, int R, const float* __restrict__ w1, const float* __restrict__ w2t,
     const float* __restrict__ hpre, int act, float* __restrict__ ds, float* __restrict__ dz,
     float* __restrict__ dp) {
   extern __shared__ float sm[];
@@ -1282,45 +1285,41 @@ __global__ __launch_bounds__(256) void se_bwd_data_kernel(
   const int nb = min(NB, N - n0);
   for (int k = 0; k < nb; ++k) se_pool8<NB>(x, dout, s, HW, C, n0 + k, red, vec + k * C);
   for (int i = threadIdx.x; i < nb * C; i += 256) ds[(size_t)n0 * C + i] = vec[i];
-  // dh[r] = sum_c ds[c] W2[c][r]: threads over c read their W2 rows 8 outputs at a time; the 256
-  // partials per output are folded by wave sums + LDS
+  // dh[r] = sum_c ds[c] W2[c][r] = sum_c ds[c] W2^T[r][c]: each wave owns 8 rows at a time,
+  // lanes across C (coalesced W2^T rows, 8 independent loads per channel), one wave sum per row
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int r0 = 0; r0 < R; r0 += 8) {
+  for (int r0 = wv * 8; r0 < R; r0 += 32) {
     float p[NB][8];
 #pragma unroll
     for (int k = 0; k < NB; ++k)
 #pragma unroll
       for (int j = 0; j < 8; ++j) p[k][j] = 0.f;
-    for (int c = threadIdx.x; c < C; c += 256) {
-      const float* wr = w2 + (size_t)c * R + r0;
+    for (int c = lane; c < C; c += 64) {
+      float dv[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) dv[k] = vec[k * C + c];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float w = r0 + j < R ? wr[j] : 0.f;
+        const float w = r0 + j < R ? w2t[(size_t)(r0 + j) * C + c] : 0.f;
 #pragma unroll
-        for (int k = 0; k < NB; ++k) p[k][j] += w * vec[k * C + c];
+        for (int k = 0; k < NB; ++k) p[k][j] += w * dv[k];
       }
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
+        const int r = r0 + j;
         const float v = wave_sum(p[k][j]);
-        if (lane == 0) red[(wv * NB + k) * 8 + j] = v;
+        if (lane == 0 && k < nb && r < R) {
+          const size_t o = (size_t)(n0 + k) * R + r;
+          const float d = v * se_act_grad(hpre[o], act);
+          dz[o] = d;
+          h[k * R + r] = d;
+        }
       }
-    __syncthreads();
-    if (threadIdx.x < NB * 8) {
-      const int k = threadIdx.x / 8, j = threadIdx.x % 8, r = r0 + j;
-      if (k < nb && r < R) {
-        const float v = red[(0 * NB + k) * 8 + j] + red[(1 * NB + k) * 8 + j] +
-                        red[(2 * NB + k) * 8 + j] + red[(3 * NB + k) * 8 + j];
-        const size_t o = (size_t)(n0 + k) * R + r;
-        const float d = v * se_act_grad(hpre[o], act);
-        dz[o] = d;
-        h[k * R + r] = d;
-      }
-    }
-    __syncthreads();
   }
+  __syncthreads();
   // dp[c] = sum_r W1[r][c] dz[r] (threads over c: coalesced W1 rows)
   for (int c = threadIdx.x; c < C; c += 256) {
     float a[NB];
@@ -2127,30 +2126,30 @@ bool se_fused_supported(int C, int R) {
          se_fused_lds(4, C, R) <= 64 * 1024;
 }
 void se_fwd_fused_launch(const bf16* x, int N, int HW, int C, int R, const float* w1,
-                         const float* b1, const float* w2, const float* b2, int act, float* pooled,
+                         const float* b1, const float* w2t, const float* b2, int act, float* pooled,
                          float* hpre, float* s, hipStream_t st) {
   const int NB = se_fused_nb(N);
   const dim3 grid(cdiv(N, NB)), block(256);
   const size_t lds = se_fused_lds(NB, C, R);
   if (NB == 4)
-    hipLaunchKernelGGL(se_fwd_fused_kernel<4>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2, b2, act, pooled, hpre, s);
+    hipLaunchKernelGGL(se_fwd_fused_kernel<4>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2t, b2, act, pooled, hpre, s);
   else if (NB == 2)
-    hipLaunchKernelGGL(se_fwd_fused_kernel<2>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2, b2, act, pooled, hpre, s);
+    hipLaunchKernelGGL(se_fwd_fused_kernel<2>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2t, b2, act, pooled, hpre, s);
   else
-    hipLaunchKernelGGL(se_fwd_fused_kernel<1>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2, b2, act, pooled, hpre, s);
+    hipLaunchKernelGGL(se_fwd_fused_kernel<1>, grid, block, lds, st, x, N, HW, C, R, w1, b1, w2t, b2, act, pooled, hpre, s);
 }
 void se_bwd_data_launch(const bf16* dout, const bf16* x, const float* s, int N, int HW, int C,
-                        int R, const float* w1, const float* w2, const float* hpre, int act,
+                        int R, const float* w1, const float* w2t, const float* hpre, int act,
                         float* ds, float* dz, float* dp, hipStream_t st) {
   const int NB = se_fused_nb(N);
   const dim3 grid(cdiv(N, NB)), block(256);
   const size_t lds = se_fused_lds(NB, C, R);
   if (NB == 4)
-    hipLaunchKernelGGL(se_bwd_data_kernel<4>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2, hpre, act, ds, dz, dp);
+    hipLaunchKernelGGL(se_bwd_data_kernel<4>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2t, hpre, act, ds, dz, dp);
   else if (NB == 2)
-    hipLaunchKernelGGL(se_bwd_data_kernel<2>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2, hpre, act, ds, dz, dp);
+    hipLaunchKernelGGL(se_bwd_data_kernel<2>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2t, hpre, act, ds, dz, dp);
   else
-    hipLaunchKernelGGL(se_bwd_data_kernel<1>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2, hpre, act, ds, dz, dp);
+    hipLaunchKernelGGL(se_bwd_data_kernel<1>, grid, block, lds, st, dout, x, s, N, HW, C, R, w1, w2t, hpre, act, ds, dz, dp);
 }
 
 void se_ds_launch(const bf16* dout, const bf16* x, const float* s, int N, int HW, int C, float* ds,

@@ -387,7 +387,9 @@ class WeightPrepPlan:
                 chunks += [[t, r0, min(rows, r0 + step), 3] for r0 in range(0, rows, step)]
                 continue
             if e.groups == DW_PREP:
-                desc.append([wp.data_ptr(), e.wb.data_ptr(), 0, 1, Cout, KH * KW, 1, n])
+                # [Co][K] -> [K][Co] with K = KH*KW*Cg: a depthwise weight's taps (Cg = 1), or a
+                # 1x1 weight's input channels (the squeeze-excite W2 transposed)
+                desc.append([wp.data_ptr(), e.wb.data_ptr(), 0, 1, Cout, KH * KW * Cg, 1, n])
                 chunks += [[t, c0, min(Cout, c0 + 64), 2] for c0 in range(0, Cout, 64)]
                 continue
             desc.append([wp.data_ptr(), e.wb.data_ptr(), e.wt.data_ptr(), e.groups,
@@ -2284,6 +2286,16 @@ def se_excite(x, s_logits):
     return to_nchw(_SEScale.apply(to_nhwc(x), s))
 
 
+# PCA_SE_FUSED=1: the fused squeeze-excite kernels — pool + both MLP layers in one launch (+ the
+# scale: 2 forward launches), excitation reduce + MLP data path in one (+ parameters + dx: 3
+# backward) — reading W2 transposed from the weight-prep plan. Off by default: even with the
+# coalesced W2^T reads (fused backward at C 1152 / R 48: 65.7 -> 45.8 us per call) the per-sample
+# blocks serialise pool -> MLP -> MLP latency, and the split kernels win the step, same box:
+# EfficientNet-B0 bs128 3.865-3.867 vs 3.991-3.992 ms, bs1024 8.31 vs 9.12 ms
+# (profiles/bench/r6b/ab_se_fused.log, tools/se_bench.py per shape: se_bench_r6.jsonl)
+_SE_FUSED = os.environ.get("PCA_SE_FUSED", "0") == "1"
+
+
 class _SqueezeExcite(torch.autograd.Function):
     """The whole squeeze-excite block on NHWC bf16 x (csrc/misc.hip se_*): 3 launches forward
     (pool, MLP, scale) and 4 backward (excitation reduce, MLP data, MLP parameters with fp32
@@ -2292,7 +2304,11 @@ class _SqueezeExcite(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, act):
-        out, pooled, hpre, s = _C().se_forward(x, w1, b1, w2, b2, act)
+        # W2 transposed [R][C] for the fused kernels: the weight-prep plan's fp32 copy (refreshed
+        # by its one batched launch per forward / by the fused SGD step), like a depthwise weight
+        w2t = _dw_weight(w2) if _SE_FUSED else None
+        out, pooled, hpre, s = _C().se_forward(x, w1, b1, w2, b2, act, w2t)
+        ctx.w2t = w2t
         ctx.save_for_backward(x, pooled, hpre, s, w1, w2)
         ctx.act = act
         ctx.params = (w1, b1, w2, b2)
@@ -2308,10 +2324,11 @@ class _SqueezeExcite(torch.autograd.Function):
             return G.grad_buffer(p) if (p is not None and p.requires_grad and p.is_leaf) else None
 
         bufs = [buf(p) for p in params]
+        w2t, ctx.w2t = ctx.w2t, None
         dx, dw1, db1, dw2, db2 = _C().se_backward(
             dout.contiguous(), x, pooled, hpre, s, w1s, w2s, ctx.act,
             *[b.view(-1) if b is not None else None for b in bufs],
-            params[1] is not None, params[3] is not None)
+            params[1] is not None, params[3] is not None, w2t)
         ret = []
         for p, b, g in zip(params, bufs, (dw1, db1, dw2, db2)):
             r = None
