@@ -1778,6 +1778,7 @@ struct HeadBnFuse {
   const float* aux;   // [mean | istd | ...][C]
   float* acc;         // [R][2][C]
   int R;
+  int spb;            // samples per block of the fused path: (N / spb) / R same-address atomics
 };
 
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dl,
@@ -1791,59 +1792,66 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
                                                        HeadBnFuse bf) {
   extern __shared__ float hs[];
   const int tid = threadIdx.x;
-  if ((int)blockIdx.x < N) {
-    const int n = blockIdx.x;
+  // sample blocks: one sample each, or bf.spb samples each in the fused-BN form (their sums are
+  // accumulated in registers and added once per block: at bs1024 one block per sample put 256
+  // same-address atomics on every accumulator shard)
+  const int spb = bf.acc ? bf.spb : 1;
+  const int NB = (N + spb - 1) / spb;
+  if ((int)blockIdx.x < NB) {
     // (dropout: the pooled-feature gradient passes kept features scaled by 1/(1-p))
     const float inv = 1.f / HW * (dmask ? 1.f / (1.f - p) : 1.f);
-    float d[kHeadMaxK];
-#pragma unroll
-    for (int k = 0; k < kHeadMaxK; ++k) {
-      const float v = dl[(size_t)n * K + min(k, K - 1)];
-      d[k] = k < K ? v * inv : 0.f;
-    }
-    for (int c = tid; c < C; c += 256) {
-      float t = 0.f;
-#pragma unroll
-      for (int k = 0; k < kHeadMaxK; ++k) t += d[k] * w[(size_t)min(k, K - 1) * C + c];
-      hs[c] = (dmask && !dmask[(size_t)n * C + c]) ? 0.f : t;
-    }
-    __syncthreads();
     const int CG = C >> 3;
-    bf16* dxn = dx + (size_t)n * HW * C;
-    if (!bf.acc) {
-      for (int i = tid; i < HW * CG; i += 256) {
-        const int g = i % CG;
-        *reinterpret_cast<uint4*>(dxn + (size_t)i * 8) = pack8(hs + g * 8);
-      }
-      return;
-    }
     // fused BN-backward sums: this thread's channel group g = tid % CG is fixed (256 % CG == 0)
     const int g = tid % CG;
     float mean[8], istd[8], s1[8], s2[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      mean[q] = bf.aux[g * 8 + q];
-      istd[q] = bf.aux[C + g * 8 + q];
+      mean[q] = bf.acc ? bf.aux[g * 8 + q] : 0.f;
+      istd[q] = bf.acc ? bf.aux[C + g * 8 + q] : 0.f;
       s1[q] = s2[q] = 0.f;
     }
-    const uint4 v = pack8(hs + g * 8);   // every pixel of the sample carries the same dX row
-    float f[8];
-    unpack8(v, f);
-    const size_t base = (size_t)n * HW * C;
-    for (int i = tid; i < HW * CG; i += 256) {
-      const size_t o = base + (size_t)i * 8;
-      *reinterpret_cast<uint4*>(dx + o) = v;
-      float yy[8];
-      unpack8(*reinterpret_cast<const uint4*>(bf.y + o), yy);
-      const uint8_t m = bf.mask[o >> 3];
+    const int nb0 = blockIdx.x * spb, nb1 = min(N, nb0 + spb);
+    for (int n = nb0; n < nb1; ++n) {
+      float d[kHeadMaxK];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
-        s1[q] += dz;
-        s2[q] += dz * (yy[q] - mean[q]) * istd[q];
+      for (int k = 0; k < kHeadMaxK; ++k) {
+        const float v = dl[(size_t)n * K + min(k, K - 1)];
+        d[k] = k < K ? v * inv : 0.f;
       }
+      for (int c = tid; c < C; c += 256) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < kHeadMaxK; ++k) t += d[k] * w[(size_t)min(k, K - 1) * C + c];
+        hs[c] = (dmask && !dmask[(size_t)n * C + c]) ? 0.f : t;
+      }
+      __syncthreads();
+      bf16* dxn = dx + (size_t)n * HW * C;
+      if (!bf.acc) {
+        for (int i = tid; i < HW * CG; i += 256) {
+          const int gi = i % CG;
+          *reinterpret_cast<uint4*>(dxn + (size_t)i * 8) = pack8(hs + gi * 8);
+        }
+        return;
+      }
+      const uint4 v = pack8(hs + g * 8);   // every pixel of the sample carries the same dX row
+      float f[8];
+      unpack8(v, f);
+      const size_t base = (size_t)n * HW * C;
+      for (int i = tid; i < HW * CG; i += 256) {
+        const size_t o = base + (size_t)i * 8;
+        *reinterpret_cast<uint4*>(dx + o) = v;
+        float yy[8];
+        unpack8(*reinterpret_cast<const uint4*>(bf.y + o), yy);
+        const uint8_t m = bf.mask[o >> 3];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float dz = ((m >> q) & 1u) ? f[q] : 0.f;
+          s1[q] += dz;
+          s2[q] += dz * (yy[q] - mean[q]) * istd[q];
+        }
+      }
+      __syncthreads();                   // hs (this sample's dX row) is no longer read
     }
-    __syncthreads();                     // hs (the dX row) is no longer read
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       hs[tid * 16 + q] = s1[q];
@@ -1859,14 +1867,14 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
         for (int q = 0; q < 16; ++q) a[q] += hs[j * 16 + q];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        stat_out(bf.acc, n, bf.R, 2 * C, tid * 8 + q, a[q]);
-        stat_out(bf.acc, n, bf.R, 2 * C, C + tid * 8 + q, a[8 + q]);
+        stat_out(bf.acc, blockIdx.x, bf.R, 2 * C, tid * 8 + q, a[q]);
+        stat_out(bf.acc, blockIdx.x, bf.R, 2 * C, C + tid * 8 + q, a[8 + q]);
       }
     }
     return;
   }
   // weight / bias gradient: block (j, q) = 64 columns x kHeadSamples samples, 4 sample lanes
-  const int jq = blockIdx.x - N;
+  const int jq = blockIdx.x - NB;
   const int ncb = cdiv(C, 64);
   const int j = jq % ncb, q = jq / ncb;
   const int cl = tid & 63, nl = tid >> 6;
@@ -1928,12 +1936,14 @@ void head_bwd_launch(const float* dl, const float* w, const float* pooled, int N
                      int K, bf16* dx, float* dw, float* db, float p, const uint8_t* dmask,
                      hipStream_t st, const bf16* bn_y, const uint8_t* bn_mask, const float* bn_aux,
                      float* bn_acc, int bn_R) {
-  HeadBnFuse bf{bn_y, bn_mask, bn_aux, bn_acc, bn_R};
+  // fused BN sums: at most 64 sample blocks per accumulator shard row
+  const int spb = bn_acc ? std::max(1, cdiv(N, 64 * std::max(1, bn_R))) : 1;
+  HeadBnFuse bf{bn_y, bn_mask, bn_aux, bn_acc, bn_R, spb};
   size_t lds = std::max<size_t>((size_t)C, (size_t)kHeadMaxK * 4 * 64) * sizeof(float);
   if (bn_acc) lds = std::max<size_t>(lds, 256 * 16 * sizeof(float));
   const int wblocks = cdiv(C, 64) * cdiv(N, kHeadSamples);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(N + wblocks), dim3(256), lds, st, dl, w, pooled, N,
-                     HW, C, K, dx, dw, db, p, dmask, bf);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(cdiv(N, spb) + wblocks), dim3(256), lds, st, dl, w,
+                     pooled, N, HW, C, K, dx, dw, db, p, dmask, bf);
 }
 
 void gap_fwd_launch(const bf16* x, int N, int HW, int C, float* y, hipStream_t st) {

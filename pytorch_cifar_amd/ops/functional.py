@@ -2073,6 +2073,13 @@ def global_avg_pool(x):
     return _GAP.apply(to_nhwc(x)).view(x.shape[0], x.shape[1], 1, 1)
 
 
+# PCA_HEAD_BN_FUSE_BIG=1: the head backward adds the block-tail BN's backward sums at every batch
+# size (the kernel then groups ceil(N / 64R) samples per block). Off by default: at bs1024 it does
+# not beat the separate reduce + finalize + apply (same box 6.50-6.52 vs 6.48-6.51 ms,
+# profiles/bench/r6b/ab_head_bn_fuse_big.log); the fused form is used while N / R <= 64
+_HEAD_BN_FUSE_BIG = os.environ.get("PCA_HEAD_BN_FUSE_BIG", "0") == "1"
+
+
 class _PoolLinear(torch.autograd.Function):
     """Global average pool [+ dropout] + Linear in one kernel each way (csrc/misc.hip head_*)."""
 
@@ -2085,13 +2092,13 @@ class _PoolLinear(torch.autograd.Function):
         ctx.p = p
         # the producing BN+ReLU (block tail): its backward sums are added by the head backward
         C = x.shape[-1]
-        # (one block per sample adds into the R shard rows: N / R same-address atomics each —
-        # measured: bs128 8.9 -> 14 us for the head with 11 us of reduce + finalize removed, bs1024
-        # 20 -> 74 us; so only while N / R <= 64)
+        # (sample blocks add into the R shard rows; the kernel gives each block enough samples to
+        # keep <= 64 blocks per shard row — one block per sample at bs1024 ran the head 20 -> 74 us
+        # on same-address atomics)
         ok = (bnsrc is not None and bnsrc.act == 1 and bnsrc.mask is not None and bnsrc.y2 is None
               and bnsrc.acc is not None and C % 8 == 0 and 256 % (C // 8) == 0
               and bnsrc.y.is_contiguous()
-              and x.shape[0] <= 64 * bnsrc.acc.R)
+              and (_HEAD_BN_FUSE_BIG or x.shape[0] <= 64 * bnsrc.acc.R))
         ctx.bnsrc = bnsrc if ok else None
         return logits
 

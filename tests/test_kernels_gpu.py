@@ -1057,3 +1057,33 @@ def test_conv1x1_narrow_k_dgrad(C, shape):
     assert rel_err(part[:, 0, :].sum(0), s1) < 1e-4 and rel_err(part[:, 1, :].sum(0), s2) < 1e-4
     a = bacc.view(R, 2, Cin).sum(0)
     assert rel_err(a[0], s1) < 1e-4 and rel_err(a[1], s2) < 1e-4
+
+
+@pytest.mark.parametrize("N,R", [(128, 4), (1024, 4), (1000, 2)])
+def test_fused_head_bn_backward_sums(N, R):
+    """Head backward with the block-tail BatchNorm's backward sums (sum dz, sum dz * xhat of
+    dz = dX * relu-mask) added into the [R][2][C] accumulator: the kernel gives each workgroup
+    ceil(N / 64R) samples (<= 64 same-address atomics per shard row at any batch); sums against
+    an fp32 torch reduction of the same dX, and dX itself against the plain head backward."""
+    from pytorch_cifar_amd import _native
+
+    C_ = _native.lib()
+    torch.manual_seed(4)
+    H, C, K = 4, 512, 10
+    w = torch.randn(K, C, device="cuda") * 0.05
+    pooled = torch.randn(N, C, device="cuda")
+    dl = torch.randn(N, K, device="cuda")
+    y = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
+    bits = torch.randint(0, 2, (N * H * H * C,), device="cuda", dtype=torch.uint8)
+    mask = (bits.view(-1, 8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1).to(torch.uint8)
+    aux = torch.cat([torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5,
+                     torch.zeros(2 * C, device="cuda")])
+    acc = torch.zeros(R * 2 * C + C, device="cuda")
+    dx, _, _ = C_.head_bwd(dl, w, pooled, H, H, None, None, True, 0.0, None, y, mask, aux, acc, R)
+    dx0, _, _ = C_.head_bwd(dl, w, pooled, H, H, None, None, True)
+    assert torch.equal(dx, dx0)
+    dz = dx.float().view(N, H, H, C) * bits.view(N, H, H, C).float()
+    xhat = (y.float() - aux[:C]) * aux[C:2 * C]
+    s = acc[: R * 2 * C].view(R, 2, C).sum(0)
+    assert rel_err(s[0], dz.sum((0, 1, 2))) < 1e-4
+    assert rel_err(s[1], (dz * xhat).sum((0, 1, 2))) < 1e-4
