@@ -328,34 +328,36 @@ def test_shufflenetv2_no_stock_add():
     """ShuffleNetV2's DownBlock input feeds the left depthwise conv and the right 1x1 conv3 (a
     zero-padded odd-width input at 116 / 232 channels): the unpad of conv3's dX adds the depthwise
     dgrad's gradient in the same remap pass (ops/functional.py _PadInput), so no stock add is
-    left in the step; gradients vs the autograd sum to bf16 tolerance."""
+    left in the step; gradients vs the autograd-summed path (_FUSE_GRAD=0) to bf16 tolerance.
+    The loss is a random projection of the logits: with sum() every sample and pixel got the same
+    dY, which the training-mode BatchNorm backward cancels to roundoff — the comparison was then
+    ill-conditioned (0.03-0.2 norm-relative across boxes). Accuracy against fp32:
+    test_ops_gpu.py test_zoo_matches_reference[ShuffleNetV2_1] (relative to stock bf16: the
+    stacked no-activation BatchNorms of this net leave several gradients numerically zero)."""
     from pytorch_cifar_amd.models import ShuffleNetV2
     from pytorch_cifar_amd.ops import functional as OF
 
     torch.manual_seed(0)
-    m0 = ShuffleNetV2(1).cuda().to(memory_format=torch.channels_last)
+    base = ShuffleNetV2(1)
+    m0 = copy.deepcopy(base).cuda().to(memory_format=torch.channels_last)
+    m1 = copy.deepcopy(base).cuda().to(memory_format=torch.channels_last)
     x = torch.randn(8, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    dl = torch.randn(8, 10, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1))
     with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
-        m0(x).float().sum().backward()
+        (m0(x).float() * dl).sum().backward()
         torch.cuda.synchronize()
     adds = [e.name for e in prof.events() if "CUDAFunctor_add" in e.name]
     assert not adds, adds
-    g0 = {n: p.grad.clone() for n, p in m0.named_parameters()}
-    m1 = copy.deepcopy(m0)
-    for p in m1.parameters():
-        p.grad = None
     saved = OF._FUSE_GRAD
     OF._FUSE_GRAD = False            # every branch gradient summed by autograd
     try:
-        m1(x).float().sum().backward()
+        (m1(x).float() * dl).sum().backward()
     finally:
         OF._FUSE_GRAD = saved
-    # (norm-relative, loose: _FUSE_GRAD=0 also turns every other fused gradient add into an
-    # autograd bf16 add, and the fp32-atomic BN sums differ run to run; at batch 8 the BNs amplify
-    # those roundings. Accuracy against fp32 with the junction on: test_ops_gpu.py
-    # test_zoo_matches_reference[ShuffleNetV2_1])
+    p0, p1 = dict(m0.named_parameters()), dict(m1.named_parameters())
     for n in ("layer2.0.conv3.weight", "layer2.0.conv1.weight", "layer1.2.conv3.weight",
               "conv1.weight"):
-        a, b = g0[n].float(), m1.state_dict(keep_vars=True)[n].grad.float()
+        a, b = p0[n].grad.float(), p1[n].grad.float()
         err = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
-        assert err < 6e-2, (n, err)
+        print(f"{n}: fused vs autograd {err:.5f}")
+        assert err < 4e-2, (n, err)   # (measured 0.012-0.015)
