@@ -1617,11 +1617,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       float a[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) a[q] = b[q];
-      for (int k = 0; k < S; ++k) {
-        const float4 v0 = *reinterpret_cast<const float4*>(ws + k * plane + o);
-        const float4 v1 = *reinterpret_cast<const float4*>(ws + k * plane + o + 4);
-        a[0] += v0.x; a[1] += v0.y; a[2] += v0.z; a[3] += v0.w;
-        a[4] += v1.x; a[5] += v1.y; a[6] += v1.z; a[7] += v1.w;
+      // up to 8 partial planes' loads in flight before the first add (a runtime-S loop issued
+      // them one round trip at a time); the adds keep the plane order, so the sum is unchanged
+      for (int k0 = 0; k0 < S; k0 += 8) {
+        float4 v0[8], v1[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k0 + k < S) {
+            v0[k] = *reinterpret_cast<const float4*>(ws + (k0 + k) * plane + o);
+            v1[k] = *reinterpret_cast<const float4*>(ws + (k0 + k) * plane + o + 4);
+          }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k0 + k < S) {
+            a[0] += v0[k].x; a[1] += v0[k].y; a[2] += v0[k].z; a[3] += v0[k].w;
+            a[4] += v1[k].x; a[5] += v1[k].y; a[6] += v1[k].z; a[7] += v1[k].w;
+          }
       }
       if constexpr (STATS) {
 #pragma unroll
